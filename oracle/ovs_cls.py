@@ -1,0 +1,245 @@
+"""OVS userspace-classifier semantics over Antrea NetworkPolicy flows (TEST INFRASTRUCTURE ONLY).
+
+Restates (third-party, not vendored in the reference; OVS 2.17.7 per build/images/deps/ovs-version):
+* `lib/classifier.c: classifier_lookup__` -- highest-priority hard match; soft (conjunction-only)
+  matches strictly above it; conjunctions evaluated level by level from the highest soft priority
+  down; a completed conjunction `id` triggers a second lookup with `conj_id=id` that ignores soft
+  matches, whose result is the table's verdict.
+* OpenFlow table-miss behaviour of Antrea's policy tables = "next table"
+  (`pkg/agent/openflow/pipeline.go:2714-2739`).
+* The policy stages of `docs/design/ovs-pipeline.md:1159-1330 (egress), 1633-1812 (ingress)`:
+  {AntreaPolicy,,Default}{Egress,Ingress}Rule -> {Egress,Ingress}Metric, plus the
+  IngressSecurityClassifier bypass of `pipeline.go:2144-2182`.
+
+Tie policy (OVS-implementation-defined, `docs/antrea-network-policy.md:1966-1980`): when several
+conjunctions complete at the same priority the LOWEST conj id wins and the TIE flag is raised.
+
+Pure Python: for the small and medium cases of the test-suite. `ovs_cls.c` is the C twin.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from typing import Dict, List, Optional
+
+from .flowtext import parse_flow
+
+# verdict action codes (must equal include/gpc.h GPC_ACT_*)
+ACT_NONE, ACT_NO_MATCH, ACT_ALLOW, ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP, ACT_BYPASS = range(7)
+FLAG_PASS, FLAG_TIE = 1, 2
+# packet destination classes seen by IngressSecurityClassifier (fields.go PktDestinationField)
+DEST_POD, DEST_GATEWAY, DEST_TUNNEL, DEST_UPLINK = 0, 1, 2, 3
+CT_NEW, CT_EST, CT_REL, CT_RPL, CT_TRK = 1, 2, 4, 8, 32
+
+EGRESS = ("AntreaPolicyEgressRule", "EgressRule", "EgressDefaultRule", "EgressMetric")
+INGRESS = ("AntreaPolicyIngressRule", "IngressRule", "IngressDefaultRule", "IngressMetric")
+
+
+def _field(pkt: dict, st: dict, name: str):
+    """Packet/pipeline value of an OpenFlow field."""
+    if name == "dl_type":
+        return pkt.get("eth", 0x0800)
+    if name == "nw_proto":
+        return pkt["proto"]
+    if name in ("nw_src", "ipv6_src"):
+        return pkt["src"] if (pkt.get("eth", 0x0800) == 0x0800) == (name == "nw_src") else None
+    if name in ("nw_dst", "ipv6_dst"):
+        return pkt["dst"] if (pkt.get("eth", 0x0800) == 0x0800) == (name == "nw_dst") else None
+    if name in ("ct_nw_src", "ct_ipv6_src"):
+        return pkt.get("ct_src", pkt["src"])
+    if name in ("ct_nw_dst", "ct_ipv6_dst"):
+        return pkt.get("ct_dst", pkt["dst"])
+    if name == "tp_src":
+        return pkt.get("sport", 0) if pkt["proto"] in (6, 17, 132) else None
+    if name == "tp_dst":
+        return pkt.get("dport", 0) if pkt["proto"] in (6, 17, 132) else None
+    if name == "icmp_type":  # OVS keeps ICMP type/code in tp_src/tp_dst
+        return pkt.get("sport", 0) if pkt["proto"] in (1, 58) else None
+    if name == "icmp_code":
+        return pkt.get("dport", 0) if pkt["proto"] in (1, 58) else None
+    if name == "in_port":
+        return pkt.get("in_port", 0)
+    if name == "tun_id":
+        return pkt.get("tun_id", 0)
+    if name == "ct_state":
+        return pkt.get("ct_state", CT_NEW | CT_TRK)
+    if name == "conj_id":
+        return st["conj_id"]
+    if name == "ct_label":
+        return st["ct_label"]
+    if name == "reg1":
+        return pkt.get("out_port", 0)
+    if name == "reg7":
+        return pkt.get("svc_group", 0)
+    if name.startswith("reg"):
+        return st["regs"].get(int(name[3:]), 0)
+    raise KeyError(name)
+
+
+def flow_matches(flow: dict, pkt: dict, st: dict) -> bool:
+    for name, (v, m) in flow["match"].items():
+        pv = _field(pkt, st, name)
+        if pv is None:
+            return False
+        if m is None:
+            if pv != v:
+                return False
+        elif (pv & m) != (v & m):
+            return False
+    return True
+
+
+def _is_soft(flow) -> bool:
+    acts = flow["actions"]
+    return bool(acts) and all(a[0] == "conjunction" for a in acts)
+
+
+def classifier_lookup(flows: List[dict], pkt: dict, st: dict, allow_conj=True):
+    """Returns (flow|None, tie:bool)."""
+    hard, hard_pri, tie = None, -1, False
+    soft = []
+    for f in flows:
+        if not flow_matches(f, pkt, st):
+            continue
+        if _is_soft(f):
+            if allow_conj:
+                soft.append(f)
+        elif f["priority"] > hard_pri:
+            hard, hard_pri, tie = f, f["priority"], False
+        elif f["priority"] == hard_pri:
+            tie = True
+    if not allow_conj:
+        return hard, tie
+    soft = [f for f in soft if f["priority"] > hard_pri]
+    for level in sorted({f["priority"] for f in soft}, reverse=True):
+        clauses: Dict[int, set] = defaultdict(set)
+        ncl: Dict[int, int] = {}
+        for f in soft:
+            if f["priority"] != level:
+                continue
+            for a in f["actions"]:
+                clauses[a[1]].add(a[2])
+                ncl[a[1]] = a[3]
+        done = sorted(cid for cid, ks in clauses.items() if ks >= set(range(1, ncl[cid] + 1)))
+        for cid in done:
+            st2 = dict(st, conj_id=cid)
+            r, _ = classifier_lookup(flows, pkt, st2, allow_conj=False)
+            if r is not None:
+                return r, len(done) > 1
+    return hard, tie
+
+
+class Pipeline:
+    """The two policy stages over a flow dump (list of flow-text lines)."""
+
+    def __init__(self, flow_lines: List[str], tiers: Optional[Dict[int, int]] = None):
+        self.tables: Dict[str, List[dict]] = defaultdict(list)
+        for line in flow_lines:
+            f = parse_flow(line)
+            f["_pk"] = 0
+            f["_by"] = 0
+            self.tables[f["table"]].append(f)
+        self.tiers = tiers or {}
+
+    def _stage(self, tables, pkt, st):
+        t1, t2, t3, metric = tables
+        order = [t1, t2, t3, metric]
+        t, flags, action, conj, tindex = t1, 0, ACT_NO_MATCH, 0, 0
+        while t != metric:
+            f, tie = classifier_lookup(self.tables.get(t, []), pkt, st)
+            if f is None:
+                t = order[order.index(t) + 1]
+                continue
+            goto = None
+            deny = False
+            reject = False
+            for a in f["actions"]:
+                if a[0] == "set_reg":
+                    _, r, v, m = a
+                    m = 0xFFFFFFFF if m is None else m
+                    st["regs"][r] = (st["regs"].get(r, 0) & ~m) | (v & m)
+                    if r == 0 and v & m & 0x400:
+                        deny = True
+                    if r == 0 and m == 0xFE000000 and (v >> 25) & 4:
+                        reject = True
+                elif a[0] == "ct_commit":
+                    for v, m in a[2]:
+                        st["ct_label"] = (st["ct_label"] & ~m) | (v & m)
+                    goto = a[1]
+                elif a[0] == "goto_table":
+                    goto = a[1]
+                elif a[0] == "group":
+                    goto = "group"
+            cid = f["match"].get("conj_id", (0, None))[0]
+            if tie:
+                flags |= FLAG_TIE
+            tindex = order.index(t) + 1
+            if cid:
+                conj = cid
+                if deny:
+                    action = ACT_REJECT if reject else ACT_DROP
+                    goto = metric
+                elif goto in (t2,) or (goto == "group" and not deny and st["regs"].get(0, 0) & 0x1800 == 0x1800):
+                    flags |= FLAG_PASS
+                    t = t2
+                    continue
+                else:
+                    action = ACT_ALLOW
+                    goto = metric
+            else:
+                if goto is None:
+                    return ACT_ISOLATION_DROP, 0, tindex, flags, None
+                action = ACT_BYPASS
+                conj = 0
+                goto = metric
+            t = goto
+        # metric table: allow/deny counters (pipeline.go:1604-1670)
+        mf, _ = classifier_lookup(self.tables.get(metric, []), pkt, st, allow_conj=False)
+        if mf is not None:
+            mf["_pk"] += 1
+            mf["_by"] += pkt.get("len", 0)
+        if action == ACT_NO_MATCH:
+            tindex = 0
+        return action, conj, tindex, flags, mf
+
+    def classify(self, pkt: dict):
+        """Returns ((e_act, e_conj, e_table, e_tier, e_flags), (i_act, ...))."""
+        st = {"regs": {}, "ct_label": 0, "conj_id": 0}
+        ct = pkt.get("ct_state", CT_NEW | CT_TRK)
+        e = self._stage(EGRESS, pkt, st)
+        ev = (e[0], e[1], e[2], self.tiers.get(e[1], 0) if e[1] else 0, e[3])
+        if e[0] in (ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP):
+            return ev, (ACT_NONE, 0, 0, 0, 0)
+        st = {"regs": {}, "ct_label": st["ct_label"], "conj_id": 0}
+        if pkt.get("dest", DEST_POD) != DEST_POD:
+            # IngressSecurityClassifier: to gateway / tunnel / uplink -> IngressMetric
+            return ev, (ACT_BYPASS, 0, 0, 0, 0)
+        i = self._stage(INGRESS, pkt, st)
+        iv = (i[0], i[1], i[2], self.tiers.get(i[1], 0) if i[1] else 0, i[3])
+        return ev, iv
+
+    def metric_dumps(self):
+        """ovs-ofctl dump of the two metric tables with counters (for NetworkPolicyMetrics)."""
+        out = {}
+        for name in ("EgressMetric", "IngressMetric"):
+            lines = []
+            for f in self.tables.get(name, []):
+                lines.append("table=%s, n_packets=%d, n_bytes=%d, %s" % (
+                    name, f["_pk"], f["_by"], _match_text(f)))
+            out[name] = lines
+        return out
+
+
+def _match_text(f):
+    from .compiler import Flow, match_to_string  # re-emit the match the way utils.go does
+    fl = Flow(f["table"], f["priority"], {}, [])
+    m = {}
+    for k, (v, mk) in f["match"].items():
+        if k == "dl_type":
+            m["dl_type"] = v
+        elif k == "nw_proto":
+            m["nw_proto"] = v
+        else:
+            m[k] = (v, mk)
+    fl.match = m
+    acts = " actions=drop" if not f["actions"] or f["actions"][0][0] == "drop" else " actions=goto_table:x"
+    return match_to_string(fl) + acts
