@@ -1,0 +1,473 @@
+// Device classification image + per-packet evaluation (shared by the gfx950 kernel and the
+// test-only host emulation in tests/csrc). See DESIGN.md §3 for the algorithm.
+//
+// Semantics restated (per rule table, per packet): OVS classifier_lookup__ with conjunctive
+// matches (lib/classifier.c, OVS 2.17.7): H = best hard (non-conjunctive) flow; a conjunction can
+// win only at a priority strictly above H; the highest completed conjunction (lowest conj id on a
+// tie) wins, and its conj_id action flow (or H, if H has a higher priority) is the table verdict.
+// Antrea's compile invariant -- every clause flow of conjunction `id` has the rule's priority
+// (network_policy.go:866-889) -- lets the image store one record per conjunction ("rule") whose
+// clauses are OR-lists of match atoms, instead of per-priority flow lists.
+//
+// Image = one uint32 blob. Per rule table: RuleRec[] sorted by (priority desc, hard first, id asc),
+// clause segments (sorted interval lists, point-hash references, generic masked boxes) and a
+// driver index per clause 0/1: bucket -> ranks, so a packet only visits rules that can match.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define GPC_HD __host__ __device__ __forceinline__
+#else
+#define GPC_HD inline
+#endif
+
+namespace gpc {
+
+// Packet axes (all 32-bit; IPv4 image).
+enum Axis : uint8_t {
+  AX_SRC = 0,    // nw_src
+  AX_DST = 1,    // nw_dst
+  AX_CTSRC = 2,  // ct_nw_src
+  AX_CTDST = 3,  // ct_nw_dst
+  AX_INPORT = 4, // in_port
+  AX_REG1 = 5,   // reg1 TargetOFPortField
+  AX_REG7 = 6,   // reg7 ServiceGroupIDField
+  AX_TUN = 7,    // tun_id (label identity)
+  AX_L4D = 8,    // nw_proto << 16 | tp_dst   (ICMP: code)
+  AX_L4S = 9,    // nw_proto << 16 | tp_src   (ICMP: type)
+  AX_CTST = 10,  // ct_state bits
+  AX_N = 11
+};
+
+enum SegKind : uint8_t { SEG_IVAL = 0, SEG_HASH = 1, SEG_BOX = 2, SEG_ALWAYS = 3 };
+enum RuleKind : uint8_t { RK_SOFT = 0, RK_HARD = 1 };
+// What the table walk does with a rule's verdict.
+enum RVerdict : uint8_t { RV_MISS = 1, RV_ALLOW = 2, RV_DROP = 3, RV_REJECT = 4, RV_ISO_DROP = 5, RV_BYPASS = 6, RV_PASS = 7 };
+enum RuleFlags : uint8_t { RF_ACT = 1, RF_COUNTED = 2 };
+
+constexpr int kMaxClauses = 3;
+constexpr int kIdxPerClause = 6;  // sub-indexes (axis, band) per driver clause
+constexpr uint32_t kNoIdx = 0xffffffffu;
+constexpr uint32_t kBuckets = 65536;
+
+struct RuleRec {  // 32 B
+  uint32_t conj_id;
+  uint16_t priority;
+  uint16_t act_priority;
+  uint8_t kind, n_clauses, verdict, flags;
+  uint8_t tier, nseg0, nseg1, nseg2;
+  uint32_t slot;
+  uint32_t seg_begin;
+  uint32_t reserved[2];
+};
+
+struct SegRec {  // 16 B
+  uint8_t axis, kind, clause, reserved;
+  uint32_t n;
+  uint32_t off;  // IVAL: word offset of n (lo,hi) pairs ; BOX: word offset of n BoxRec
+  uint32_t reserved2;
+};
+
+struct BoxRec {  // 32 B: AND of up to 3 masked terms
+  uint32_t val[3];
+  uint32_t mask[3];
+  uint8_t axis[3];
+  uint8_t nterms;
+  uint32_t reserved;
+};
+
+struct SubIdx {  // one (axis, band) bucket index of a driver clause
+  uint8_t axis, band, reserved[2];
+  uint32_t off;  // word offset of kBuckets+1 offsets (relative to entries base)
+  uint32_t ent;  // word offset of the rank entries
+};
+
+struct TableHdr {
+  uint32_t n_rules, n_hard;
+  uint32_t rules_off;  // RuleRec array (word offset)
+  uint32_t hard_off;   // ranks of hard pseudo-rules (ascending)
+  uint32_t seg_off;    // SegRec array
+  uint32_t always_off[2], always_n[2];
+  uint32_t n_idx[2];
+  SubIdx idx[2][kIdxPerClause];
+};
+
+struct ImageHdr {
+  TableHdr t[6];        // AP egress, egress, egress default, AP ingress, ingress, ingress default
+  uint32_t hash_off;    // point hash: 2^hash_log2 buckets x 8 uint64 keys
+  uint32_t hash_log2;
+  uint32_t n_slots;
+  uint32_t reserved;
+};
+
+struct Pkt {
+  uint32_t ax[AX_N];
+};
+
+struct TableResult {
+  uint8_t verdict;  // RVerdict
+  uint8_t tie;
+  uint8_t tier;
+  uint8_t counted;
+  uint32_t conj;
+  uint32_t slot;
+};
+
+// ------------------------------------------------------------------------------ hashing / buckets
+GPC_HD uint32_t mix32(uint32_t x) {  // murmur3 finalizer
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+GPC_HD uint64_t mix64(uint64_t x) {  // splitmix64 finalizer
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+GPC_HD uint32_t proto_class(uint32_t proto) {
+  switch (proto) {
+    case 6: return 1;
+    case 17: return 2;
+    case 132: return 3;
+    case 1: return 4;
+    case 2: return 5;
+    case 58: return 6;
+    default: return 0;
+  }
+}
+// Bands: IP axes 0 = prefix len 0..16 (top-16 bits), 1 = 17..24 (hash of top-24), 2 = 25..32
+// (hash of the address); exact axes (in_port, reg1, reg7, tun) band 0 = hash of the value;
+// L4 axes band 0 = proto class x port/8.
+GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t v) {
+  if (axis <= AX_CTDST) {
+    if (band == 0) return v >> 16;
+    if (band == 1) return mix32(v >> 8) & 0xffffu;
+    return mix32(v) & 0xffffu;
+  }
+  if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
+  return mix32(v) & 0xffffu;
+}
+GPC_HD uint64_t point_key(uint32_t table, uint32_t clause, uint32_t axis, uint32_t rank, uint32_t v) {
+  uint32_t hi = (table << 29) | (clause << 27) | (axis << 23) | (rank & 0x7fffffu);
+  return (uint64_t(hi) << 32) | v;
+}
+GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
+GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0x9e3779b97f4a7c15ull) >> 32) & mask; }
+
+// ------------------------------------------------------------------------------ evaluation
+#ifdef GPC_EMU_STATS  // test-only instrumentation (tests/csrc/emu.cpp); never defined in the product build
+extern "C" unsigned long long gpc_emu_stats[8];
+extern "C" void gpc_emu_touch(const void* p, unsigned bytes);
+#define GPC_STAT(i, v) (gpc_emu_stats[i] += (v))
+#define GPC_TOUCH(p, n) gpc_emu_touch((p), (n))
+#else
+#define GPC_STAT(i, v) ((void)0)
+#define GPC_TOUCH(p, n) ((void)0)
+#endif
+
+struct Img {
+  const uint32_t* blob;
+  const ImageHdr* hdr;
+};
+
+GPC_HD bool hash_contains(const Img& im, uint64_t key) {
+  const uint64_t* tab = reinterpret_cast<const uint64_t*>(im.blob + im.hdr->hash_off);
+  uint32_t mask = (1u << im.hdr->hash_log2) - 1;
+  const uint64_t* b = tab + size_t(hash_b1(key, mask)) * 8;
+  GPC_TOUCH(b, 64);
+  bool hit = false;
+#pragma unroll
+  for (int i = 0; i < 8; i++) hit |= b[i] == key;
+  if (hit) return true;
+  b = tab + size_t(hash_b2(key, mask)) * 8;
+  GPC_TOUCH(b, 64);
+#pragma unroll
+  for (int i = 0; i < 8; i++) hit |= b[i] == key;
+  return hit;
+}
+
+GPC_HD bool seg_match(const Img& im, uint32_t table, uint32_t rank, const SegRec& s, const Pkt& p) {
+  switch (s.kind) {
+    case SEG_ALWAYS:
+      return true;
+    case SEG_IVAL: {
+      const uint32_t v = p.ax[s.axis];
+      const uint32_t* iv = im.blob + s.off;
+      uint32_t n = s.n;
+      if (n <= 8) {
+        for (uint32_t i = 0; i < n; i++) {
+          GPC_TOUCH(iv + 2 * i, 8);
+          if (v < iv[2 * i]) return false;
+          if (v <= iv[2 * i + 1]) return true;
+        }
+        return false;
+      }
+      uint32_t lo = 0, hi = n;  // first interval with lo > v
+      while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        GPC_TOUCH(iv + 2 * mid, 8);
+        if (iv[2 * mid] <= v) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo > 0 && v <= iv[2 * (lo - 1) + 1];
+    }
+    case SEG_HASH:
+      return hash_contains(im, point_key(table, s.clause, s.axis, rank, p.ax[s.axis]));
+    case SEG_BOX: {
+      const BoxRec* bx = reinterpret_cast<const BoxRec*>(im.blob + s.off);
+      for (uint32_t i = 0; i < s.n; i++) {
+        const BoxRec& b = bx[i];
+        GPC_TOUCH(&b, sizeof(BoxRec));
+        bool ok = true;
+        for (int t = 0; t < b.nterms; t++) ok &= (p.ax[b.axis[t]] & b.mask[t]) == b.val[t];
+        if (ok) return true;
+      }
+      return false;
+    }
+  }
+  return false;
+}
+
+GPC_HD bool rule_match(const Img& im, uint32_t table, const TableHdr& th, uint32_t rank, const RuleRec& r, const Pkt& p) {
+  const SegRec* segs = reinterpret_cast<const SegRec*>(im.blob + th.seg_off) + r.seg_begin;
+  uint32_t nseg[3] = {r.nseg0, r.nseg1, r.nseg2};
+  uint32_t s = 0;
+  for (uint32_t k = 0; k < r.n_clauses; k++) {
+    bool ok = false;
+    for (uint32_t j = 0; j < nseg[k] && !ok; j++) {
+      GPC_TOUCH(&segs[s + j], sizeof(SegRec));
+      ok = seg_match(im, table, rank, segs[s + j], p);
+    }
+    if (!ok) return false;
+    s += nseg[k];
+  }
+  return true;
+}
+
+// One rule table (table = 1..6).
+GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
+  const TableHdr& th = im.hdr->t[table - 1];
+  const RuleRec* rules = reinterpret_cast<const RuleRec*>(im.blob + th.rules_off);
+  TableResult res;
+  res.verdict = RV_MISS;
+  res.tie = 0;
+  res.tier = 0;
+  res.counted = 0;
+  res.conj = 0;
+  res.slot = 0;
+  // --- hard pseudo-rules (few): best hard match H
+  uint32_t rH = th.n_rules;
+  uint16_t hprio = 0;
+  uint8_t hverdict = RV_MISS;
+  const uint32_t* hard = im.blob + th.hard_off;
+  for (uint32_t h = 0; h < th.n_hard; h++) {
+    GPC_TOUCH(&hard[h], 4);
+    uint32_t rank = hard[h];
+    GPC_TOUCH(&rules[rank], sizeof(RuleRec));
+    RuleRec r = rules[rank];
+    if (rH != th.n_rules) {  // tie among hard flows of equal priority and different verdicts
+      if (r.priority != hprio) break;
+      if (r.verdict != hverdict && rule_match(im, table, th, rank, r, p)) res.tie = 1;
+      continue;
+    }
+    if (rule_match(im, table, th, rank, r, p)) {
+      rH = rank;
+      hprio = r.priority;
+      hverdict = r.verdict;
+    }
+  }
+  // --- driver clause: the one with fewer candidate ranks
+  uint32_t cnt[2] = {0, 0};
+  uint32_t bk[2][kIdxPerClause];
+  const uint32_t* offs[2][kIdxPerClause];
+  for (int k = 0; k < 2; k++) {
+    cnt[k] = th.always_n[k];
+    for (uint32_t i = 0; i < th.n_idx[k]; i++) {
+      const SubIdx& si = th.idx[k][i];
+      uint32_t b = bucket_of(si.axis, si.band, p.ax[si.axis]);
+      const uint32_t* o = im.blob + si.off;
+      bk[k][i] = b;
+      offs[k][i] = o;
+      GPC_TOUCH(o + b, 8);
+      cnt[k] += o[b + 1] - o[b];
+    }
+  }
+  int d = cnt[1] < cnt[0] ? 1 : 0;
+  GPC_STAT(0, 1);
+  GPC_STAT(1, cnt[d]);
+  GPC_STAT(2, cnt[1 - d]);
+  if (th.n_idx[0] == 0 && th.always_n[0] == 0 && th.n_idx[1] == 0 && th.always_n[1] == 0) d = -1;  // no soft rules
+  // k-way merge of the driver lists (ascending rank = descending priority)
+  const uint32_t* cur[kIdxPerClause + 1];
+  const uint32_t* end[kIdxPerClause + 1];
+  int nl = 0;
+  if (d >= 0) {
+    if (th.always_n[d]) {
+      cur[nl] = im.blob + th.always_off[d];
+      end[nl] = cur[nl] + th.always_n[d];
+      nl++;
+    }
+    for (uint32_t i = 0; i < th.n_idx[d]; i++) {
+      const uint32_t* ent = im.blob + th.idx[d][i].ent;
+      uint32_t b = bk[d][i];
+      cur[nl] = ent + offs[d][i][b];
+      end[nl] = ent + offs[d][i][b + 1];
+      if (cur[nl] != end[nl]) nl++;
+    }
+  }
+  uint32_t last = 0xffffffffu;
+  int have = 0;            // result found
+  uint32_t level = 0xffffffffu;
+  uint32_t level_done = 0; // completed conjunctions at the current level
+  uint32_t win = 0;        // winner rank (soft) when have == 1 and !use_h
+  int use_h = 0;
+  while (true) {
+    uint32_t best = 0xffffffffu;
+    int bi = -1;
+    for (int l = 0; l < nl; l++) {
+      if (cur[l] < end[l]) {
+        GPC_TOUCH(cur[l], 4);
+        uint32_t r = *cur[l];
+        if (r < best) {
+          best = r;
+          bi = l;
+        }
+      }
+    }
+    if (bi < 0 || best >= rH) break;
+    cur[bi]++;
+    if (best == last) continue;
+    last = best;
+    GPC_TOUCH(&rules[best], sizeof(RuleRec));
+    RuleRec r = rules[best];
+    if (r.priority != level) {
+      if (have) break;  // winning level finished
+      level = r.priority;
+      level_done = 0;
+    }
+    GPC_STAT(3, 1);
+    if (!rule_match(im, table, th, best, r, p)) continue;
+    level_done++;
+    if (have) {  // a second completion at the winning level
+      res.tie = 1;
+      break;
+    }
+    if (r.flags & RF_ACT) {
+      have = 1;
+      use_h = (rH != th.n_rules && hprio > r.act_priority) ? 1 : 0;
+      win = best;
+    } else if (rH != th.n_rules) {
+      have = 1;
+      use_h = 1;
+    }
+  }
+  if (have && !use_h) {
+    RuleRec r = rules[win];
+    res.verdict = r.verdict;
+    res.conj = r.conj_id;
+    res.tier = r.tier;
+    res.counted = (r.flags & RF_COUNTED) ? 1 : 0;
+    res.slot = r.slot;
+    if (level_done > 1) res.tie = 1;
+    return res;
+  }
+  if (rH != th.n_rules) {
+    res.verdict = hverdict;
+    if (have && level_done > 1) res.tie = 1;
+  }
+  return res;
+}
+
+// Verdict word layout (gpc_verdict): conj_id | action | table | tier | flags.
+struct VerdictOut {
+  uint32_t conj;
+  uint32_t packed;  // action | table << 8 | tier << 16 | flags << 24
+};
+
+GPC_HD uint32_t pack_verdict(uint32_t action, uint32_t table, uint32_t tier, uint32_t flags) {
+  return action | (table << 8) | (tier << 16) | (flags << 24);
+}
+
+// One policy stage: tables base+1..base+3 (base 0 egress, 3 ingress).
+GPC_HD VerdictOut eval_stage(const Img& im, uint32_t base, const Pkt& p, uint32_t* slot_out, int* counted_out) {
+  uint32_t flags = 0;
+  uint32_t conj = 0, tier = 0;  // reg5/reg6 after a Pass keeps the Pass rule's conj id
+  *counted_out = 0;
+  for (uint32_t i = 0; i < 3; i++) {
+    TableResult r = eval_table(im, base + 1 + i, p);
+    if (r.tie) flags |= 2;
+    if (r.verdict == RV_MISS) continue;
+    if (r.verdict == RV_PASS) {  // Pass: goto {Egress,Ingress}Rule (pipeline.go:1861-1886)
+      flags |= 1;
+      conj = r.conj;
+      tier = r.tier;
+      continue;
+    }
+    VerdictOut o;
+    uint32_t act = r.verdict;  // RV_* values 2..6 equal GPC_ACT_*
+    if (r.verdict != RV_ISO_DROP && r.verdict != RV_BYPASS) {
+      conj = r.conj;
+      tier = r.tier;
+    }
+    o.conj = conj;
+    o.packed = pack_verdict(act, i + 1, tier, flags);
+    *slot_out = r.slot;
+    *counted_out = r.counted && (act == RV_ALLOW || act == RV_DROP || act == RV_REJECT);
+    return o;
+  }
+  VerdictOut o;
+  o.conj = conj;
+  o.packed = pack_verdict(1 /*NO_MATCH*/, 0, tier, flags);
+  return o;
+}
+
+// Both stages of one packet (the kernel body). Returns verdicts; counted slots via out params.
+struct PacketOut {
+  VerdictOut e, g;
+  uint32_t eslot, gslot;
+  int ecounted, gcounted;
+};
+
+GPC_HD PacketOut classify_packet(const Img& im, const Pkt& p, uint32_t dest) {
+  PacketOut o;
+  o.gslot = 0;
+  o.gcounted = 0;
+  o.e = eval_stage(im, 0, p, &o.eslot, &o.ecounted);
+  const uint32_t eact = o.e.packed & 0xffu;
+  if (eact == RV_DROP || eact == RV_REJECT || eact == RV_ISO_DROP) {
+    o.g.conj = 0;
+    o.g.packed = 0;  // GPC_ACT_NONE: the ingress stage is never reached
+  } else if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
+    o.g.conj = 0;
+    o.g.packed = RV_BYPASS;
+  } else {
+    o.g = eval_stage(im, 3, p, &o.gslot, &o.gcounted);
+  }
+  return o;
+}
+
+// Column loads -> axes (kernel and emulation share the defaults of gpc_pkt_soa).
+GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto, uint32_t out_port,
+                     uint32_t in_port, uint32_t svc_group, uint32_t tun_id, uint32_t ct_src, uint32_t ct_dst, uint32_t ct_state) {
+  p.ax[AX_SRC] = src;
+  p.ax[AX_DST] = dst;
+  p.ax[AX_CTSRC] = ct_src;
+  p.ax[AX_CTDST] = ct_dst;
+  p.ax[AX_INPORT] = in_port;
+  p.ax[AX_REG1] = out_port;
+  p.ax[AX_REG7] = svc_group;
+  p.ax[AX_TUN] = tun_id;
+  const bool ported = proto == 6 || proto == 17 || proto == 132 || proto == 1 || proto == 58;
+  p.ax[AX_L4D] = (proto << 16) | (ported ? dport : 0u);
+  p.ax[AX_L4S] = (proto << 16) | (ported ? sport : 0u);
+  p.ax[AX_CTST] = ct_state;
+}
+
+}  // namespace gpc

@@ -1,0 +1,38 @@
+// Builds the device classification image (core.hpp layout) from the realized flow table.
+#pragma once
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "compiler.hpp"
+#include "core.hpp"
+
+namespace gpc {
+
+struct HostImage {
+  ImageHdr hdr{};
+  std::vector<uint32_t> blob;        // hdr offsets index this (uint32 words)
+  uint32_t n_rules[6] = {0}, n_hard[6] = {0};
+  uint32_t n_flows = 0;
+  std::string error;                 // non-empty: unsupported flow shape
+};
+
+// Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
+// rank that applies the same control-plane calls, so slots line up for the RCCL all-reduce).
+class SlotMap {
+ public:
+  uint32_t get(uint32_t conj);
+  void release(uint32_t conj, std::vector<uint32_t>* freed);
+  uint32_t size() const { return uint32_t(slot_conj_.size()); }
+  const std::vector<uint32_t>& slot_conj() const { return slot_conj_; }
+
+ private:
+  std::map<uint32_t, uint32_t> slot_;
+  std::vector<uint32_t> slot_conj_;
+  std::vector<uint32_t> free_;
+};
+
+int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out);
+
+}  // namespace gpc

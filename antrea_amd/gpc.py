@@ -1,0 +1,381 @@
+"""ctypes binding of include/gpc.h (test-harness / bench plumbing).
+
+The product is the C-ABI library `antrea_amd/_build/libgpc.so` (C++ compiler + HIP kernels). This
+module only marshals the JSON-style rule records used by the test vectors into `gpc_rule` structs
+and numpy packet columns into `gpc_pkt_soa`. It has no classification logic of its own: when no
+HIP device is usable every classify call fails with GPC_EDEV.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import ipaddress
+import os
+from typing import Dict, List, Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libgpc.so")
+
+GPC_EINVAL, GPC_ENOTFOUND, GPC_ENOCLAUSE, GPC_EDEV, GPC_ERANGE = 2, 1, 5, 4, 7
+
+TABLES = {"AntreaPolicyEgressRule": 1, "EgressRule": 2, "EgressDefaultRule": 3,
+          "AntreaPolicyIngressRule": 4, "IngressRule": 5, "IngressDefaultRule": 6}
+POLICY_TYPES = {"K8sNetworkPolicy": 0, "AntreaNetworkPolicy": 1, "AntreaClusterNetworkPolicy": 2,
+                "AdminNetworkPolicy": 3, "BaselineAdminNetworkPolicy": 4}
+RULE_ACTIONS = {None: 0, "Allow": 0, "Drop": 1, "Reject": 2, "Pass": 3}
+PROTOCOLS = {None: 0, "TCP": 1, "UDP": 2, "SCTP": 3, "ICMP": 4, "IGMP": 5}
+ADDR_KINDS = {"ip": 1, "ipnet": 2, "ofport": 3, "svcgroup": 4, "ctip": 5, "ctipnet": 6, "labelid": 7}
+ACT_NAMES = ["NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "BYPASS"]
+
+# verdict dtype: gpc_verdict (8 B)
+VERDICT_DTYPE = np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"), ("flags", "u1")])
+
+
+class gpc_config(C.Structure):
+    _fields_ = [("ipv4_enabled", C.c_int32), ("ipv6_enabled", C.c_int32), ("enable_antrea_policy", C.c_int32),
+                ("enable_deny_tracking", C.c_int32), ("cookie", C.c_uint64), ("device", C.c_int32),
+                ("reserved", C.c_int32 * 7)]
+
+
+class gpc_addr(C.Structure):
+    _fields_ = [("kind", C.c_uint8), ("family", C.c_uint8), ("prefix_len", C.c_uint8), ("reserved", C.c_uint8),
+                ("value", C.c_uint32), ("ip", C.c_uint8 * 16)]
+
+
+class gpc_service(C.Structure):
+    _fields_ = [("protocol", C.c_uint8), ("has_port", C.c_uint8), ("has_end_port", C.c_uint8),
+                ("has_src_port", C.c_uint8), ("has_src_end_port", C.c_uint8), ("has_icmp_type", C.c_uint8),
+                ("has_icmp_code", C.c_uint8), ("has_igmp_type", C.c_uint8), ("port", C.c_uint16),
+                ("end_port", C.c_uint16), ("src_port", C.c_uint16), ("src_end_port", C.c_uint16),
+                ("icmp_type", C.c_int32), ("icmp_code", C.c_int32), ("igmp_type", C.c_int32),
+                ("has_group_address", C.c_uint8), ("group_address", C.c_uint8 * 4), ("reserved", C.c_uint8 * 3)]
+
+
+class gpc_rule(C.Structure):
+    _fields_ = [("direction", C.c_uint8), ("table", C.c_uint8), ("action", C.c_uint8), ("policy_type", C.c_uint8),
+                ("has_priority", C.c_uint8), ("enable_logging", C.c_uint8), ("priority", C.c_uint16),
+                ("flow_id", C.c_uint32), ("tier_priority", C.c_int32), ("n_from", C.c_int32), ("n_to", C.c_int32),
+                ("n_service", C.c_int32), ("from_", C.POINTER(gpc_addr)), ("to", C.POINTER(gpc_addr)),
+                ("service", C.POINTER(gpc_service)), ("name", C.c_char_p), ("log_label", C.c_char_p),
+                ("policy_namespace", C.c_char_p), ("policy_name", C.c_char_p), ("policy_uid", C.c_char_p)]
+
+
+class gpc_pkt_soa(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("src", "dst", "sport", "dport", "proto", "out_port", "in_port", "svc_group",
+                                          "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "len")]
+
+
+class gpc_policy_info(C.Structure):
+    _fields_ = [("found", C.c_int32), ("policy_type", C.c_uint8), ("of_priority", C.c_uint16),
+                ("policy_namespace", C.c_char * 64), ("policy_name", C.c_char * 128), ("policy_uid", C.c_char * 64),
+                ("rule_name", C.c_char * 128), ("log_label", C.c_char * 64)]
+
+
+class gpc_rule_metric(C.Structure):
+    _fields_ = [("conj_id", C.c_uint32), ("reserved", C.c_uint32), ("packets", C.c_uint64), ("bytes", C.c_uint64),
+                ("sessions", C.c_uint64)]
+
+
+class gpc_image_stats(C.Structure):
+    _fields_ = [("epoch", C.c_uint64), ("device_bytes", C.c_uint64), ("n_rules", C.c_uint32 * 6),
+                ("n_hard", C.c_uint32 * 6), ("n_flows", C.c_uint32), ("n_counter_slots", C.c_uint32)]
+
+
+EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "gpc_batch_install",
+           "gpc_uninstall_rule", "gpc_add_rule_addrs", "gpc_del_rule_addrs", "gpc_reassign_priorities",
+           "gpc_get_policy_info", "gpc_metrics", "gpc_commit", "gpc_classify", "gpc_classify_host", "gpc_counters",
+           "gpc_reset_counters", "gpc_dump_flows", "gpc_get_image_stats", "gpc_debug_image", "gpc_strerror",
+           "gpc_abi_version"]
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError("libgpc.so not built (run `python -m antrea_amd.build`): %s" % path)
+    lib = C.CDLL(path)
+    vp, i32, sz = C.c_void_p, C.c_int32, C.c_size_t
+    lib.gpc_create.argtypes = [C.POINTER(gpc_config), C.POINTER(vp)]
+    lib.gpc_destroy.argtypes = [vp]
+    lib.gpc_destroy.restype = None
+    lib.gpc_initialize.argtypes = [vp]
+    lib.gpc_install_rule.argtypes = [vp, C.POINTER(gpc_rule)]
+    lib.gpc_batch_install.argtypes = [vp, C.POINTER(gpc_rule), sz]
+    lib.gpc_uninstall_rule.argtypes = [vp, C.c_uint32, C.POINTER(C.c_uint16), sz, C.POINTER(sz)]
+    lib.gpc_add_rule_addrs.argtypes = [vp, C.c_uint32, i32, C.POINTER(gpc_addr), sz, C.POINTER(C.c_uint16), i32, i32]
+    lib.gpc_del_rule_addrs.argtypes = [vp, C.c_uint32, i32, C.POINTER(gpc_addr), sz, C.POINTER(C.c_uint16)]
+    lib.gpc_reassign_priorities.argtypes = [vp, C.POINTER(C.c_uint16), C.POINTER(C.c_uint16), sz, C.c_uint8]
+    lib.gpc_get_policy_info.argtypes = [vp, C.c_uint32, C.POINTER(gpc_policy_info)]
+    lib.gpc_metrics.argtypes = [vp, C.POINTER(gpc_rule_metric), sz, C.POINTER(sz)]
+    lib.gpc_commit.argtypes = [vp]
+    lib.gpc_classify.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32, vp]
+    lib.gpc_classify_host.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32]
+    lib.gpc_counters.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
+    lib.gpc_reset_counters.argtypes = [vp]
+    lib.gpc_dump_flows.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]
+    lib.gpc_get_image_stats.argtypes = [vp, C.POINTER(gpc_image_stats)]
+    lib.gpc_debug_image.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp), C.POINTER(sz)]
+    lib.gpc_strerror.argtypes = [i32]
+    lib.gpc_strerror.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+class GpcError(RuntimeError):
+    def __init__(self, code, what):
+        self.code = -code if code < 0 else code
+        super().__init__("%s: %s (%d)" % (what, load().gpc_strerror(code).decode(), code))
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise GpcError(rc, what)
+
+
+# ------------------------------------------------------------------------------ marshalling
+def _addr(a) -> gpc_addr:
+    out = gpc_addr()
+    if isinstance(a, str):
+        if "." not in a and ":" not in a:
+            a = {"ofport": int(a)}
+        elif "/" in a:
+            a = {"ipnet": a}
+        else:
+            a = {"ip": a}
+    (kind, v), = a.items()
+    out.kind = ADDR_KINDS[kind]
+    if kind in ("ip", "ctip"):
+        ip = ipaddress.ip_address(v)
+        out.family = ip.version
+        out.ip[:len(ip.packed)] = list(ip.packed)
+    elif kind in ("ipnet", "ctipnet"):
+        n = ipaddress.ip_network(v, strict=False)
+        out.family = n.version
+        out.prefix_len = n.prefixlen
+        out.ip[:len(n.network_address.packed)] = list(n.network_address.packed)
+    else:
+        out.value = int(v)
+    return out
+
+
+def _service(s: dict) -> gpc_service:
+    out = gpc_service()
+    out.protocol = PROTOCOLS[s.get("protocol")]
+    for f in ("port", "end_port", "src_port", "src_end_port"):
+        if s.get(f) is not None:
+            setattr(out, "has_" + f, 1)
+            setattr(out, f, int(s[f]))
+    for f in ("icmp_type", "icmp_code", "igmp_type"):
+        if s.get(f) is not None:
+            setattr(out, "has_" + f, 1)
+            setattr(out, f, int(s[f]))
+    if s.get("group_address"):
+        out.has_group_address = 1
+        out.group_address[:] = list(ipaddress.ip_address(s["group_address"]).packed)
+    return out
+
+
+class RuleBuf:
+    """Keeps the ctypes objects of one or more gpc_rule alive."""
+
+    def __init__(self, rules: List[dict]):
+        self.keep = []
+        self.arr = (gpc_rule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            self._fill(self.arr[i], r)
+        self.n = len(rules)
+
+    def _addrs(self, lst):
+        if lst is None:
+            return -1, None
+        arr = (gpc_addr * max(1, len(lst)))(*[_addr(a) for a in lst])
+        self.keep.append(arr)
+        return len(lst), arr
+
+    def _fill(self, g: gpc_rule, r: dict):
+        g.direction = 1 if r["direction"] == "Out" else 0
+        g.table = TABLES[r["table"]]
+        g.action = RULE_ACTIONS[r.get("action")]
+        g.policy_type = POLICY_TYPES[r.get("policy_type", "K8sNetworkPolicy")]
+        if r.get("priority") is not None:
+            g.has_priority = 1
+            g.priority = int(r["priority"])
+        g.enable_logging = 1 if r.get("enable_logging") else 0
+        g.flow_id = int(r["flow_id"])
+        g.tier_priority = int(r.get("tier_priority") or 0)
+        g.n_from, g.from_ = self._addrs(r.get("from"))
+        g.n_to, g.to = self._addrs(r.get("to"))
+        svc = r.get("service")
+        if svc is None:
+            g.n_service = -1
+        else:
+            arr = (gpc_service * max(1, len(svc)))(*[_service(s) for s in svc])
+            self.keep.append(arr)
+            g.n_service, g.service = len(svc), arr
+        for f in ("name", "log_label", "policy_namespace", "policy_name", "policy_uid"):
+            b = (r.get(f) or "").encode()
+            self.keep.append(b)
+            setattr(g, f, b)
+
+
+PKT_COLUMNS = {"src": np.uint32, "dst": np.uint32, "sport": np.uint16, "dport": np.uint16, "proto": np.uint8,
+               "out_port": np.uint32, "in_port": np.uint32, "svc_group": np.uint32, "tun_id": np.uint32,
+               "ct_src": np.uint32, "ct_dst": np.uint32, "ct_state": np.uint8, "dest": np.uint8, "len": np.uint16}
+
+
+def pkt_soa_host(cols: Dict[str, np.ndarray]):
+    """numpy columns -> (gpc_pkt_soa, keepalive list)."""
+    soa = gpc_pkt_soa()
+    keep = []
+    n = None
+    for name, dt in PKT_COLUMNS.items():
+        a = cols.get(name)
+        if a is None:
+            continue
+        a = np.ascontiguousarray(a, dtype=dt)
+        if n is None:
+            n = len(a)
+        elif len(a) != n:
+            raise ValueError("column %s has %d rows, expected %d" % (name, len(a), n))
+        keep.append(a)
+        setattr(soa, name, a.ctypes.data)
+    return soa, keep, n or 0
+
+
+def pkt_soa_device(cols: Dict[str, "object"]):
+    """torch device tensors -> gpc_pkt_soa of device pointers."""
+    soa = gpc_pkt_soa()
+    for name in PKT_COLUMNS:
+        t = cols.get(name)
+        if t is not None:
+            setattr(soa, name, t.data_ptr())
+    return soa
+
+
+class Classifier:
+    """One gpc context (one GPU)."""
+
+    def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
+                 cookie=0x1020000000000, device=0):
+        self.lib = load()
+        cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
+                         enable_antrea_policy=int(enable_antrea_policy),
+                         enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device)
+        h = C.c_void_p()
+        _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.gpc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- openflow.Client NP surface
+    def initialize(self):
+        _check(self.lib.gpc_initialize(self.h), "Initialize")
+
+    def install_policy_rule_flows(self, rule: dict):
+        b = RuleBuf([rule])
+        _check(self.lib.gpc_install_rule(self.h, b.arr), "InstallPolicyRuleFlows")
+
+    def batch_install_policy_rule_flows(self, rules: List[dict]):
+        b = RuleBuf(rules)
+        _check(self.lib.gpc_batch_install(self.h, b.arr, b.n), "BatchInstallPolicyRuleFlows")
+
+    def uninstall_policy_rule_flows(self, rule_id: int) -> List[str]:
+        st = (C.c_uint16 * 64)()
+        n = C.c_size_t()
+        _check(self.lib.gpc_uninstall_rule(self.h, rule_id, st, 64, C.byref(n)), "UninstallPolicyRuleFlows")
+        return [str(st[i]) for i in range(n.value)]
+
+    def _addr_call(self, fn, rule_id, addr_type, addrs, priority, *extra):
+        arr = (gpc_addr * max(1, len(addrs)))(*[_addr(a) for a in addrs])
+        p = C.pointer(C.c_uint16(priority)) if priority is not None else None
+        return fn(self.h, rule_id, 0 if addr_type == "src" else 1, arr, len(addrs), p, *extra)
+
+    def add_policy_rule_address(self, rule_id, addr_type, addrs, priority=None, enable_logging=False, is_mcnp=False):
+        _check(self._addr_call(self.lib.gpc_add_rule_addrs, rule_id, addr_type, addrs, priority,
+                               int(enable_logging), int(is_mcnp)), "AddPolicyRuleAddress")
+
+    def delete_policy_rule_address(self, rule_id, addr_type, addrs, priority=None):
+        _check(self._addr_call(self.lib.gpc_del_rule_addrs, rule_id, addr_type, addrs, priority),
+               "DeletePolicyRuleAddress")
+
+    def reassign_flow_priorities(self, updates: Dict[int, int], table: str):
+        ks = list(updates)
+        f = (C.c_uint16 * max(1, len(ks)))(*ks)
+        t = (C.c_uint16 * max(1, len(ks)))(*[updates[k] for k in ks])
+        _check(self.lib.gpc_reassign_priorities(self.h, f, t, len(ks), TABLES[table]), "ReassignFlowPriorities")
+
+    def get_policy_info_from_conjunction(self, rule_id):
+        info = gpc_policy_info()
+        _check(self.lib.gpc_get_policy_info(self.h, rule_id, C.byref(info)), "GetPolicyInfoFromConjunction")
+        if not info.found:
+            return (False, None, "", "", "")
+        ref = ({v: k for k, v in POLICY_TYPES.items()}[info.policy_type], info.policy_namespace.decode(),
+               info.policy_name.decode(), info.policy_uid.decode())
+        return (True, ref, str(info.of_priority), info.rule_name.decode(), info.log_label.decode())
+
+    def network_policy_metrics(self) -> Dict[int, tuple]:
+        n = C.c_size_t()
+        _check(self.lib.gpc_metrics(self.h, None, 0, C.byref(n)), "NetworkPolicyMetrics")
+        arr = (gpc_rule_metric * max(1, n.value))()
+        _check(self.lib.gpc_metrics(self.h, arr, n.value, C.byref(n)), "NetworkPolicyMetrics")
+        return {arr[i].conj_id: (arr[i].packets, arr[i].bytes, arr[i].sessions) for i in range(n.value)}
+
+    # --- data path
+    def commit(self):
+        _check(self.lib.gpc_commit(self.h), "gpc_commit")
+
+    def classify_host(self, cols: Dict[str, np.ndarray], count=False) -> np.ndarray:
+        soa, keep, n = pkt_soa_host(cols)
+        out = np.zeros(2 * n, dtype=VERDICT_DTYPE)
+        _check(self.lib.gpc_classify_host(self.h, C.byref(soa), n, out.ctypes.data, int(count)), "gpc_classify_host")
+        return out.reshape(n, 2)
+
+    def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0):
+        _check(self.lib.gpc_classify(self.h, C.byref(soa), n, out_ptr, int(count), stream or None), "gpc_classify")
+
+    def counters(self):
+        p = C.POINTER(C.c_uint64)()
+        s = C.POINTER(C.c_uint32)()
+        n = C.c_size_t()
+        _check(self.lib.gpc_counters(self.h, C.byref(p), C.byref(s), C.byref(n)), "gpc_counters")
+        slots = [s[i] for i in range(n.value)]
+        return C.cast(p, C.c_void_p).value, slots
+
+    def reset_counters(self):
+        _check(self.lib.gpc_reset_counters(self.h), "gpc_reset_counters")
+
+    # --- introspection
+    def dump_flows(self) -> List[str]:
+        need = C.c_size_t()
+        self.lib.gpc_dump_flows(self.h, None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value)
+        _check(self.lib.gpc_dump_flows(self.h, buf, need.value, C.byref(need)), "gpc_dump_flows")
+        return [l for l in buf.value.decode().split("\n") if l]
+
+    def debug_image(self):
+        """(blob pointer, n_words, hdr pointer, hdr_bytes) of the last committed host image."""
+        b = C.POINTER(C.c_uint32)()
+        n = C.c_size_t()
+        h = C.c_void_p()
+        hb = C.c_size_t()
+        _check(self.lib.gpc_debug_image(self.h, C.byref(b), C.byref(n), C.byref(h), C.byref(hb)), "gpc_debug_image")
+        return C.cast(b, C.c_void_p).value, n.value, h.value, hb.value
+
+    def image_stats(self) -> dict:
+        st = gpc_image_stats()
+        _check(self.lib.gpc_get_image_stats(self.h, C.byref(st)), "gpc_get_image_stats")
+        return {"epoch": st.epoch, "device_bytes": st.device_bytes, "n_rules": list(st.n_rules),
+                "n_hard": list(st.n_hard), "n_flows": st.n_flows, "n_counter_slots": st.n_counter_slots}

@@ -1,0 +1,187 @@
+"""Headline benchmark: Mpps classified (5-tuple -> rule verdict, both policy stages) @100k rules.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--packets 67108864]
+
+One process per GPU (torchrun for N > 1). Each rank builds the same rule set (C3 = 100k rules),
+classifies its own packet shard (weak scaling: `--packets` per GPU, inputs resident in HBM before
+the timed region) and, when counters are on, all-reduces the per-rule counters over RCCL at the
+end of the run (the only collective of the path). A step = one gpc_classify launch
+over the whole per-GPU batch. Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def _lbar(wl, clf, n=20000):
+    """Mean distinct 64-B image lines one packet's evaluation reads (instrumented host emulation of
+    the same image, tests/csrc/emu.cpp), i.e. L-bar of SURVEY §8(d)."""
+    try:
+        from tests import emu
+        from antrea_amd import workload
+        cols = workload.gen_packets(wl, n, seed=12345)
+        emu.stats(reset=True)
+        emu.classify(clf, cols)
+        s = emu.stats()
+        return s[6] / max(1, s[7])
+    except Exception as e:  # pragma: no cover - g++ missing
+        print("L-bar unavailable: %s" % e, file=sys.stderr)
+        return None
+
+
+class _CAI:
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2}
+
+
+def _device_view(ptr, n, dev):
+    import torch
+    return torch.as_tensor(_CAI(ptr, n), device=dev)
+
+
+def _cpu_baseline(wl, seconds):
+    try:
+        from oracle import cbaseline
+        return cbaseline.run(wl, seconds)
+    except Exception as e:
+        print("cpu baseline unavailable: %s" % e, file=sys.stderr)
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--packets", type=int, default=1 << 26)
+    ap.add_argument("--no-count", action="store_true", help="disable per-rule counters")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from antrea_amd import gpc, workload
+    from antrea_amd.build import build
+    if rank == 0 or world == 1:
+        build()
+    if world > 1:
+        dist.barrier()
+
+    t0 = time.time()
+    wl = workload.CONFIGS[args.config]()
+    clf = gpc.Classifier(device=local)
+    clf.initialize()
+    clf.batch_install_policy_rule_flows(wl.rules)
+    clf.commit()
+    t_build = time.time() - t0
+
+    n = args.packets
+    cols = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + rank, device=dev)
+    out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
+    soa = gpc.pkt_soa_device(cols)
+    count = not args.no_count
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    for _ in range(args.warmup):
+        clf.classify_device(soa, n, out.data_ptr(), count=count, stream=sptr)
+    clf.reset_counters()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        clf.classify_device(soa, n, out.data_ptr(), count=count, stream=sptr)
+        ends[i].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # per-rule counters: the path's only collective (RCCL all-reduce). The
+        # library's device counters are wrapped zero-copy and reduced in place.
+        ptr, slots = clf.counters()
+        if count and ptr and slots:
+            cnt = _device_view(ptr, 2 * len(slots), dev)
+            torch.cuda.synchronize(dev)
+            dist.all_reduce(cnt)
+            torch.cuda.synchronize(dev)
+    elapsed = float(t.item())
+
+    total = n * args.steps * world
+    mpps = total / elapsed / 1e6
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    v = out.view(torch.uint8).reshape(n, 2, 8)[: min(n, 1 << 20)].cpu().numpy()
+    mix = {}
+    names = ["NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "BYPASS"]
+    for j, stage in enumerate(("egress", "ingress")):
+        import numpy as np
+        a, c = np.unique(v[:, j, 4], return_counts=True)
+        mix[stage] = {names[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
+
+    lbar = _lbar(wl, clf)
+    b_in, b_out = 17, 16
+    b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
+    pps_kernel = n / (kern_ms / 1e3)
+    achieved = pps_kernel * b_alg / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_packet_alg": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
+                "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
+    cpu = None if args.no_cpu_baseline else _cpu_baseline(wl, args.cpu_seconds)
+    st = clf.image_stats()
+    res = {
+        "metric": "Mpps classified (5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW",
+        "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": args.config, "rules": len(wl.rules), "packets_per_gpu": n,
+                   "flows": st["n_flows"], "image_mb": round(st["device_bytes"] / 1e6, 1),
+                   "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
+                   "verdict_mix": mix, "build_s": round(t_build, 1)},
+        "kernel_ms": round(kern_ms, 3),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,278 @@
+/*
+ * gpc.h -- C-ABI of the MI355X NetworkPolicy packet classifier ("gpuclassify").
+ *
+ * Drop-in boundary for the NetworkPolicy half of Antrea's `openflow.Client`
+ * (reference: pkg/agent/openflow/client.go:56-414; NP methods :128-148, 215-223, 240-251, 310-317;
+ * implementation pkg/agent/openflow/network_policy.go). A Go `pkg/agent/gpuclassify` layer binds
+ * these symbols over cgo; C++ callers use include/gpc_client.hpp; the Python
+ * test harness and bench use ctypes.
+ *
+ * Conventions
+ *   - Every call returns 0 on success or a negative GPC_E* code (gpc_strerror()).
+ *   - The caller owns every buffer it passes; the library copies what it keeps.
+ *   - Control-plane calls (install/uninstall/add/del/reassign/commit) are serialized by an internal
+ *     mutex (the role of conjMatchFlowLock + replayMutex, network_policy.go:1161-1167, 2077).
+ *   - gpc_classify() may run concurrently with control-plane calls; it always sees exactly one
+ *     committed epoch (gpc_commit publishes atomically, as an OpenFlow bundle does:
+ *     pkg/ovs/openflow/ofctrl_bridge.go:468-539).
+ *   - No torch / HIP types appear in this header; streams are passed as `void*` (hipStream_t).
+ */
+#ifndef GPC_H
+#define GPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPC_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------- error codes */
+#define GPC_OK 0
+#define GPC_ENOTFOUND 1   /* ConjunctionNotFound (network_policy.go:309-319)                   */
+#define GPC_EINVAL 2      /* malformed argument / unsupported flow shape                          */
+#define GPC_ENOMEM 3      /* host or device allocation failed                                     */
+#define GPC_EDEV 4        /* HIP runtime error / no device                                        */
+#define GPC_ENOCLAUSE 5   /* "no clause is using addrType %d" (network_policy.go:1674-1676)       */
+#define GPC_EBUNDLE 6     /* flow bundle rejected; caches rolled back (network_policy.go:1344-1349)*/
+#define GPC_ERANGE 7      /* output buffer too small (needed size returned)                      */
+
+/* ---------------------------------------------------------------------------- enums */
+enum gpc_direction { GPC_DIR_IN = 0, GPC_DIR_OUT = 1 };            /* v1beta2.Direction */
+
+/* Rule tables (pipeline.go:150-176). */
+enum gpc_table {
+  GPC_TABLE_ANTREA_POLICY_EGRESS_RULE = 1,
+  GPC_TABLE_EGRESS_RULE = 2,
+  GPC_TABLE_EGRESS_DEFAULT_RULE = 3,
+  GPC_TABLE_ANTREA_POLICY_INGRESS_RULE = 4,
+  GPC_TABLE_INGRESS_RULE = 5,
+  GPC_TABLE_INGRESS_DEFAULT_RULE = 6
+};
+
+enum gpc_policy_type {                                             /* v1beta2.NetworkPolicyType */
+  GPC_POLICY_K8S = 0,
+  GPC_POLICY_ANNP = 1,
+  GPC_POLICY_ACNP = 2,
+  GPC_POLICY_ANP = 3,
+  GPC_POLICY_BANP = 4
+};
+
+enum gpc_rule_action {                                             /* crdv1beta1.RuleAction */
+  GPC_RULE_ALLOW = 0,
+  GPC_RULE_DROP = 1,
+  GPC_RULE_REJECT = 2,
+  GPC_RULE_PASS = 3
+};
+
+enum gpc_addr_kind {                          /* types.Address implementations, network_policy.go */
+  GPC_ADDR_IP = 1,        /* IPAddress        :97-131  */
+  GPC_ADDR_IPNET = 2,     /* IPNetAddress     :133-167 */
+  GPC_ADDR_OFPORT = 3,    /* OFPortAddress    :169-197 */
+  GPC_ADDR_SVC_GROUP = 4, /* ServiceGroupIDAddress :199-216 */
+  GPC_ADDR_CT_IP = 5,     /* CTIPAddress      :218-252 */
+  GPC_ADDR_CT_IPNET = 6,  /* CTIPNetAddress   :254-288 */
+  GPC_ADDR_LABEL_ID = 7   /* LabelIDAddress   :290-307 */
+};
+
+enum gpc_addr_type { GPC_SRC_ADDRESS = 0, GPC_DST_ADDRESS = 1 };   /* types.AddressType */
+
+enum gpc_protocol {                                                /* v1beta2.Protocol */
+  GPC_PROTO_NONE = 0, /* nil protocol: defaults to TCP (network_policy.go:979-981) */
+  GPC_PROTO_TCP = 1,
+  GPC_PROTO_UDP = 2,
+  GPC_PROTO_SCTP = 3,
+  GPC_PROTO_ICMP = 4,
+  GPC_PROTO_IGMP = 5
+};
+
+/* Verdict actions. */
+enum gpc_verdict_action {
+  GPC_ACT_NONE = 0,           /* stage not reached (packet dropped in the egress stage)        */
+  GPC_ACT_NO_MATCH = 1,       /* no policy flow hit: allowed by default (Metric table miss)    */
+  GPC_ACT_ALLOW = 2,          /* conj action flow with ct commit (pipeline.go:1718-1808)       */
+  GPC_ACT_DROP = 3,           /* conj deny flow, APDeny + reg3 (pipeline.go:1812-1859)          */
+  GPC_ACT_REJECT = 4,         /* conj deny flow with reject disposition                        */
+  GPC_ACT_ISOLATION_DROP = 5, /* K8s default / MCNP drop flow (pipeline.go:2040-2076)           */
+  GPC_ACT_BYPASS = 6          /* ct est/rel skip flow or IngressSecurityClassifier bypass       */
+};
+#define GPC_VFLAG_PASS 0x1    /* a Pass rule of the AntreaPolicy table was hit on the way      */
+#define GPC_VFLAG_TIE 0x2     /* >1 conjunction completed at the winning priority (OVS-defined
+                                 order; resolved to the lowest conj id)                        */
+
+/* Packet destination class, as IngressSecurityClassifier sees reg0 (fields.go PktDestinationField). */
+enum gpc_dest { GPC_DEST_POD = 0, GPC_DEST_GATEWAY = 1, GPC_DEST_TUNNEL = 2, GPC_DEST_UPLINK = 3 };
+#define GPC_CT_NEW 0x01
+#define GPC_CT_EST 0x02
+#define GPC_CT_REL 0x04
+#define GPC_CT_RPL 0x08
+#define GPC_CT_TRK 0x20
+
+/* ---------------------------------------------------------------------------- records */
+typedef struct gpc_ctx gpc_ctx;
+
+typedef struct gpc_config {
+  int32_t ipv4_enabled;          /* featureNetworkPolicy.ipProtocols                           */
+  int32_t ipv6_enabled;
+  int32_t enable_antrea_policy;  /* AntreaPolicy feature gate (egressTables, skip flows)        */
+  int32_t enable_deny_tracking;
+  uint64_t cookie;               /* cookie printed in flow dumps (round<<48 | category<<40)     */
+  int32_t device;                /* HIP device ordinal used by this context                    */
+  int32_t reserved[7];
+} gpc_config;
+
+typedef struct gpc_addr {        /* 24 bytes */
+  uint8_t kind;                  /* gpc_addr_kind */
+  uint8_t family;                /* 4 or 6 for IP kinds */
+  uint8_t prefix_len;            /* IPNET kinds */
+  uint8_t reserved;
+  uint32_t value;                /* OFPORT / SVC_GROUP / LABEL_ID */
+  uint8_t ip[16];                /* network byte order; IPv4 in ip[0..3] */
+} gpc_addr;
+
+typedef struct gpc_service {     /* v1beta2.Service (controlplane/v1beta2/types.go:299-321) */
+  uint8_t protocol;              /* gpc_protocol */
+  uint8_t has_port, has_end_port, has_src_port, has_src_end_port;
+  uint8_t has_icmp_type, has_icmp_code, has_igmp_type;
+  uint16_t port, end_port, src_port, src_end_port;
+  int32_t icmp_type, icmp_code, igmp_type;
+  uint8_t has_group_address;
+  uint8_t group_address[4];      /* IGMP query group (IPv4) */
+  uint8_t reserved[3];
+} gpc_service;
+
+typedef struct gpc_rule {        /* types.PolicyRule (pkg/agent/types/networkpolicy.go:92-108) */
+  uint8_t direction;             /* gpc_direction */
+  uint8_t table;                 /* gpc_table (PolicyRule.TableID) */
+  uint8_t action;                /* gpc_rule_action (PolicyRule.Action; ignored for K8s) */
+  uint8_t policy_type;           /* gpc_policy_type (PolicyRef.Type) */
+  uint8_t has_priority;          /* PolicyRule.Priority != nil */
+  uint8_t enable_logging;
+  uint16_t priority;
+  uint32_t flow_id;              /* conjunction id */
+  int32_t tier_priority;         /* reported in verdicts (not part of PolicyRule) */
+  int32_t n_from;                /* < 0 : From == nil (no clause); >= 0 : clause with n addresses */
+  int32_t n_to;
+  int32_t n_service;
+  const gpc_addr* from;
+  const gpc_addr* to;
+  const gpc_service* service;
+  const char* name;              /* may be NULL */
+  const char* log_label;
+  const char* policy_namespace;
+  const char* policy_name;
+  const char* policy_uid;
+} gpc_rule;
+
+/* Structure-of-arrays packet batch. Required columns: src, dst, sport, dport, proto, out_port.
+ * Optional columns may be NULL (default in parentheses). Addresses/ports in host byte order.
+ * For ICMP, sport = type and dport = code (OVS keeps them in tp_src/tp_dst). */
+typedef struct gpc_pkt_soa {
+  const uint32_t* src;           /* nw_src */
+  const uint32_t* dst;           /* nw_dst */
+  const uint16_t* sport;         /* tp_src */
+  const uint16_t* dport;         /* tp_dst */
+  const uint8_t* proto;          /* nw_proto */
+  const uint32_t* out_port;      /* reg1 TargetOFPortField */
+  const uint32_t* in_port;       /* (0) */
+  const uint32_t* svc_group;     /* reg7 ServiceGroupIDField (0) */
+  const uint32_t* tun_id;        /* label identity (0) */
+  const uint32_t* ct_src;        /* ct_nw_src (= src) */
+  const uint32_t* ct_dst;        /* ct_nw_dst (= dst) */
+  const uint8_t* ct_state;       /* (+new+trk) */
+  const uint8_t* dest;           /* gpc_dest (POD) */
+  const uint16_t* len;           /* bytes for per-rule counters (0) */
+} gpc_pkt_soa;
+
+typedef struct gpc_verdict {     /* 8 bytes; gpc_classify writes 2 per packet: [egress, ingress] */
+  uint32_t conj_id;              /* reg5/reg6 or reg3 conjunction id (0 if none) */
+  uint8_t action;                /* gpc_verdict_action */
+  uint8_t table;                 /* 1 = AntreaPolicy*Rule, 2 = *Rule, 3 = *DefaultRule, 0 = none */
+  uint8_t tier;                  /* tier priority of the winning rule (0 if none / K8s) */
+  uint8_t flags;                 /* GPC_VFLAG_* */
+} gpc_verdict;
+
+typedef struct gpc_policy_info { /* GetPolicyInfoFromConjunction result */
+  int32_t found;
+  uint8_t policy_type;
+  uint16_t of_priority;          /* priority of the first action flow */
+  char policy_namespace[64];
+  char policy_name[128];
+  char policy_uid[64];
+  char rule_name[128];
+  char log_label[64];
+} gpc_policy_info;
+
+typedef struct gpc_rule_metric { /* types.RuleMetric keyed by conjunction id */
+  uint32_t conj_id;
+  uint32_t reserved;
+  uint64_t packets, bytes, sessions;
+} gpc_rule_metric;
+
+typedef struct gpc_image_stats { /* shape of the committed device image (for roofline math) */
+  uint64_t epoch;
+  uint64_t device_bytes;
+  uint32_t n_rules[6];           /* per rule table, soft + hard pseudo-rules */
+  uint32_t n_hard[6];
+  uint32_t n_flows;
+  uint32_t n_counter_slots;
+} gpc_image_stats;
+
+/* ---------------------------------------------------------------------------- lifecycle */
+int gpc_create(const gpc_config* cfg, gpc_ctx** out);
+void gpc_destroy(gpc_ctx* ctx);
+/* Client.Initialize NP part: skipPolicyRuleCheckFlows (network_policy.go:2144-2211). */
+int gpc_initialize(gpc_ctx* ctx);
+
+/* ---------------------------------------------------------------------------- openflow.Client NP surface */
+/* InstallPolicyRuleFlows(*types.PolicyRule) error            network_policy.go:1160 */
+int gpc_install_rule(gpc_ctx* ctx, const gpc_rule* rule);
+/* BatchInstallPolicyRuleFlows([]*types.PolicyRule) error     network_policy.go:1310 */
+int gpc_batch_install(gpc_ctx* ctx, const gpc_rule* rules, size_t n);
+/* UninstallPolicyRuleFlows(ruleID) ([]string, error)         network_policy.go:1570
+ * Stale OF priorities are returned in stale[0..*n_stale). */
+int gpc_uninstall_rule(gpc_ctx* ctx, uint32_t rule_id, uint16_t* stale, size_t stale_cap, size_t* n_stale);
+/* AddPolicyRuleAddress(ruleID, addrType, addresses, priority, enableLogging, isMCNPRule) network_policy.go:1661 */
+int gpc_add_rule_addrs(gpc_ctx* ctx, uint32_t rule_id, int32_t addr_type, const gpc_addr* addrs, size_t n,
+                       const uint16_t* priority_or_null, int32_t enable_logging, int32_t is_mcnp);
+/* DeletePolicyRuleAddress(ruleID, addrType, addresses, priority) network_policy.go:1686 */
+int gpc_del_rule_addrs(gpc_ctx* ctx, uint32_t rule_id, int32_t addr_type, const gpc_addr* addrs, size_t n,
+                       const uint16_t* priority_or_null);
+/* ReassignFlowPriorities(map[uint16]uint16, tableID) error   network_policy.go:1873 */
+int gpc_reassign_priorities(gpc_ctx* ctx, const uint16_t* from, const uint16_t* to, size_t n, uint8_t table);
+/* GetPolicyInfoFromConjunction(ruleID)                        network_policy.go:1555 */
+int gpc_get_policy_info(gpc_ctx* ctx, uint32_t rule_id, gpc_policy_info* out);
+/* NetworkPolicyMetrics() map[uint32]*types.RuleMetric          network_policy.go:2034
+ * Reads the per-rule device counters of this context. */
+int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n);
+
+/* ---------------------------------------------------------------------------- data path */
+/* Build the device image from the realized flow table and publish it atomically. */
+int gpc_commit(gpc_ctx* ctx);
+/* Classify n packets whose columns are DEVICE pointers; writes 2*n verdicts (device pointer).
+ * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t. */
+int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
+/* Same with HOST pointers (copies in and out; synchronous). */
+int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
+/* Per-rule counters as a device buffer of n_slots x {packets, bytes} uint64 (for an RCCL
+ * all-reduce by the caller), plus the slot -> conj id map (host, valid until the next commit). */
+int gpc_counters(gpc_ctx* ctx, uint64_t** dev_counters, const uint32_t** slot_conj, size_t* n_slots);
+int gpc_reset_counters(gpc_ctx* ctx);
+
+/* ---------------------------------------------------------------------------- introspection */
+/* ovs-ofctl style dump of the realized flow table (utils.go FlowModToString), '\n' separated. */
+int gpc_dump_flows(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed);
+int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out);
+/* The last committed image as built on the host (kept as shadow state for re-upload after a
+ * device reset). Pointers stay valid until the next gpc_commit. Used by tests to verify the
+ * image independently of the device. */
+int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes);
+const char* gpc_strerror(int err);
+int gpc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPC_H */

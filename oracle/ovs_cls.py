@@ -93,6 +93,11 @@ def _is_soft(flow) -> bool:
     return bool(acts) and all(a[0] == "conjunction" for a in acts)
 
 
+def _verdict_sig(flow):
+    acts = [a for a in flow["actions"] if a[0] in ("drop", "goto_table", "ct_commit", "group")]
+    return tuple(a[0] + str(a[1] if len(a) > 1 else "") for a in acts) or ("drop",)
+
+
 def classifier_lookup(flows: List[dict], pkt: dict, st: dict, allow_conj=True):
     """Returns (flow|None, tie:bool)."""
     hard, hard_pri, tie = None, -1, False
@@ -105,7 +110,9 @@ def classifier_lookup(flows: List[dict], pkt: dict, st: dict, allow_conj=True):
                 soft.append(f)
         elif f["priority"] > hard_pri:
             hard, hard_pri, tie = f, f["priority"], False
-        elif f["priority"] == hard_pri:
+        elif f["priority"] == hard_pri and _verdict_sig(f) != _verdict_sig(hard):
+            # overlapping hard flows of one priority: OpenFlow leaves the choice undefined; it only
+            # matters (and is reported) when their actions differ
             tie = True
     if not allow_conj:
         return hard, tie
@@ -179,6 +186,8 @@ class Pipeline:
                     action = ACT_REJECT if reject else ACT_DROP
                     goto = metric
                 elif goto in (t2,) or (goto == "group" and not deny and st["regs"].get(0, 0) & 0x1800 == 0x1800):
+                    # Pass: the conj id stays in reg5/reg6 (traceflow readback) unless a later
+                    # table's rule overwrites it
                     flags |= FLAG_PASS
                     t = t2
                     continue
@@ -187,9 +196,8 @@ class Pipeline:
                     goto = metric
             else:
                 if goto is None:
-                    return ACT_ISOLATION_DROP, 0, tindex, flags, None
+                    return ACT_ISOLATION_DROP, conj, tindex, flags, None
                 action = ACT_BYPASS
-                conj = 0
                 goto = metric
             t = goto
         # metric table: allow/deny counters (pipeline.go:1604-1670)

@@ -1,0 +1,43 @@
+// TEST-ONLY host emulation of the device kernel body (core.hpp classify_packet) over the image the
+// product library built (gpc_debug_image). Lets the CPU test tier verify the image builder and the
+// evaluation logic without a GPU. Never linked into libgpc.so; the product has no CPU classify path.
+#include <cstddef>
+#include <cstdint>
+
+#include <algorithm>
+#include <vector>
+extern "C" {
+unsigned long long gpc_emu_stats[8];
+}
+static std::vector<uintptr_t> g_lines;
+extern "C" void gpc_emu_touch(const void* p, unsigned bytes) {
+  uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  for (uintptr_t l = a >> 6; l <= (a + bytes - 1) >> 6; l++) g_lines.push_back(l);
+}
+#define GPC_EMU_STATS 1
+#include "core.hpp"
+#include "gpc.h"
+
+using namespace gpc;
+
+extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out) {
+  Img im{blob, static_cast<const ImageHdr*>(hdr)};
+  for (size_t i = 0; i < n; i++) {
+    Pkt p;
+    const uint32_t src = pk->src[i], dst = pk->dst[i];
+    make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
+             pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, pk->ct_src ? pk->ct_src[i] : src,
+             pk->ct_dst ? pk->ct_dst[i] : dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+    g_lines.clear();
+    PacketOut o = classify_packet(im, p, pk->dest ? pk->dest[i] : 0u);
+    std::sort(g_lines.begin(), g_lines.end());
+    ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
+    ::gpc_emu_stats[7] += 1;                                                              // packets
+    uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);
+    w[0] = o.e.conj;
+    w[1] = o.e.packed;
+    w[2] = o.g.conj;
+    w[3] = o.g.packed;
+  }
+  return 0;
+}

@@ -1,0 +1,56 @@
+"""Loader for the TEST-ONLY host emulation library (tests/csrc/emu.cpp)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from antrea_amd import gpc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT, "libgpc_emu.so")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    src = os.path.join(HERE, "csrc", "emu.cpp")
+    core = os.path.join(ROOT, "antrea_amd", "csrc", "core.hpp")
+    os.makedirs(OUT, exist_ok=True)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(src), os.path.getmtime(core)):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"),
+                        "-I" + os.path.join(ROOT, "antrea_amd", "csrc"), src, "-o", LIB], check=True)
+    _lib = C.CDLL(LIB)
+    _lib.gpc_emu_stats_arr = (C.c_ulonglong * 8).in_dll(_lib, "gpc_emu_stats")
+    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p]
+    return _lib
+
+
+def classify(clf: "gpc.Classifier", cols):
+    """Emulated verdicts (n, 2) of the image last committed by `clf` (commit may fail with EDEV
+    on a host without GPU: the host image is built before the upload)."""
+    blob, nw, hdr, _ = clf.debug_image()
+    soa, keep, n = gpc.pkt_soa_host(cols)
+    out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
+    load().emu_classify(blob, hdr, C.byref(soa), n, out.ctypes.data)
+    return out.reshape(n, 2)
+
+
+def commit_host(clf: "gpc.Classifier"):
+    """gpc_commit that tolerates the missing device (image is still built)."""
+    rc = clf.lib.gpc_commit(clf.h)
+    if rc not in (0, -gpc.GPC_EDEV):
+        raise gpc.GpcError(rc, "gpc_commit")
+
+
+def stats(reset=False):
+    arr = load().gpc_emu_stats_arr
+    v = list(arr)
+    if reset:
+        for i in range(8):
+            arr[i] = 0
+    return v

@@ -1,0 +1,62 @@
+"""C-ABI library: loads, exports every gpc.h symbol, and its compiler realizes the reference's
+golden flow tables (CPU only -- no classify calls here)."""
+import copy
+import re
+import subprocess
+
+import pytest
+
+from antrea_amd import gpc
+from oracle import compiler as oc
+from tests.util import assign_tables, load_golden, normalize_flows
+
+GOLD = load_golden("np_batch_install.json")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from antrea_amd.build import build
+    build()
+
+
+def test_exports_every_header_symbol():
+    hdr = open(gpc.os.path.join(gpc.os.path.dirname(gpc.HERE), "include", "gpc.h")).read()
+    declared = set(re.findall(r"^(?:int|void|const char\*)\s+(gpc_\w+)\(", hdr, re.M))
+    assert declared == set(gpc.EXPORTS)
+    syms = subprocess.run(["nm", "-D", "--defined-only", gpc.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (gpc_\w+)", syms))
+    assert declared <= exported, declared - exported
+    lib = gpc.load()
+    assert lib.gpc_abi_version() == 1
+
+
+@pytest.mark.parametrize("case", GOLD["cases"], ids=[c["name"] for c in GOLD["cases"]])
+def test_batch_install_golden(case):
+    c = gpc.Classifier()
+    c.batch_install_policy_rule_flows(assign_tables(copy.deepcopy(case["rules"])))
+    got = normalize_flows(c.dump_flows())
+    want = normalize_flows(case["expected_flows"])
+    assert got == want, "\nmissing: %s\nextra: %s" % (sorted(want - got), sorted(got - want))
+
+
+@pytest.mark.parametrize("case", GOLD["cases"], ids=[c["name"] for c in GOLD["cases"]])
+def test_incremental_install_golden(case):
+    c = gpc.Classifier()
+    for r in assign_tables(copy.deepcopy(case["rules"])):
+        c.install_policy_rule_flows(r)
+    assert normalize_flows(c.dump_flows()) == normalize_flows(case["expected_flows"])
+
+
+def test_errors_mirror_reference():
+    c = gpc.Classifier()
+    with pytest.raises(gpc.GpcError) as e:
+        c.add_policy_rule_address(99, "src", ["10.0.0.1"])
+    assert e.value.code == gpc.GPC_ENOTFOUND  # ConjunctionNotFound
+    r = {"direction": "Out", "from": ["10.0.0.1"], "service": [{"protocol": "TCP", "port": 80}], "flow_id": 7,
+         "table": "EgressRule"}
+    c.install_policy_rule_flows(r)
+    with pytest.raises(gpc.GpcError) as e:
+        c.add_policy_rule_address(7, "dst", ["10.0.0.2"])
+    assert e.value.code == gpc.GPC_ENOCLAUSE  # "no clause is using addrType"
+    with pytest.raises(gpc.GpcError):
+        c.commit() if False else c.classify_host({})  # classify before commit -> error

@@ -1,0 +1,67 @@
+"""CPU tier: the product's image builder + evaluation core (host emulation of the kernel body)
+against the oracle classifier on the oracle-compiled flow set. Same verdict tuple as the GPU
+parity tests; small sizes so the pure-Python oracle finishes in seconds."""
+import copy
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from oracle import compiler as oc
+from oracle import ovs_cls
+from tests import emu
+
+
+def _small_c3(seed):
+    return workload.config3(seed=seed, n_policies_per_dir=6, rules_per_policy=8)
+
+
+def _small_c2(seed):
+    wl = workload.config2(seed=seed)
+    return wl
+
+
+WORKLOADS = {"C1": lambda s: workload.config1(seed=s), "C3s": _small_c3}
+
+
+def oracle_verdicts(rules, cols, n):
+    fnp = oc.FeatureNetworkPolicy()
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in rules}
+    pipe = ovs_cls.Pipeline(fnp.dump_flows(), tiers)
+    out = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
+    for i in range(n):
+        pkt = {k: int(v[i]) for k, v in cols.items()}
+        e, g = pipe.classify(pkt)
+        for j, v in enumerate((e, g)):
+            out[i, j] = (v[1], v[0], v[2], v[3], v[4])
+    return out, pipe
+
+
+def product_verdicts(rules, cols):
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    emu.commit_host(c)
+    return emu.classify(c, cols), c
+
+
+def _cmp(got, want, cols):
+    bad = np.nonzero(got != want)[0]
+    if len(bad):
+        i = bad[0]
+        pkt = {k: int(v[i]) for k, v in cols.items()}
+        raise AssertionError("%d/%d mismatches; first pkt %s\n product %s\n oracle  %s" % (
+            len(bad), len(got), pkt, got[i], want[i]))
+
+
+@pytest.mark.parametrize("name", sorted(WORKLOADS))
+@pytest.mark.parametrize("seed", [1, 2])
+def test_emu_vs_oracle(name, seed):
+    wl = WORKLOADS[name](seed)
+    n = 400
+    cols = workload.gen_packets(wl, n, seed=seed)
+    want, _ = oracle_verdicts(wl.rules, cols, n)
+    got, _ = product_verdicts(wl.rules, cols)
+    _cmp(got, want, cols)
