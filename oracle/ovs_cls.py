@@ -195,7 +195,7 @@ class Pipeline:
                     action = ACT_ALLOW
                     goto = metric
             else:
-                if goto is None:
+                if goto is None or goto == "Output":  # drop, or logging drop via packet-in
                     return ACT_ISOLATION_DROP, conj, tindex, flags, None
                 action = ACT_BYPASS
                 goto = metric
