@@ -40,54 +40,47 @@ enum Axis : uint8_t {
   AX_N = 11
 };
 
-enum SegKind : uint8_t { SEG_IVAL = 0, SEG_HASH = 1, SEG_BOX = 2, SEG_ALWAYS = 3 };
+// Per-rule record: uint32 words, 16-word (64-B) aligned, laid out in rank order, so a record's
+// word offset orders rules exactly like their rank (priority desc, hard first, conj id asc).
+//   w0 conj_id (0 for hard pseudo-rules)
+//   w1 priority | act_priority << 16
+//   w2 flags byte (RecFlags) | off0 << 8 | off1 << 16 | off2 << 24   (word offsets of the clauses)
+//   w3 counter slot
+//   w4 tier | rid << 8                                               (rid: image-wide rule id)
+// clause k at word off_k: nseg, then nseg segments, each a tag word kind | axis << 4 | n << 8
+// followed by its data:
+//   SK_IVAL  2n words, sorted disjoint [lo,hi]     SK_XIVAL  1 word: offset of the 2n words
+//   SK_PTS   n words, sorted points                SK_XPTS   1 word: offset of the n words
+//   SK_BOX   7n words (val[3], mask[3], axes|nt)   SK_XBOX   1 word: offset of the 7n words
+//   SK_HASH  no data: points live in the image-wide point hash, key (table, clause, axis, rid, v)
+//   SK_ALWAYS
+enum SegKind : uint8_t { SK_ALWAYS = 0, SK_IVAL = 1, SK_PTS = 2, SK_HASH = 3, SK_BOX = 4, SK_XIVAL = 5, SK_XPTS = 6, SK_XBOX = 7 };
 enum RuleKind : uint8_t { RK_SOFT = 0, RK_HARD = 1 };
 // What the table walk does with a rule's verdict.
 enum RVerdict : uint8_t { RV_MISS = 1, RV_ALLOW = 2, RV_DROP = 3, RV_REJECT = 4, RV_ISO_DROP = 5, RV_BYPASS = 6, RV_PASS = 7 };
-enum RuleFlags : uint8_t { RF_ACT = 1, RF_COUNTED = 2 };
+// w2 flag byte: verdict (bits 0-2) | kind (3) | has action flow (4) | counted (5) | n_clauses (6-7)
+GPC_HD uint32_t rec_verdict(uint32_t w2) { return w2 & 7u; }
+GPC_HD uint32_t rec_hard(uint32_t w2) { return (w2 >> 3) & 1u; }
+GPC_HD uint32_t rec_has_act(uint32_t w2) { return (w2 >> 4) & 1u; }
+GPC_HD uint32_t rec_counted(uint32_t w2) { return (w2 >> 5) & 1u; }
+GPC_HD uint32_t rec_nclauses(uint32_t w2) { return (w2 >> 6) & 3u; }
+GPC_HD uint32_t rec_off(uint32_t w2, uint32_t k) { return (w2 >> (8 + 8 * k)) & 0xffu; }
+constexpr uint32_t kRecHdrWords = 5;
+constexpr uint32_t kBoxWords = 7;
 
 constexpr int kMaxClauses = 3;
 constexpr int kIdxPerClause = 6;  // sub-indexes (axis, band) per driver clause
-constexpr uint32_t kNoIdx = 0xffffffffu;
-constexpr uint32_t kBuckets = 65536;
-
-struct RuleRec {  // 32 B
-  uint32_t conj_id;
-  uint16_t priority;
-  uint16_t act_priority;
-  uint8_t kind, n_clauses, verdict, flags;
-  uint8_t tier, nseg0, nseg1, nseg2;
-  uint32_t slot;
-  uint32_t seg_begin;
-  uint32_t reserved[2];
-};
-
-struct SegRec {  // 16 B
-  uint8_t axis, kind, clause, reserved;
-  uint32_t n;
-  uint32_t off;  // IVAL: word offset of n (lo,hi) pairs ; BOX: word offset of n BoxRec
-  uint32_t reserved2;
-};
-
-struct BoxRec {  // 32 B: AND of up to 3 masked terms
-  uint32_t val[3];
-  uint32_t mask[3];
-  uint8_t axis[3];
-  uint8_t nterms;
-  uint32_t reserved;
-};
 
 struct SubIdx {  // one (axis, band) bucket index of a driver clause
-  uint8_t axis, band, reserved[2];
-  uint32_t off;  // word offset of kBuckets+1 offsets (relative to entries base)
-  uint32_t ent;  // word offset of the rank entries
+  uint8_t axis, band, bits, reserved;
+  uint32_t off;  // word offset of 2^bits + 1 bucket offsets (relative to `ent`)
+  uint32_t ent;  // word offset of the entries (record offsets, ascending per bucket)
 };
 
 struct TableHdr {
   uint32_t n_rules, n_hard;
-  uint32_t rules_off;  // RuleRec array (word offset)
-  uint32_t hard_off;   // ranks of hard pseudo-rules (ascending)
-  uint32_t seg_off;    // SegRec array
+  uint32_t hard_off;  // record offsets of the hard pseudo-rules (ascending)
+  uint32_t end_off;   // larger than every record offset of this table ("no hard match")
   uint32_t always_off[2], always_n[2];
   uint32_t n_idx[2];
   SubIdx idx[2][kIdxPerClause];
@@ -142,20 +135,20 @@ GPC_HD uint32_t proto_class(uint32_t proto) {
     default: return 0;
   }
 }
-// Bands: IP axes 0 = prefix len 0..16 (top-16 bits), 1 = 17..24 (hash of top-24), 2 = 25..32
-// (hash of the address); exact axes (in_port, reg1, reg7, tun) band 0 = hash of the value;
-// L4 axes band 0 = proto class x port/8.
-GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t v) {
+// Bands: IP axes 0 = prefix len 0..16 (top-16 bits, exact), 1 = 17..24 (hash of top-24),
+// 2 = 25..32 (hash of the address); exact axes (in_port, reg1, reg7, tun) band 0 = low `bits`
+// bits of the value; L4 axes band 0 = proto class x port/8.
+GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t bits, uint32_t v) {
   if (axis <= AX_CTDST) {
     if (band == 0) return v >> 16;
-    if (band == 1) return mix32(v >> 8) & 0xffffu;
-    return mix32(v) & 0xffffu;
+    if (band == 1) return mix32(v >> 8) >> (32 - bits);
+    return mix32(v) >> (32 - bits);
   }
   if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
-  return mix32(v) & 0xffffu;
+  return v & ((1u << bits) - 1u);
 }
-GPC_HD uint64_t point_key(uint32_t table, uint32_t clause, uint32_t axis, uint32_t rank, uint32_t v) {
-  uint32_t hi = (table << 29) | (clause << 27) | (axis << 23) | (rank & 0x7fffffu);
+GPC_HD uint64_t point_key(uint32_t table, uint32_t clause, uint32_t axis, uint32_t rid, uint32_t v) {
+  uint32_t hi = (table << 29) | (clause << 27) | (axis << 23) | (rid & 0x7fffffu);
   return (uint64_t(hi) << 32) | v;
 }
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
@@ -164,9 +157,9 @@ GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0
 // ------------------------------------------------------------------------------ evaluation
 #ifdef GPC_EMU_STATS  // test-only instrumentation (tests/csrc/emu.cpp); never defined in the product build
 extern "C" unsigned long long gpc_emu_stats[8];
-extern "C" void gpc_emu_touch(const void* p, unsigned bytes);
+extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 #define GPC_STAT(i, v) (gpc_emu_stats[i] += (v))
-#define GPC_TOUCH(p, n) gpc_emu_touch((p), (n))
+#define GPC_TOUCH(p, n) gpc_emu_touch((p), (n), __LINE__)
 #else
 #define GPC_STAT(i, v) ((void)0)
 #define GPC_TOUCH(p, n) ((void)0)
@@ -193,68 +186,96 @@ GPC_HD bool hash_contains(const Img& im, uint64_t key) {
   return hit;
 }
 
-GPC_HD bool seg_match(const Img& im, uint32_t table, uint32_t rank, const SegRec& s, const Pkt& p) {
-  switch (s.kind) {
-    case SEG_ALWAYS:
-      return true;
-    case SEG_IVAL: {
-      const uint32_t v = p.ax[s.axis];
-      const uint32_t* iv = im.blob + s.off;
-      uint32_t n = s.n;
-      if (n <= 8) {
-        for (uint32_t i = 0; i < n; i++) {
-          GPC_TOUCH(iv + 2 * i, 8);
-          if (v < iv[2 * i]) return false;
-          if (v <= iv[2 * i + 1]) return true;
-        }
-        return false;
-      }
-      uint32_t lo = 0, hi = n;  // first interval with lo > v
-      while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        GPC_TOUCH(iv + 2 * mid, 8);
-        if (iv[2 * mid] <= v) lo = mid + 1;
-        else hi = mid;
-      }
-      return lo > 0 && v <= iv[2 * (lo - 1) + 1];
+GPC_HD bool ival_hit(const uint32_t* iv, uint32_t n, uint32_t v) {
+  if (n <= 8) {
+    for (uint32_t i = 0; i < n; i++) {
+      GPC_TOUCH(iv + 2 * i, 8);
+      if (v < iv[2 * i]) return false;
+      if (v <= iv[2 * i + 1]) return true;
     }
-    case SEG_HASH:
-      return hash_contains(im, point_key(table, s.clause, s.axis, rank, p.ax[s.axis]));
-    case SEG_BOX: {
-      const BoxRec* bx = reinterpret_cast<const BoxRec*>(im.blob + s.off);
-      for (uint32_t i = 0; i < s.n; i++) {
-        const BoxRec& b = bx[i];
-        GPC_TOUCH(&b, sizeof(BoxRec));
-        bool ok = true;
-        for (int t = 0; t < b.nterms; t++) ok &= (p.ax[b.axis[t]] & b.mask[t]) == b.val[t];
-        if (ok) return true;
-      }
-      return false;
+    return false;
+  }
+  uint32_t lo = 0, hi = n;  // first interval with lo > v
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    GPC_TOUCH(iv + 2 * mid, 8);
+    if (iv[2 * mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo > 0 && v <= iv[2 * (lo - 1) + 1];
+}
+
+GPC_HD bool pts_hit(const uint32_t* pt, uint32_t n, uint32_t v) {
+  if (n <= 16) {
+    for (uint32_t i = 0; i < n; i++) {
+      GPC_TOUCH(pt + i, 4);
+      if (pt[i] >= v) return pt[i] == v;
     }
+    return false;
+  }
+  uint32_t lo = 0, hi = n;  // first point >= v
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    GPC_TOUCH(pt + mid, 4);
+    if (pt[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && pt[lo] == v;
+}
+
+GPC_HD bool box_hit(const uint32_t* bx, uint32_t n, const Pkt& p) {
+  for (uint32_t i = 0; i < n; i++, bx += kBoxWords) {
+    GPC_TOUCH(bx, kBoxWords * 4);
+    const uint32_t meta = bx[6];
+    const uint32_t nt = meta >> 24;
+    bool ok = true;
+    for (uint32_t t = 0; t < nt; t++) ok &= (p.ax[(meta >> (8 * t)) & 0xffu] & bx[3 + t]) == bx[t];
+    if (ok) return true;
   }
   return false;
 }
 
-GPC_HD bool rule_match(const Img& im, uint32_t table, const TableHdr& th, uint32_t rank, const RuleRec& r, const Pkt& p) {
-  const SegRec* segs = reinterpret_cast<const SegRec*>(im.blob + th.seg_off) + r.seg_begin;
-  uint32_t nseg[3] = {r.nseg0, r.nseg1, r.nseg2};
-  uint32_t s = 0;
-  for (uint32_t k = 0; k < r.n_clauses; k++) {
-    bool ok = false;
-    for (uint32_t j = 0; j < nseg[k] && !ok; j++) {
-      GPC_TOUCH(&segs[s + j], sizeof(SegRec));
-      ok = seg_match(im, table, rank, segs[s + j], p);
+// One clause of the record at `rec` (OR of its segments).
+GPC_HD bool clause_match(const Img& im, uint32_t table, uint32_t k, uint32_t rid, const uint32_t* c, const Pkt& p) {
+  GPC_TOUCH(c, 4);
+  const uint32_t nseg = c[0];
+  const uint32_t* w = c + 1;
+  for (uint32_t s = 0; s < nseg; s++) {
+    GPC_TOUCH(w, 4);
+    const uint32_t tag = *w++;
+    const uint32_t kind = tag & 0xfu, axis = (tag >> 4) & 0xfu, n = tag >> 8;
+    bool hit;
+    switch (kind) {
+      case SK_ALWAYS: return true;
+      case SK_IVAL: hit = ival_hit(w, n, p.ax[axis]); w += 2 * n; break;
+      case SK_PTS: hit = pts_hit(w, n, p.ax[axis]); w += n; break;
+      case SK_HASH: hit = hash_contains(im, point_key(table, k, axis, rid, p.ax[axis])); break;
+      case SK_BOX: hit = box_hit(w, n, p); w += kBoxWords * n; break;
+      case SK_XIVAL: GPC_TOUCH(w, 4); hit = ival_hit(im.blob + *w, n, p.ax[axis]); w++; break;
+      case SK_XPTS: GPC_TOUCH(w, 4); hit = pts_hit(im.blob + *w, n, p.ax[axis]); w++; break;
+      case SK_XBOX: GPC_TOUCH(w, 4); hit = box_hit(im.blob + *w, n, p); w++; break;
+      default: hit = false; break;
     }
-    if (!ok) return false;
-    s += nseg[k];
+    if (hit) return true;
   }
+  return false;
+}
+
+// All clauses of a record; clause `last` (the driver, already a likely hit) is checked last.
+GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint32_t w2, uint32_t rid, uint32_t last,
+                       const Pkt& p) {
+  const uint32_t ncl = rec_nclauses(w2);
+  for (uint32_t k = 0; k < ncl; k++) {
+    if (k == last) continue;
+    if (!clause_match(im, table, k, rid, rec + rec_off(w2, k), p)) return false;
+  }
+  if (last < ncl && !clause_match(im, table, last, rid, rec + rec_off(w2, last), p)) return false;
   return true;
 }
 
 // One rule table (table = 1..6).
 GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   const TableHdr& th = im.hdr->t[table - 1];
-  const RuleRec* rules = reinterpret_cast<const RuleRec*>(im.blob + th.rules_off);
   TableResult res;
   res.verdict = RV_MISS;
   res.tie = 0;
@@ -263,48 +284,47 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   res.conj = 0;
   res.slot = 0;
   // --- hard pseudo-rules (few): best hard match H
-  uint32_t rH = th.n_rules;
-  uint16_t hprio = 0;
-  uint8_t hverdict = RV_MISS;
+  uint32_t rH = th.end_off;
+  uint32_t hprio = 0, hverdict = RV_MISS;
   const uint32_t* hard = im.blob + th.hard_off;
   for (uint32_t h = 0; h < th.n_hard; h++) {
     GPC_TOUCH(&hard[h], 4);
-    uint32_t rank = hard[h];
-    GPC_TOUCH(&rules[rank], sizeof(RuleRec));
-    RuleRec r = rules[rank];
-    if (rH != th.n_rules) {  // tie among hard flows of equal priority and different verdicts
-      if (r.priority != hprio) break;
-      if (r.verdict != hverdict && rule_match(im, table, th, rank, r, p)) res.tie = 1;
+    const uint32_t off = hard[h];
+    const uint32_t* rec = im.blob + off;
+    GPC_TOUCH(rec, 4 * kRecHdrWords);
+    const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
+    if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
+      if ((w1 & 0xffffu) != hprio) break;
+      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, p)) res.tie = 1;
       continue;
     }
-    if (rule_match(im, table, th, rank, r, p)) {
-      rH = rank;
-      hprio = r.priority;
-      hverdict = r.verdict;
+    if (rule_match(im, table, rec, w2, rid, 3, p)) {
+      rH = off;
+      hprio = w1 & 0xffffu;
+      hverdict = rec_verdict(w2);
     }
   }
-  // --- driver clause: the one with fewer candidate ranks
+  // --- driver clause: the one with fewer candidate records
   uint32_t cnt[2] = {0, 0};
-  uint32_t bk[2][kIdxPerClause];
-  const uint32_t* offs[2][kIdxPerClause];
+  uint32_t lo_[2][kIdxPerClause], hi_[2][kIdxPerClause];
   for (int k = 0; k < 2; k++) {
     cnt[k] = th.always_n[k];
     for (uint32_t i = 0; i < th.n_idx[k]; i++) {
       const SubIdx& si = th.idx[k][i];
-      uint32_t b = bucket_of(si.axis, si.band, p.ax[si.axis]);
+      const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
       const uint32_t* o = im.blob + si.off;
-      bk[k][i] = b;
-      offs[k][i] = o;
       GPC_TOUCH(o + b, 8);
-      cnt[k] += o[b + 1] - o[b];
+      lo_[k][i] = o[b];
+      hi_[k][i] = o[b + 1];
+      cnt[k] += hi_[k][i] - lo_[k][i];
     }
   }
   int d = cnt[1] < cnt[0] ? 1 : 0;
-  GPC_STAT(0, 1);
-  GPC_STAT(1, cnt[d]);
-  GPC_STAT(2, cnt[1 - d]);
   if (th.n_idx[0] == 0 && th.always_n[0] == 0 && th.n_idx[1] == 0 && th.always_n[1] == 0) d = -1;  // no soft rules
-  // k-way merge of the driver lists (ascending rank = descending priority)
+  GPC_STAT(0, 1);
+  GPC_STAT(1, d >= 0 ? cnt[d] : 0);
+  GPC_STAT(2, d >= 0 ? cnt[1 - d] : 0);
+  // k-way merge of the driver lists (ascending record offset = descending priority)
   const uint32_t* cur[kIdxPerClause + 1];
   const uint32_t* end[kIdxPerClause + 1];
   int nl = 0;
@@ -316,17 +336,16 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     }
     for (uint32_t i = 0; i < th.n_idx[d]; i++) {
       const uint32_t* ent = im.blob + th.idx[d][i].ent;
-      uint32_t b = bk[d][i];
-      cur[nl] = ent + offs[d][i][b];
-      end[nl] = ent + offs[d][i][b + 1];
+      cur[nl] = ent + lo_[d][i];
+      end[nl] = ent + hi_[d][i];
       if (cur[nl] != end[nl]) nl++;
     }
   }
   uint32_t last = 0xffffffffu;
-  int have = 0;            // result found
+  int have = 0;             // result found
   uint32_t level = 0xffffffffu;
-  uint32_t level_done = 0; // completed conjunctions at the current level
-  uint32_t win = 0;        // winner rank (soft) when have == 1 and !use_h
+  uint32_t level_done = 0;  // completed conjunctions at the current level
+  uint32_t win = 0;         // winner record offset (soft) when have == 1 and !use_h
   int use_h = 0;
   while (true) {
     uint32_t best = 0xffffffffu;
@@ -334,7 +353,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     for (int l = 0; l < nl; l++) {
       if (cur[l] < end[l]) {
         GPC_TOUCH(cur[l], 4);
-        uint32_t r = *cur[l];
+        const uint32_t r = *cur[l];
         if (r < best) {
           best = r;
           bi = l;
@@ -345,41 +364,44 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     cur[bi]++;
     if (best == last) continue;
     last = best;
-    GPC_TOUCH(&rules[best], sizeof(RuleRec));
-    RuleRec r = rules[best];
-    if (r.priority != level) {
+    const uint32_t* rec = im.blob + best;
+    GPC_TOUCH(rec, 4 * kRecHdrWords);
+    const uint32_t w1 = rec[1], w2 = rec[2];
+    const uint32_t prio = w1 & 0xffffu;
+    if (prio != level) {
       if (have) break;  // winning level finished
-      level = r.priority;
+      level = prio;
       level_done = 0;
     }
     GPC_STAT(3, 1);
-    if (!rule_match(im, table, th, best, r, p)) continue;
+    if (!rule_match(im, table, rec, w2, rec[4] >> 8, uint32_t(d), p)) continue;
     level_done++;
     if (have) {  // a second completion at the winning level
       res.tie = 1;
       break;
     }
-    if (r.flags & RF_ACT) {
+    if (rec_has_act(w2)) {
       have = 1;
-      use_h = (rH != th.n_rules && hprio > r.act_priority) ? 1 : 0;
+      use_h = (rH != th.end_off && hprio > (w1 >> 16)) ? 1 : 0;
       win = best;
-    } else if (rH != th.n_rules) {
+    } else if (rH != th.end_off) {
       have = 1;
       use_h = 1;
     }
   }
   if (have && !use_h) {
-    RuleRec r = rules[win];
-    res.verdict = r.verdict;
-    res.conj = r.conj_id;
-    res.tier = r.tier;
-    res.counted = (r.flags & RF_COUNTED) ? 1 : 0;
-    res.slot = r.slot;
+    const uint32_t* rec = im.blob + win;
+    const uint32_t w2 = rec[2];
+    res.verdict = uint8_t(rec_verdict(w2));
+    res.conj = rec[0];
+    res.tier = uint8_t(rec[4] & 0xffu);
+    res.counted = uint8_t(rec_counted(w2));
+    res.slot = rec[3];
     if (level_done > 1) res.tie = 1;
     return res;
   }
-  if (rH != th.n_rules) {
-    res.verdict = hverdict;
+  if (rH != th.end_off) {
+    res.verdict = uint8_t(hverdict);
     if (have && level_done > 1) res.tie = 1;
   }
   return res;

@@ -163,54 +163,40 @@ uint8_t action_verdict(const Flow& f, bool* ok) {  // conj_id flows and hard flo
 }
 
 // Segment builder ------------------------------------------------------------------------------
-struct Blob {
-  std::vector<uint32_t> w;
-  uint32_t align(uint32_t words) {
-    while (w.size() % words) w.push_back(0);
-    return uint32_t(w.size());
-  }
-  template <class T>
-  uint32_t put(const T* p, size_t n, uint32_t align_words) {
-    uint32_t off = align(align_words);
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(p);
-    w.insert(w.end(), s, s + n * sizeof(T) / 4);
-    return off;
-  }
-};
-
-constexpr uint32_t kHashMinPoints = 16;
+constexpr uint32_t kHashMinPoints = 64;   // > 64 points: image-wide point hash
+constexpr uint32_t kInlinePoints = 16;    // <= 16 points inline in the record
+constexpr uint32_t kInlineIvals = 6;      // <= 6 intervals inline
+constexpr uint32_t kInlineBoxes = 2;
 
 struct PendingSeg {
-  SegRec s;
-  std::vector<uint32_t> ival;   // lo,hi pairs
-  std::vector<BoxRec> boxes;
-  std::vector<uint32_t> points;
+  uint8_t kind = SK_ALWAYS, axis = 0;
+  std::vector<uint32_t> data;  // IVAL: lo,hi pairs ; PTS / HASH: points ; BOX: 7 words per box
+  uint32_t n = 0;
 };
 
-void clause_segments(const std::vector<Atom>& atoms, uint8_t clause, std::vector<PendingSeg>* out) {
+void clause_segments(const std::vector<Atom>& atoms, std::vector<PendingSeg>* out) {
   for (auto& a : atoms)
     if (a.t.empty()) {
-      PendingSeg ps{};
-      ps.s.kind = SEG_ALWAYS;
-      ps.s.clause = clause;
-      out->push_back(ps);
+      out->push_back(PendingSeg());  // SK_ALWAYS
       return;
     }
   std::map<uint8_t, std::vector<std::pair<uint32_t, uint32_t>>> by_axis;
-  std::vector<BoxRec> boxes;
+  PendingSeg boxes;
+  boxes.kind = SK_BOX;
   for (auto& a : atoms) {
     if (a.t.size() == 1 && is_prefix(a.t[0].mask)) {
       uint32_t lo = a.t[0].val & a.t[0].mask, hi = lo | ~a.t[0].mask;
       by_axis[a.t[0].axis].push_back({lo, hi});
     } else {
-      BoxRec b{};
-      b.nterms = uint8_t(a.t.size());
+      uint32_t w[kBoxWords] = {0, 0, 0, 0, 0, 0, 0};
       for (size_t i = 0; i < a.t.size(); i++) {
-        b.axis[i] = a.t[i].axis;
-        b.val[i] = a.t[i].val & a.t[i].mask;
-        b.mask[i] = a.t[i].mask;
+        w[i] = a.t[i].val & a.t[i].mask;
+        w[3 + i] = a.t[i].mask;
+        w[6] |= uint32_t(a.t[i].axis) << (8 * i);
       }
-      boxes.push_back(b);
+      w[6] |= uint32_t(a.t.size()) << 24;
+      boxes.data.insert(boxes.data.end(), w, w + kBoxWords);
+      boxes.n++;
     }
   }
   for (auto& kv : by_axis) {
@@ -226,39 +212,80 @@ void clause_segments(const std::vector<Atom>& atoms, uint8_t clause, std::vector
     }
     bool points = true;
     for (auto& x : merged) points &= x.first == x.second;
-    PendingSeg ps{};
-    ps.s.axis = kv.first;
-    ps.s.clause = clause;
-    if (points && merged.size() > kHashMinPoints) {
-      ps.s.kind = SEG_HASH;
-      ps.s.n = uint32_t(merged.size());
-      for (auto& x : merged) ps.points.push_back(x.first);
+    PendingSeg ps;
+    ps.axis = kv.first;
+    ps.n = uint32_t(merged.size());
+    if (points) {
+      ps.kind = merged.size() > kHashMinPoints ? SK_HASH : SK_PTS;
+      for (auto& x : merged) ps.data.push_back(x.first);
     } else {
-      ps.s.kind = SEG_IVAL;
-      ps.s.n = uint32_t(merged.size());
+      ps.kind = SK_IVAL;
       for (auto& x : merged) {
-        ps.ival.push_back(x.first);
-        ps.ival.push_back(x.second);
+        ps.data.push_back(x.first);
+        ps.data.push_back(x.second);
       }
     }
     out->push_back(std::move(ps));
   }
-  if (!boxes.empty()) {
-    PendingSeg ps{};
-    ps.s.kind = SEG_BOX;
-    ps.s.clause = clause;
-    ps.s.n = uint32_t(boxes.size());
-    ps.boxes = std::move(boxes);
-    out->push_back(std::move(ps));
-  }
+  if (boxes.n) out->push_back(std::move(boxes));
+  std::stable_sort(out->begin(), out->end(), [](const PendingSeg& a, const PendingSeg& b) {
+    return a.data.size() < b.data.size();  // cheapest segment first
+  });
 }
 
+// Encodes one clause: returns its words; external data goes to `ext` with its patch positions
+// (word index inside the clause) recorded in `patches` (clause-relative position, ext offset).
+std::vector<uint32_t> encode_clause(const std::vector<PendingSeg>& segs, std::vector<uint32_t>* ext,
+                                    std::vector<std::pair<uint32_t, uint32_t>>* patches) {
+  std::vector<uint32_t> w;
+  w.push_back(uint32_t(segs.size()));
+  for (auto& s : segs) {
+    uint32_t kind = s.kind;
+    bool external = (kind == SK_IVAL && s.n > kInlineIvals) || (kind == SK_PTS && s.n > kInlinePoints) ||
+                    (kind == SK_BOX && s.n > kInlineBoxes);
+    if (external) kind = kind == SK_IVAL ? SK_XIVAL : kind == SK_PTS ? SK_XPTS : SK_XBOX;
+    w.push_back(kind | (uint32_t(s.axis) << 4) | (s.n << 8));
+    if (kind == SK_ALWAYS || kind == SK_HASH) continue;
+    if (external) {
+      while (ext->size() % 16) ext->push_back(0);
+      patches->push_back({uint32_t(w.size()), uint32_t(ext->size())});
+      w.push_back(0);
+      ext->insert(ext->end(), s.data.begin(), s.data.end());
+    } else {
+      w.insert(w.end(), s.data.begin(), s.data.end());
+    }
+  }
+  return w;
+}
+
+// Image blob (uint32 words) ------------------------------------------------------------------------
+struct Blob {
+  std::vector<uint32_t> w;
+  void align(size_t words) {
+    while (w.size() % words) w.push_back(0);
+  }
+  template <typename T>
+  uint32_t put(const T* p, size_t n, size_t align_words) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized elements");
+    align(align_words);
+    uint32_t off = uint32_t(w.size());
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    w.insert(w.end(), q, q + n * (sizeof(T) / 4));
+    return off;
+  }
+};
+
 // Driver index -----------------------------------------------------------------------------------
-constexpr uint32_t kMaxBucketsPerAtom = 1024;
+constexpr uint64_t kMaxBucketsPerAtom = 1024;
 const uint8_t kAxisPref[AX_N] = {AX_SRC, AX_DST, AX_CTSRC, AX_CTDST, AX_REG1, AX_INPORT, AX_REG7, AX_TUN, AX_L4D, AX_L4S, AX_CTST};
 
-// Buckets of one atom for the driver index; false = index it in the always list.
-bool atom_buckets(const Atom& a, uint8_t* axis, uint8_t* band, std::vector<uint32_t>* bks) {
+struct AtomKey {  // an atom's primary term as seen by the driver index
+  uint8_t axis, band;
+  uint32_t lo, hi;
+};
+
+// false = index it in the always list
+bool atom_key(const Atom& a, AtomKey* k) {
   if (a.t.empty()) return false;
   const Term* pt = nullptr;
   for (uint8_t ax : kAxisPref) {
@@ -267,38 +294,52 @@ bool atom_buckets(const Atom& a, uint8_t* axis, uint8_t* band, std::vector<uint3
     if (pt) break;
   }
   if (!pt || pt->axis == AX_CTST) return false;
-  uint32_t mk = pt->mask;
-  int L = leading_ones(mk);
-  uint32_t cov_mask = prefix_mask(L);
-  uint32_t lo = pt->val & cov_mask, hi = lo | ~cov_mask;
-  *axis = pt->axis;
-  bks->clear();
+  int L = leading_ones(pt->mask);
+  uint32_t cov = prefix_mask(L);
+  k->axis = pt->axis;
+  k->lo = pt->val & cov;
+  k->hi = k->lo | ~cov;
   if (pt->axis <= AX_CTDST) {
-    if (L <= 16) {
-      *band = 0;
-      uint64_t n = (uint64_t(hi >> 16) - (lo >> 16)) + 1;
-      if (n > kMaxBucketsPerAtom) return false;
-      for (uint32_t b = lo >> 16; b <= (hi >> 16); b++) bks->push_back(b);
-    } else if (L <= 24) {
-      *band = 1;
-      for (uint32_t t = lo >> 8; t <= (hi >> 8); t++) bks->push_back(mix32(t) & 0xffffu);
-    } else {
-      *band = 2;
-      for (uint64_t v = lo; v <= hi; v++) bks->push_back(mix32(uint32_t(v)) & 0xffffu);
-    }
+    k->band = L <= 16 ? 0 : L <= 24 ? 1 : 2;
+    if (k->band == 0 && (uint64_t(k->hi >> 16) - (k->lo >> 16) + 1) > kMaxBucketsPerAtom) return false;
   } else if (pt->axis == AX_L4D || pt->axis == AX_L4S) {
-    *band = 0;
-    if ((lo >> 16) != (hi >> 16)) return false;
-    uint32_t pc = proto_class(lo >> 16) << 13;
-    uint32_t b0 = pc | ((lo & 0xffffu) >> 3), b1 = pc | ((hi & 0xffffu) >> 3);
-    if (b1 - b0 + 1 > kMaxBucketsPerAtom) return false;
-    for (uint32_t b = b0; b <= b1; b++) bks->push_back(b);
+    k->band = 0;
+    if ((k->lo >> 16) != (k->hi >> 16)) return false;
+    if ((((k->hi & 0xffffu) >> 3) - ((k->lo & 0xffffu) >> 3) + 1) > kMaxBucketsPerAtom) return false;
   } else {
-    *band = 0;
-    if (uint64_t(hi) - lo >= 128) return false;
-    for (uint64_t v = lo; v <= hi; v++) bks->push_back(mix32(uint32_t(v)) & 0xffffu);
+    k->band = 0;
+    if (uint64_t(k->hi) - k->lo >= 128) return false;
   }
   return true;
+}
+
+uint64_t atom_span(const AtomKey& k) {  // number of bucket-key values the atom covers
+  if (k.axis <= AX_CTDST) {
+    if (k.band == 0) return (k.hi >> 16) - (k.lo >> 16) + 1;
+    if (k.band == 1) return (k.hi >> 8) - (k.lo >> 8) + 1;
+  }
+  if (k.axis == AX_L4D || k.axis == AX_L4S) return ((k.hi & 0xffffu) >> 3) - ((k.lo & 0xffffu) >> 3) + 1;
+  return uint64_t(k.hi) - k.lo + 1;
+}
+
+void atom_bucket_list(const AtomKey& k, uint32_t bits, std::vector<uint32_t>* out) {
+  out->clear();
+  if (k.axis <= AX_CTDST) {
+    if (k.band == 0) {
+      for (uint32_t b = k.lo >> 16; b <= (k.hi >> 16); b++) out->push_back(b);
+    } else if (k.band == 1) {
+      for (uint32_t t = k.lo >> 8; t <= (k.hi >> 8); t++) out->push_back(bucket_of(k.axis, 1, bits, t << 8));
+    } else {
+      for (uint64_t v = k.lo; v <= k.hi; v++) out->push_back(bucket_of(k.axis, 2, bits, uint32_t(v)));
+    }
+  } else if (k.axis == AX_L4D || k.axis == AX_L4S) {
+    uint32_t b0 = bucket_of(k.axis, 0, 16, k.lo), b1 = bucket_of(k.axis, 0, 16, k.hi);
+    for (uint32_t b = b0; b <= b1; b++) out->push_back(b);
+  } else {
+    for (uint64_t v = k.lo; v <= k.hi; v++) out->push_back(bucket_of(k.axis, 0, bits, uint32_t(v)));
+  }
+  std::sort(out->begin(), out->end());
+  out->erase(std::unique(out->begin(), out->end()), out->end());
 }
 
 bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vector<uint64_t>* tab) {
@@ -428,11 +469,12 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       if (ar == 0) r.clause[0].push_back(a);
     }
   }
-  // ---- 2. per table: rank, emit
+  // ---- 2. per table: rank, emit records, driver indexes
   Blob B;
   B.w.reserve(1 << 20);
-  B.w.push_back(0);  // keep offset 0 unused
+  for (int i = 0; i < 16; i++) B.w.push_back(0);  // keep offset 0 unused
   std::vector<uint64_t> hash_keys;
+  uint32_t next_rid = 0;
   for (int t = 1; t <= 6; t++) {
     std::vector<RuleB*> rs;
     for (auto& kv : hard[t])
@@ -457,89 +499,114 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     });
     TableHdr& th = out->hdr.t[t - 1];
     th.n_rules = uint32_t(rs.size());
-    std::vector<RuleRec> recs(rs.size());
-    std::vector<SegRec> segs;
-    std::vector<uint32_t> hard_ranks;
+    // records (rank order), then this table's external data
+    std::vector<uint32_t> rec_off(rs.size());
+    std::vector<uint32_t> ext;
+    std::vector<std::pair<uint32_t, uint32_t>> abs_patches;  // (absolute record word, ext offset)
+    std::vector<uint32_t> hard_offs;
     for (size_t rank = 0; rank < rs.size(); rank++) {
       RuleB& r = *rs[rank];
-      RuleRec& rec = recs[rank];
-      std::memset(&rec, 0, sizeof rec);
-      rec.conj_id = r.hard ? 0 : r.conj_id;
-      rec.priority = r.prio;
-      rec.act_priority = r.act_prio;
-      rec.kind = r.hard ? RK_HARD : RK_SOFT;
-      rec.n_clauses = r.n;
-      rec.verdict = r.verdict;
-      rec.flags = uint8_t((r.has_act ? RF_ACT : 0) | (r.counted ? RF_COUNTED : 0));
-      rec.tier = r.tier;
-      rec.slot = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0;
-      rec.seg_begin = uint32_t(segs.size());
-      if (r.hard) hard_ranks.push_back(uint32_t(rank));
-      uint8_t* nseg[3] = {&rec.nseg0, &rec.nseg1, &rec.nseg2};
+      uint32_t rid = next_rid++;
+      if (rid >= (1u << 23)) {
+        out->error = "too many rules for the point-hash key";
+        return -GPC_EINVAL;
+      }
+      // encode clauses, smallest first in the record
+      std::vector<std::vector<uint32_t>> cw(r.n);
+      std::vector<std::vector<std::pair<uint32_t, uint32_t>>> cp(r.n);
       for (int k = 0; k < r.n; k++) {
         std::vector<PendingSeg> ps;
-        clause_segments(r.clause[k], uint8_t(k), &ps);
-        std::stable_sort(ps.begin(), ps.end(), [](const PendingSeg& a, const PendingSeg& b) {
-          static const int order[4] = {1, 2, 3, 0};  // ALWAYS first, then IVAL, HASH, BOX
-          return order[a.s.kind] < order[b.s.kind];
-        });
-        if (ps.size() > 255) {
-          out->error = "too many segments in a clause";
+        clause_segments(r.clause[k], &ps);
+        for (auto& sg : ps)
+          if (sg.kind == SK_HASH)
+            for (uint32_t v : sg.data) hash_keys.push_back(point_key(uint32_t(t), uint32_t(k), sg.axis, rid, v));
+        cw[k] = encode_clause(ps, &ext, &cp[k]);
+      }
+      std::vector<int> order(r.n);
+      for (int k = 0; k < r.n; k++) order[k] = k;
+      std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cw[a].size() < cw[b].size(); });
+      B.align(16);
+      uint32_t base = uint32_t(B.w.size());
+      std::vector<uint32_t> rec(kRecHdrWords, 0);
+      uint32_t offs[3] = {0, 0, 0};
+      for (int k : order) {
+        if (rec.size() > 255) {
+          out->error = "rule record too large";
           return -GPC_EINVAL;
         }
-        *nseg[k] = uint8_t(ps.size());
-        for (auto& p : ps) {
-          SegRec s = p.s;
-          if (p.s.kind == SEG_IVAL) s.off = B.put(p.ival.data(), p.ival.size(), 2);
-          else if (p.s.kind == SEG_BOX) s.off = B.put(p.boxes.data(), p.boxes.size(), 8);
-          else if (p.s.kind == SEG_HASH)
-            for (uint32_t v : p.points) hash_keys.push_back(point_key(uint32_t(t), uint32_t(k), p.s.axis, uint32_t(rank), v));
-          segs.push_back(s);
-        }
+        offs[k] = uint32_t(rec.size());
+        for (auto& pt : cp[k]) abs_patches.push_back({base + uint32_t(rec.size()) + pt.first, pt.second});
+        rec.insert(rec.end(), cw[k].begin(), cw[k].end());
       }
+      rec[0] = r.hard ? 0 : r.conj_id;
+      rec[1] = uint32_t(r.prio) | (uint32_t(r.act_prio) << 16);
+      uint32_t flags = (r.verdict & 7u) | ((r.hard ? 1u : 0u) << 3) | ((r.has_act ? 1u : 0u) << 4) | ((r.counted ? 1u : 0u) << 5) |
+                       (uint32_t(r.n & 3) << 6);
+      rec[2] = flags | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
+      rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0;
+      rec[4] = uint32_t(r.tier) | (rid << 8);
+      rec_off[rank] = base;
+      B.w.insert(B.w.end(), rec.begin(), rec.end());
+      if (r.hard) hard_offs.push_back(base);
     }
-    th.n_hard = uint32_t(hard_ranks.size());
-    th.rules_off = recs.empty() ? 0 : B.put(recs.data(), recs.size(), 8);
-    th.hard_off = hard_ranks.empty() ? 0 : B.put(hard_ranks.data(), hard_ranks.size(), 1);
-    th.seg_off = segs.empty() ? 0 : B.put(segs.data(), segs.size(), 4);
+    B.align(16);
+    th.end_off = uint32_t(B.w.size()) + 1;
+    uint32_t ext_base = uint32_t(B.w.size());
+    B.w.insert(B.w.end(), ext.begin(), ext.end());
+    for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
+    th.n_hard = uint32_t(hard_offs.size());
+    th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
     // driver indexes for clauses 0 and 1 of the soft rules
     for (int k = 0; k < 2; k++) {
       std::vector<uint32_t> always;
-      std::map<std::pair<uint8_t, uint8_t>, std::vector<std::pair<uint32_t, uint32_t>>> sub;  // (axis,band) -> (bucket, rank)
-      std::vector<uint32_t> bks;
+      std::map<std::pair<uint8_t, uint8_t>, std::vector<std::pair<AtomKey, uint32_t>>> sub;  // (axis,band) -> (key, rec)
       for (size_t rank = 0; rank < rs.size(); rank++) {
         RuleB& r = *rs[rank];
-        if (r.hard) continue;
+        if (r.hard || k >= r.n) continue;
         for (auto& a : r.clause[k]) {
-          uint8_t axis = 0, band = 0;
-          if (!atom_buckets(a, &axis, &band, &bks)) {
-            always.push_back(uint32_t(rank));
+          AtomKey key;
+          if (!atom_key(a, &key)) {
+            always.push_back(rec_off[rank]);
             continue;
           }
-          auto& v = sub[{axis, band}];
-          for (uint32_t b : bks) v.push_back({b, uint32_t(rank)});
+          sub[{key.axis, key.band}].push_back({key, rec_off[rank]});
         }
       }
-      // the largest sub-indexes keep their index; extras fold into the always list
       std::vector<std::pair<size_t, std::pair<uint8_t, uint8_t>>> order;
       for (auto& kv : sub) order.push_back({kv.second.size(), kv.first});
       std::sort(order.rbegin(), order.rend());
       th.n_idx[k] = 0;
+      std::vector<uint32_t> bks;
       for (size_t i = 0; i < order.size(); i++) {
         auto& v = sub[order[i].second];
         if (i >= size_t(kIdxPerClause)) {
           for (auto& e : v) always.push_back(e.second);
           continue;
         }
-        std::sort(v.begin(), v.end());
-        v.erase(std::unique(v.begin(), v.end()), v.end());
-        std::vector<uint32_t> offs(kBuckets + 1, 0), ents(v.size());
-        for (auto& e : v) offs[e.first + 1]++;
-        for (uint32_t b = 0; b < kBuckets; b++) offs[b + 1] += offs[b];
-        for (size_t j = 0; j < v.size(); j++) ents[j] = v[j].second;  // sorted by (bucket, rank)
+        uint8_t axis = order[i].second.first, band = order[i].second.second;
+        uint32_t bits = 16;
+        if (axis <= AX_CTDST && band > 0) {  // hashed bands: ~2 buckets per entry
+          uint64_t ent = 0;
+          for (auto& e : v) ent += atom_span(e.first);
+          bits = 10;
+          while (bits < 22 && (1ull << bits) < 2 * ent) bits++;
+        }
+        std::vector<std::pair<uint32_t, uint32_t>> be;  // (bucket, record)
+        for (auto& e : v) {
+          atom_bucket_list(e.first, bits, &bks);
+          for (uint32_t b : bks) be.push_back({b, e.second});
+        }
+        std::sort(be.begin(), be.end());
+        be.erase(std::unique(be.begin(), be.end()), be.end());
+        uint32_t nb = 1u << bits;
+        std::vector<uint32_t> offs(size_t(nb) + 1, 0), ents(be.size());
+        for (auto& e : be) offs[e.first + 1]++;
+        for (uint32_t b = 0; b < nb; b++) offs[b + 1] += offs[b];
+        for (size_t j = 0; j < be.size(); j++) ents[j] = be[j].second;
         SubIdx& si = th.idx[k][th.n_idx[k]++];
-        si.axis = order[i].second.first;
-        si.band = order[i].second.second;
+        si.axis = axis;
+        si.band = band;
+        si.bits = uint8_t(bits);
         si.off = B.put(offs.data(), offs.size(), 16);
         si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
       }

@@ -9,10 +9,18 @@
 extern "C" {
 unsigned long long gpc_emu_stats[8];
 }
+#include <map>
 static std::vector<uintptr_t> g_lines;
-extern "C" void gpc_emu_touch(const void* p, unsigned bytes) {
+static std::map<uintptr_t, int> g_line_site;
+extern "C" {
+unsigned long long gpc_emu_site_lines[2048];
+}
+extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
   uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  for (uintptr_t l = a >> 6; l <= (a + bytes - 1) >> 6; l++) g_lines.push_back(l);
+  for (uintptr_t l = a >> 6; l <= (a + bytes - 1) >> 6; l++) {
+    g_lines.push_back(l);
+    g_line_site.emplace(l, site);
+  }
 }
 #define GPC_EMU_STATS 1
 #include "core.hpp"
@@ -29,10 +37,12 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const gpc_pkt
              pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, pk->ct_src ? pk->ct_src[i] : src,
              pk->ct_dst ? pk->ct_dst[i] : dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
     g_lines.clear();
+    g_line_site.clear();
     PacketOut o = classify_packet(im, p, pk->dest ? pk->dest[i] : 0u);
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
-    ::gpc_emu_stats[7] += 1;                                                              // packets
+    ::gpc_emu_stats[7] += 1;
+    for (auto& kv : g_line_site) gpc_emu_site_lines[kv.second & 2047]++;                                                              // packets
     uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);
     w[0] = o.e.conj;
     w[1] = o.e.packed;

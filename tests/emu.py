@@ -26,6 +26,7 @@ def load():
                         "-I" + os.path.join(ROOT, "antrea_amd", "csrc"), src, "-o", LIB], check=True)
     _lib = C.CDLL(LIB)
     _lib.gpc_emu_stats_arr = (C.c_ulonglong * 8).in_dll(_lib, "gpc_emu_stats")
+    _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
     _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p]
     return _lib
 
@@ -52,5 +53,14 @@ def stats(reset=False):
     v = list(arr)
     if reset:
         for i in range(8):
+            arr[i] = 0
+    return v
+
+
+def site_lines(reset=False):
+    arr = load().gpc_emu_site_arr
+    v = {i: arr[i] for i in range(2048) if arr[i]}
+    if reset:
+        for i in range(2048):
             arr[i] = 0
     return v
