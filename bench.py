@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--no-count", action="store_true", help="disable per-rule counters")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
     args = ap.parse_args()
 
     import torch
