@@ -41,7 +41,9 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, variant: str = "", defines=()) -> str:
+    """`variant`/`defines`: an experiment build of the kernel (libgpc_<variant>.so, selected at run
+    time with GPC_LIB); the default build is the product library."""
     os.makedirs(OUT, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "gpc.h")]
     objs = []
@@ -53,16 +55,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
         objs.append(obj)
     for s in HIP_SRCS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(OUT, s + ".o")
+        tag = "_" + variant if (variant and s.endswith(".hip")) else ""
+        obj = os.path.join(OUT, s + tag + ".o")
         if force or _newer(obj, [src] + hdrs):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            _run([HIPCC, "--offload-arch=" + ARCH] + CXXFLAGS + lang + ["-c", src, "-o", obj])
+            dfl = ["-D" + d for d in defines] if s.endswith(".hip") else []
+            _run([HIPCC, "--offload-arch=" + ARCH] + CXXFLAGS + dfl + lang + ["-c", src, "-o", obj])
         objs.append(obj)
-    if force or _newer(LIB, objs):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs)
+    lib = os.path.join(OUT, "libgpc_%s.so" % variant) if variant else LIB
+    if force or _newer(lib, objs):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
     if verbose:
-        print(LIB)
-    return LIB
+        print(lib)
+    return lib
 
 
 if __name__ == "__main__":

@@ -12,9 +12,15 @@
 
 namespace gpc {
 
-constexpr int kBlock = 256;
+#ifndef GPC_WAVES_PER_EU
+#define GPC_WAVES_PER_EU 4
+#endif
+#ifndef GPC_BLOCK
+#define GPC_BLOCK 256
+#endif
+constexpr int kBlock = GPC_BLOCK;
 
-__global__ __launch_bounds__(kBlock) void classify_kernel(const ImageHdr* __restrict__ hdr, const uint32_t* __restrict__ blob,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(const ImageHdr* __restrict__ hdr, const uint32_t* __restrict__ blob,
                                                           gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out,
                                                           unsigned long long* __restrict__ counters, int count) {
   uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;

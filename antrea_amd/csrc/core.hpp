@@ -71,10 +71,19 @@ constexpr uint32_t kBoxWords = 7;
 constexpr int kMaxClauses = 3;
 constexpr int kIdxPerClause = 6;  // sub-indexes (axis, band) per driver clause
 
+// Driver-index entry (8 B, uint2): x = record word offset | filter axis (low 4 bits; 15 = no IP
+// filter), y = Bloom filter of the rule's NON-driver clauses: bits 0-19 one IP / exact-axis clause
+// on axis (x & 15), bits 20-31 the service clause (proto class x 4096-port block of tp_dst).
+// A packet skips an entry without reading the record unless both parts intersect its own bits;
+// the filter is a necessary condition of the clauses, so skipping never changes a verdict.
+struct alignas(8) Ent {
+  uint32_t x, y;
+};
+
 struct SubIdx {  // one (axis, band) bucket index of a driver clause
   uint8_t axis, band, bits, reserved;
-  uint32_t off;  // word offset of 2^bits + 1 bucket offsets (relative to `ent`)
-  uint32_t ent;  // word offset of the entries (record offsets, ascending per bucket)
+  uint32_t off;  // word offset of 2^bits + 1 bucket offsets (in entries, relative to `ent`)
+  uint32_t ent;  // word offset (even) of the uint2 entries, ascending record offset per bucket
 };
 
 struct TableHdr {
@@ -96,6 +105,8 @@ struct ImageHdr {
 
 struct Pkt {
   uint32_t ax[AX_N];
+  uint32_t fm[8];  // filter bits of axes 0..7 (bits 0-19)
+  uint32_t l4m;    // filter bit of (proto class, tp_dst block) (bits 20-31)
 };
 
 struct TableResult {
@@ -153,6 +164,22 @@ GPC_HD uint64_t point_key(uint32_t table, uint32_t clause, uint32_t axis, uint32
 }
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
 GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0x9e3779b97f4a7c15ull) >> 32) & mask; }
+
+// Entry filter bits. IP axes: band 1/2/3 = prefix length 8-15 / 16-23 / 24-32 keyed by the top
+// 8 / 16 / 24 address bits; exact axes (in_port, reg1, reg7, tun_id): band 4 keyed by the value.
+constexpr uint32_t kFiltIpBits = 20, kFiltL4Shift = 20, kFiltL4Bits = 12;
+constexpr uint32_t kFiltNoAxis = 15u;
+constexpr uint32_t kFiltL4All = 0xfff00000u;
+GPC_HD uint32_t filt_ip_bit(uint32_t axis, uint32_t band, uint32_t key) {
+  return 1u << uint32_t((uint64_t(mix32(key ^ (axis << 24) ^ (band << 28))) * kFiltIpBits) >> 32);
+}
+GPC_HD uint32_t filt_l4_bit(uint32_t pclass, uint32_t block) {
+  return 1u << (kFiltL4Shift + uint32_t((uint64_t(mix32(((pclass << 4) | block) + 0x3c6ef372u)) * kFiltL4Bits) >> 32));
+}
+GPC_HD uint32_t filt_pkt_axis(uint32_t axis, uint32_t v) {
+  if (axis <= 3u) return filt_ip_bit(axis, 1, v >> 24) | filt_ip_bit(axis, 2, v >> 16) | filt_ip_bit(axis, 3, v >> 8);
+  return filt_ip_bit(axis, 4, v);
+}
 
 // ------------------------------------------------------------------------------ evaluation
 #ifdef GPC_EMU_STATS  // test-only instrumentation (tests/csrc/emu.cpp); never defined in the product build
@@ -273,7 +300,16 @@ GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint3
   return true;
 }
 
-// One rule table (table = 1..6).
+GPC_HD bool entry_pass(const Pkt& p, uint32_t x, uint32_t y) {
+  if ((y & p.l4m) == 0u) return false;
+  const uint32_t ax = x & 15u;
+  return ax == kFiltNoAxis || (y & p.fm[ax & 7u]) != 0u;
+}
+
+constexpr int kLists = kIdxPerClause + 1;  // always list + sub-indexes of the driver clause
+
+// One rule table (table = 1..6). All per-list merge state is indexed with compile-time indices
+// only (unrolled), so it stays in VGPRs.
 GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   const TableHdr& th = im.hdr->t[table - 1];
   TableResult res;
@@ -304,41 +340,60 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
       hverdict = rec_verdict(w2);
     }
   }
+  const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
+  if (n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
+    if (rH != th.end_off) res.verdict = uint8_t(hverdict);
+    return res;
+  }
   // --- driver clause: the one with fewer candidate records
-  uint32_t cnt[2] = {0, 0};
-  uint32_t lo_[2][kIdxPerClause], hi_[2][kIdxPerClause];
-  for (int k = 0; k < 2; k++) {
-    cnt[k] = th.always_n[k];
-    for (uint32_t i = 0; i < th.n_idx[k]; i++) {
-      const SubIdx& si = th.idx[k][i];
+  uint32_t lo0[kIdxPerClause], hi0[kIdxPerClause], lo1[kIdxPerClause], hi1[kIdxPerClause];
+  uint32_t cnt0 = th.always_n[0], cnt1 = th.always_n[1];
+#pragma unroll
+  for (int i = 0; i < kIdxPerClause; i++) {
+    lo0[i] = hi0[i] = lo1[i] = hi1[i] = 0;
+    if (uint32_t(i) < n0) {
+      const SubIdx& si = th.idx[0][i];
       const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
       const uint32_t* o = im.blob + si.off;
       GPC_TOUCH(o + b, 8);
-      lo_[k][i] = o[b];
-      hi_[k][i] = o[b + 1];
-      cnt[k] += hi_[k][i] - lo_[k][i];
+      lo0[i] = si.ent / 2 + o[b];
+      hi0[i] = si.ent / 2 + o[b + 1];
+      cnt0 += hi0[i] - lo0[i];
+    }
+    if (uint32_t(i) < n1) {
+      const SubIdx& si = th.idx[1][i];
+      const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
+      const uint32_t* o = im.blob + si.off;
+      GPC_TOUCH(o + b, 8);
+      lo1[i] = si.ent / 2 + o[b];
+      hi1[i] = si.ent / 2 + o[b + 1];
+      cnt1 += hi1[i] - lo1[i];
     }
   }
-  int d = cnt[1] < cnt[0] ? 1 : 0;
-  if (th.n_idx[0] == 0 && th.always_n[0] == 0 && th.n_idx[1] == 0 && th.always_n[1] == 0) d = -1;  // no soft rules
+  const bool d1 = cnt1 < cnt0;
+  const uint32_t d = d1 ? 1u : 0u;
   GPC_STAT(0, 1);
-  GPC_STAT(1, d >= 0 ? cnt[d] : 0);
-  GPC_STAT(2, d >= 0 ? cnt[1 - d] : 0);
+  GPC_STAT(1, d1 ? cnt1 : cnt0);
+  GPC_STAT(2, d1 ? cnt0 : cnt1);
   // k-way merge of the driver lists (ascending record offset = descending priority)
-  const uint32_t* cur[kIdxPerClause + 1];
-  const uint32_t* end[kIdxPerClause + 1];
-  int nl = 0;
-  if (d >= 0) {
-    if (th.always_n[d]) {
-      cur[nl] = im.blob + th.always_off[d];
-      end[nl] = cur[nl] + th.always_n[d];
-      nl++;
-    }
-    for (uint32_t i = 0; i < th.n_idx[d]; i++) {
-      const uint32_t* ent = im.blob + th.idx[d][i].ent;
-      cur[nl] = ent + lo_[d][i];
-      end[nl] = ent + hi_[d][i];
-      if (cur[nl] != end[nl]) nl++;
+  const Ent* E = reinterpret_cast<const Ent*>(im.blob);
+  uint32_t cur[kLists], end[kLists], hx[kLists], hy[kLists];
+  cur[0] = th.always_off[d] / 2;
+  end[0] = cur[0] + th.always_n[d];
+#pragma unroll
+  for (int i = 0; i < kIdxPerClause; i++) {
+    cur[i + 1] = d1 ? lo1[i] : lo0[i];
+    end[i + 1] = d1 ? hi1[i] : hi0[i];
+  }
+#pragma unroll
+  for (int l = 0; l < kLists; l++) {
+    hx[l] = 0xffffffffu;
+    hy[l] = 0;
+    if (cur[l] < end[l]) {
+      GPC_TOUCH(&E[cur[l]], 8);
+      const Ent e = E[cur[l]];
+      hx[l] = e.x;
+      hy[l] = e.y;
     }
   }
   uint32_t last = 0xffffffffu;
@@ -348,23 +403,47 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   uint32_t win = 0;         // winner record offset (soft) when have == 1 and !use_h
   int use_h = 0;
   while (true) {
-    uint32_t best = 0xffffffffu;
+    uint32_t bx = 0xffffffffu, by = 0;
     int bi = -1;
-    for (int l = 0; l < nl; l++) {
-      if (cur[l] < end[l]) {
-        GPC_TOUCH(cur[l], 4);
-        const uint32_t r = *cur[l];
-        if (r < best) {
-          best = r;
-          bi = l;
-        }
+#pragma unroll
+    for (int l = 0; l < kLists; l++) {
+      if (hx[l] < bx) {
+        bx = hx[l];
+        by = hy[l];
+        bi = l;
       }
     }
-    if (bi < 0 || best >= rH) break;
-    cur[bi]++;
-    if (best == last) continue;
-    last = best;
-    const uint32_t* rec = im.blob + best;
+    if (bi < 0 || (bx & ~15u) >= rH) break;
+    // advance the list the candidate came from: one load, selected by unrolled compares
+    uint32_t nc = 0, ne = 0;
+#pragma unroll
+    for (int l = 0; l < kLists; l++) {
+      if (l == bi) {
+        cur[l]++;
+        nc = cur[l];
+        ne = end[l];
+      }
+    }
+    Ent nx;
+    nx.x = 0xffffffffu;
+    nx.y = 0u;
+    if (nc < ne) {
+      GPC_TOUCH(&E[nc], 8);
+      nx = E[nc];
+    }
+#pragma unroll
+    for (int l = 0; l < kLists; l++) {
+      if (l == bi) {
+        hx[l] = nx.x;
+        hy[l] = nx.y;
+      }
+    }
+    if (bx == last) continue;
+    last = bx;
+    GPC_STAT(4, 1);
+    if (!entry_pass(p, bx, by)) continue;
+    const uint32_t off = bx & ~15u;
+    const uint32_t* rec = im.blob + off;
     GPC_TOUCH(rec, 4 * kRecHdrWords);
     const uint32_t w1 = rec[1], w2 = rec[2];
     const uint32_t prio = w1 & 0xffffu;
@@ -374,7 +453,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
       level_done = 0;
     }
     GPC_STAT(3, 1);
-    if (!rule_match(im, table, rec, w2, rec[4] >> 8, uint32_t(d), p)) continue;
+    if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, p)) continue;
     level_done++;
     if (have) {  // a second completion at the winning level
       res.tie = 1;
@@ -383,7 +462,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     if (rec_has_act(w2)) {
       have = 1;
       use_h = (rH != th.end_off && hprio > (w1 >> 16)) ? 1 : 0;
-      win = best;
+      win = off;
     } else if (rH != th.end_off) {
       have = 1;
       use_h = 1;
@@ -490,6 +569,9 @@ GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_
   p.ax[AX_L4D] = (proto << 16) | (ported ? dport : 0u);
   p.ax[AX_L4S] = (proto << 16) | (ported ? sport : 0u);
   p.ax[AX_CTST] = ct_state;
+#pragma unroll
+  for (uint32_t a = 0; a < 8; a++) p.fm[a] = filt_pkt_axis(a, p.ax[a]);
+  p.l4m = filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12);
 }
 
 }  // namespace gpc

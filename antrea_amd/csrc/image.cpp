@@ -342,6 +342,94 @@ void atom_bucket_list(const AtomKey& k, uint32_t bits, std::vector<uint32_t>* ou
   out->erase(std::unique(out->begin(), out->end()), out->end());
 }
 
+// Entry filter (core.hpp Ent): Bloom bits of the rule's non-driver clauses -------------------------
+// An IP / exact-axis term usable by the filter: returns false when it cannot be represented.
+bool filt_term_ip(const Term& t, uint32_t* bit) {
+  if (t.axis <= AX_CTDST) {
+    if (!is_prefix(t.mask)) return false;
+    int L = leading_ones(t.mask);
+    if (L < 8) return false;
+    uint32_t band = L < 16 ? 1 : L < 24 ? 2 : 3;
+    uint32_t shift = band == 1 ? 24 : band == 2 ? 16 : 8;
+    *bit = filt_ip_bit(t.axis, band, t.val >> shift);
+    return true;
+  }
+  if (t.axis >= AX_INPORT && t.axis <= AX_TUN) {
+    if (t.mask != 0xffffffffu) return false;
+    *bit = filt_ip_bit(t.axis, 4, t.val);
+    return true;
+  }
+  return false;
+}
+
+// IP part of one clause: all atoms must carry a usable term on one common axis.
+bool filt_clause_ip(const std::vector<Atom>& atoms, uint32_t* axis, uint32_t* bits) {
+  if (atoms.empty()) return false;
+  int ax = -1;
+  for (auto& t : atoms[0].t) {
+    uint32_t b;
+    if (filt_term_ip(t, &b)) {
+      ax = t.axis;
+      break;
+    }
+  }
+  if (ax < 0) return false;
+  uint32_t m = 0;
+  for (auto& a : atoms) {
+    bool found = false;
+    for (auto& t : a.t) {
+      uint32_t b;
+      if (t.axis == ax && filt_term_ip(t, &b)) {
+        m |= b;
+        found = true;
+        break;
+      }
+    }
+    if (!found) return false;
+  }
+  *axis = uint32_t(ax);
+  *bits = m;
+  return true;
+}
+
+// Service part of one clause: every atom needs a tp_dst (L4D) term.
+bool filt_clause_l4(const std::vector<Atom>& atoms, uint32_t* bits) {
+  if (atoms.empty()) return false;
+  uint32_t m = 0;
+  for (auto& a : atoms) {
+    const Term* l4 = nullptr;
+    for (auto& t : a.t)
+      if (t.axis == AX_L4D) l4 = &t;
+    if (!l4 || (l4->mask >> 16) != 0xffffu) return false;
+    uint32_t pc = proto_class(l4->val >> 16);
+    uint32_t pm = l4->mask & 0xffffu;
+    uint32_t lo = l4->val & pm & 0xffffu, hi = lo | (~pm & 0xffffu);
+    if (!is_prefix(l4->mask)) lo = 0, hi = 0xffffu;
+    for (uint32_t blk = lo >> 12; blk <= (hi >> 12); blk++) m |= filt_l4_bit(pc, blk);
+  }
+  *bits = m;
+  return true;
+}
+
+// Driver entry of rule r for driver clause d at record offset `off`.
+std::pair<uint32_t, uint32_t> entry_of(const RuleB& r, int d, uint32_t off) {
+  uint32_t axis = kFiltNoAxis, ipbits = 0, l4bits = kFiltL4All;
+  bool have_ip = false, have_l4 = false;
+  for (int c = 0; c < r.n; c++) {
+    if (c == d) continue;
+    uint32_t ax, b;
+    if (!have_l4 && filt_clause_l4(r.clause[c], &b)) {
+      l4bits = b;
+      have_l4 = true;
+    } else if (!have_ip && filt_clause_ip(r.clause[c], &ax, &b)) {
+      axis = ax;
+      ipbits = b;
+      have_ip = true;
+    }
+  }
+  return {off | axis, ipbits | l4bits};
+}
+
 bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vector<uint64_t>* tab) {
   uint32_t lg = 0;
   while ((8ull << lg) * 3 / 4 < keys.size() + 1) lg++;
@@ -556,20 +644,21 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
     th.n_hard = uint32_t(hard_offs.size());
     th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
-    // driver indexes for clauses 0 and 1 of the soft rules
+    // driver indexes for clauses 0 and 1 of the soft rules; entries carry the non-driver filter
     for (int k = 0; k < 2; k++) {
-      std::vector<uint32_t> always;
-      std::map<std::pair<uint8_t, uint8_t>, std::vector<std::pair<AtomKey, uint32_t>>> sub;  // (axis,band) -> (key, rec)
+      std::vector<std::pair<uint32_t, uint32_t>> always;  // (x, y)
+      std::map<std::pair<uint8_t, uint8_t>, std::vector<std::pair<AtomKey, std::pair<uint32_t, uint32_t>>>> sub;
       for (size_t rank = 0; rank < rs.size(); rank++) {
         RuleB& r = *rs[rank];
         if (r.hard || k >= r.n) continue;
+        std::pair<uint32_t, uint32_t> ent = entry_of(r, k, rec_off[rank]);
         for (auto& a : r.clause[k]) {
           AtomKey key;
           if (!atom_key(a, &key)) {
-            always.push_back(rec_off[rank]);
+            always.push_back(ent);
             continue;
           }
-          sub[{key.axis, key.band}].push_back({key, rec_off[rank]});
+          sub[{key.axis, key.band}].push_back({key, ent});
         }
       }
       std::vector<std::pair<size_t, std::pair<uint8_t, uint8_t>>> order;
@@ -591,7 +680,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
           bits = 10;
           while (bits < 22 && (1ull << bits) < 2 * ent) bits++;
         }
-        std::vector<std::pair<uint32_t, uint32_t>> be;  // (bucket, record)
+        std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> be;  // (bucket, entry)
         for (auto& e : v) {
           atom_bucket_list(e.first, bits, &bks);
           for (uint32_t b : bks) be.push_back({b, e.second});
@@ -599,10 +688,13 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
         std::sort(be.begin(), be.end());
         be.erase(std::unique(be.begin(), be.end()), be.end());
         uint32_t nb = 1u << bits;
-        std::vector<uint32_t> offs(size_t(nb) + 1, 0), ents(be.size());
+        std::vector<uint32_t> offs(size_t(nb) + 1, 0), ents(2 * be.size());
         for (auto& e : be) offs[e.first + 1]++;
         for (uint32_t b = 0; b < nb; b++) offs[b + 1] += offs[b];
-        for (size_t j = 0; j < be.size(); j++) ents[j] = be[j].second;
+        for (size_t j = 0; j < be.size(); j++) {
+          ents[2 * j] = be[j].second.first;
+          ents[2 * j + 1] = be[j].second.second;
+        }
         SubIdx& si = th.idx[k][th.n_idx[k]++];
         si.axis = axis;
         si.band = band;
@@ -612,8 +704,13 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       }
       std::sort(always.begin(), always.end());
       always.erase(std::unique(always.begin(), always.end()), always.end());
+      std::vector<uint32_t> aw;
+      for (auto& e : always) {
+        aw.push_back(e.first);
+        aw.push_back(e.second);
+      }
       th.always_n[k] = uint32_t(always.size());
-      th.always_off[k] = always.empty() ? 0 : B.put(always.data(), always.size(), 16);
+      th.always_off[k] = always.empty() ? 0 : B.put(aw.data(), aw.size(), 16);
     }
     out->n_rules[t - 1] = th.n_rules;
     out->n_hard[t - 1] = th.n_hard;

@@ -15,7 +15,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libgpc.so")
+LIB_PATH = os.environ.get("GPC_LIB") or os.path.join(HERE, "_build", "libgpc.so")  # GPC_LIB: experiment builds
 
 GPC_EINVAL, GPC_ENOTFOUND, GPC_ENOCLAUSE, GPC_EDEV, GPC_ERANGE = 2, 1, 5, 4, 7
 
