@@ -4,6 +4,7 @@ import copy
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from antrea_amd import gpc
@@ -58,5 +59,7 @@ def test_errors_mirror_reference():
     with pytest.raises(gpc.GpcError) as e:
         c.add_policy_rule_address(7, "dst", ["10.0.0.2"])
     assert e.value.code == gpc.GPC_ENOCLAUSE  # "no clause is using addrType"
+    one = {k: np.zeros(1, dt) for k, dt in (("src", np.uint32), ("dst", np.uint32), ("sport", np.uint16),
+                                            ("dport", np.uint16), ("proto", np.uint8), ("out_port", np.uint32))}
     with pytest.raises(gpc.GpcError):
-        c.commit() if False else c.classify_host({})  # classify before commit -> error
+        c.classify_host(one)  # nothing committed (and no device on this host): fails loudly

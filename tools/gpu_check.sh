@@ -16,11 +16,12 @@ step "rocprof kernel trace" && timeout -k 10 600 rocprofv3 --kernel-trace --stat
   --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-traffic \
   > gpurun_out/prof_kt.log 2>&1 || exit $?
 tail -1 gpurun_out/prof_kt.log
-step "rocprof FETCH_SIZE" && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex classify \
-  -d gpurun_out/prof_fetch -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
-  --no-traffic > gpurun_out/prof_fetch.log 2>&1 || exit $?
-step "rocprof WRITE_SIZE" && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex classify \
-  -d gpurun_out/prof_write -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
-  --no-traffic > gpurun_out/prof_write.log 2>&1 || exit $?
+step "rocprof SQ" && timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+  SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES --kernel-include-regex classify \
+  -d gpurun_out/prof_sq -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+  --no-traffic > gpurun_out/prof_sq.log 2>&1 || exit $?
+step "rocprof TCC" && timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex classify \
+  -d gpurun_out/prof_tcc -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+  --no-traffic > gpurun_out/prof_tcc.log 2>&1 || exit $?
 find gpurun_out -name "*.csv" | head -20
 echo "== done"
