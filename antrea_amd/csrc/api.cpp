@@ -200,13 +200,13 @@ int gpc_commit(gpc_ctx* ctx) {
   bool grow = need > ctx->counter_cap;
   if (grow) {
     size_t cap = std::max(need, ctx->counter_cap * 2);
-    if (hip_ok(hipMalloc(&nc, cap * 16)) || hip_ok(hipMemset(nc, 0, cap * 16))) {
+    if (hip_ok(hipMalloc(&nc, cap * kCounterBytes)) || hip_ok(hipMemset(nc, 0, cap * kCounterBytes))) {
       free_epoch(ne);
       return -GPC_EDEV;
     }
     if (ctx->d_counters) {
       (void)hipDeviceSynchronize();
-      (void)hipMemcpy(nc, ctx->d_counters, ctx->counter_cap * 16, hipMemcpyDeviceToDevice);
+      (void)hipMemcpy(nc, ctx->d_counters, ctx->counter_cap * kCounterBytes, hipMemcpyDeviceToDevice);
     }
   }
   DevEpoch old;
@@ -225,7 +225,7 @@ int gpc_commit(gpc_ctx* ctx) {
   free_epoch(old);
   if (old_counters) (void)hipFree(old_counters);
   for (uint32_t s : ctx->released_slots)
-    if (s < ctx->counter_cap) (void)hipMemset(ctx->d_counters + 2 * size_t(s), 0, 16);
+    if (s < ctx->counter_cap) (void)hipMemset(ctx->d_counters + kCounterWords * size_t(s), 0, kCounterBytes);
   ctx->released_slots.clear();
   return GPC_OK;
 }
@@ -295,14 +295,14 @@ int gpc_reset_counters(gpc_ctx* ctx) {
   std::lock_guard<std::mutex> g(ctx->ctl);
   if (!ctx->d_counters) return GPC_OK;
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  if (hip_ok(hipDeviceSynchronize()) || hip_ok(hipMemset(ctx->d_counters, 0, ctx->counter_cap * 16))) return -GPC_EDEV;
+  if (hip_ok(hipDeviceSynchronize()) || hip_ok(hipMemset(ctx->d_counters, 0, ctx->counter_cap * kCounterBytes))) return -GPC_EDEV;
   return GPC_OK;
 }
 
 int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  std::vector<unsigned long long> h(ctx->slot_conj.size() * 2, 0);
+  std::vector<unsigned long long> h(ctx->slot_conj.size() * kCounterWords, 0);
   if (ctx->d_counters && !h.empty()) {
     if (hip_ok(hipSetDevice(ctx->cfg.device)) || hip_ok(hipDeviceSynchronize()) ||
         hip_ok(hipMemcpy(h.data(), ctx->d_counters, h.size() * 8, hipMemcpyDeviceToHost)))
@@ -314,9 +314,9 @@ int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n) {
     if (out && k < cap) {
       out[k].conj_id = ctx->slot_conj[s];
       out[k].reserved = 0;
-      out[k].packets = h[2 * s];
-      out[k].bytes = h[2 * s + 1];
-      out[k].sessions = h[2 * s];  // every classified packet is ct_state=+new (pipeline.go:1643-1649)
+      out[k].packets = h[kCounterWords * s];
+      out[k].bytes = h[kCounterWords * s + 1];
+      out[k].sessions = h[kCounterWords * s + 2];
     }
     k++;
   }

@@ -35,14 +35,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   PacketOut o = classify_packet(im, p, dest);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
-    if (o.ecounted) {
-      atomicAdd(&counters[2 * o.eslot], 1ull);
-      atomicAdd(&counters[2 * o.eslot + 1], (unsigned long long)len);
-    }
-    if (o.gcounted) {
-      atomicAdd(&counters[2 * o.gslot], 1ull);
-      atomicAdd(&counters[2 * o.gslot + 1], (unsigned long long)len);
-    }
+    count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&counters[w], v); });
   }
   const VerdictOut e = o.e, g = o.g;
   out[i] = make_uint4(e.conj, e.packed, g.conj, g.packed);

@@ -16,6 +16,8 @@
 
 #include <stdint.h>
 
+#include "gpc.h"
+
 #if defined(__HIPCC__)
 #define GPC_HD __host__ __device__ __forceinline__
 #else
@@ -552,6 +554,26 @@ GPC_HD PacketOut classify_packet(const Img& im, const Pkt& p, uint32_t dest) {
     o.g = eval_stage(im, 3, p, &o.gslot, &o.gcounted);
   }
   return o;
+}
+
+// Per-rule counters: kCounterWords uint64 per slot {packets, bytes, sessions}. Sessions follow
+// the Metric flows (pipeline.go:1604-1670, parseMetricFlow network_policy.go:1917-1980): allow
+// rules count ct_state=+new packets, deny rules count every packet.
+constexpr uint32_t kCounterWords = 3;
+constexpr uint32_t kCounterBytes = kCounterWords * 8;
+
+template <typename Add>
+GPC_HD void count_stage(const VerdictOut& v, uint32_t slot, uint32_t len, uint32_t ct_state, Add add) {
+  const uint32_t base = kCounterWords * slot;
+  add(base, 1ull);
+  add(base + 1, (unsigned long long)len);
+  if ((v.packed & 0xffu) != RV_ALLOW || (ct_state & GPC_CT_NEW)) add(base + 2, 1ull);
+}
+
+template <typename Add>
+GPC_HD void count_packet(const PacketOut& o, uint32_t len, uint32_t ct_state, Add add) {
+  if (o.ecounted) count_stage(o.e, o.eslot, len, ct_state, add);
+  if (o.gcounted) count_stage(o.g, o.gslot, len, ct_state, add);
 }
 
 // Column loads -> axes (kernel and emulation share the defaults of gpc_pkt_soa).

@@ -39,16 +39,6 @@ def _lbar(wl, clf, n=20000):
         return None
 
 
-class _CAI:
-    def __init__(self, ptr, n):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2}
-
-
-def _device_view(ptr, n, dev):
-    import torch
-    return torch.as_tensor(_CAI(ptr, n), device=dev)
-
-
 def _cpu_baseline(wl, seconds):
     try:
         from oracle import cbaseline
@@ -123,6 +113,7 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    from antrea_amd import dist as gdist
     from antrea_amd import gpc, workload
     from antrea_amd.build import build
     if rank == 0 or world == 1:
@@ -172,9 +163,9 @@ def main():
         # library's device counters are wrapped zero-copy and reduced in place.
         ptr, slots = clf.counters()
         if count and ptr and slots:
-            cnt = _device_view(ptr, 2 * len(slots), dev)
+            cnt = gdist.device_counters(ptr, len(slots), dev)
             torch.cuda.synchronize(dev)
-            dist.all_reduce(cnt)
+            gdist.allreduce_counters(cnt)
             torch.cuda.synchronize(dev)
     elapsed = float(t.item())
 

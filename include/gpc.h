@@ -256,8 +256,10 @@ int gpc_commit(gpc_ctx* ctx);
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
 /* Same with HOST pointers (copies in and out; synchronous). */
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
-/* Per-rule counters as a device buffer of n_slots x {packets, bytes} uint64 (for an RCCL
- * all-reduce by the caller), plus the slot -> conj id map (host, valid until the next commit). */
+/* Per-rule counters as a device buffer of n_slots x {packets, bytes, sessions} uint64 (for an
+ * RCCL all-reduce by the caller), plus the slot -> conj id map (host, valid until the next commit).
+ * Sessions as the Metric flows count them: ct_state=+new packets for allow rules, every packet for
+ * deny rules (pipeline.go:1604-1670, network_policy.go:1917-1980). */
 int gpc_counters(gpc_ctx* ctx, uint64_t** dev_counters, const uint32_t** slot_conj, size_t* n_slots);
 int gpc_reset_counters(gpc_ctx* ctx);
 

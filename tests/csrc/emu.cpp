@@ -28,7 +28,8 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
 
 using namespace gpc;
 
-extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out) {
+extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
+                            unsigned long long* counters) {
   Img im{blob, static_cast<const ImageHdr*>(hdr)};
   for (size_t i = 0; i < n; i++) {
     Pkt p;
@@ -39,6 +40,8 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const gpc_pkt
     g_lines.clear();
     g_line_site.clear();
     PacketOut o = classify_packet(im, p, pk->dest ? pk->dest[i] : 0u);
+    if (counters)
+      count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;

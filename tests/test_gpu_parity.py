@@ -64,6 +64,8 @@ def test_gpu_counters_match_oracle_metrics():
     wl = workload.config1(seed=5)
     n = 600
     cols = workload.gen_packets(wl, n, seed=5)
+    u = np.random.default_rng(5).random(n)  # +new+trk / +trk (-new: no session) / +est+trk (bypass)
+    cols["ct_state"] = np.where(u < 0.7, 0x21, np.where(u < 0.9, 0x20, 0x22)).astype(np.uint8)
     want, pipe = oracle_verdicts(wl.rules, cols, n)
     d = pipe.metric_dumps()
     want_m = oc.network_policy_metrics(d["EgressMetric"], d["IngressMetric"])
