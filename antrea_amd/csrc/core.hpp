@@ -71,7 +71,7 @@ constexpr uint32_t kRecHdrWords = 5;
 constexpr uint32_t kBoxWords = 7;
 
 constexpr int kMaxClauses = 3;
-constexpr int kIdxPerClause = 6;  // sub-indexes (axis, band) per driver clause
+constexpr int kIdxPerClause = 4;  // sub-indexes (axis, band) per driver clause (more -> always list)
 
 // Driver-index entry (8 B, uint2): x = record word offset | filter axis (low 4 bits; 15 = no IP
 // filter), y = Bloom filter of the rule's NON-driver clauses: bits 0-19 one IP / exact-axis clause
@@ -290,15 +290,17 @@ GPC_HD bool clause_match(const Img& im, uint32_t table, uint32_t k, uint32_t rid
   return false;
 }
 
-// All clauses of a record; clause `last` (the driver, already a likely hit) is checked last.
+// All clauses of a record; clause `last` (the driver, already a likely hit) is checked last
+// (last >= n_clauses: natural order). One clause_match call site keeps the code small.
 GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint32_t w2, uint32_t rid, uint32_t last,
                        const Pkt& p) {
   const uint32_t ncl = rec_nclauses(w2);
-  for (uint32_t k = 0; k < ncl; k++) {
-    if (k == last) continue;
+  const uint32_t first = last < ncl ? last + 1 : 0;
+  for (uint32_t j = 0; j < ncl; j++) {
+    uint32_t k = first + j;
+    if (k >= ncl) k -= ncl;
     if (!clause_match(im, table, k, rid, rec + rec_off(w2, k), p)) return false;
   }
-  if (last < ncl && !clause_match(im, table, last, rid, rec + rec_off(w2, last), p)) return false;
   return true;
 }
 
@@ -379,7 +381,9 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   GPC_STAT(2, d1 ? cnt0 : cnt1);
   // k-way merge of the driver lists (ascending record offset = descending priority)
   const Ent* E = reinterpret_cast<const Ent*>(im.blob);
-  uint32_t cur[kLists], end[kLists], hx[kLists], hy[kLists];
+  // head of each list: record offset | 1 if the entry filter already rejects it (low 4 bits of an
+  // entry's x hold the filter axis; offsets are multiples of 16, so ordering is unaffected)
+  uint32_t cur[kLists], end[kLists], hx[kLists];
   cur[0] = th.always_off[d] / 2;
   end[0] = cur[0] + th.always_n[d];
 #pragma unroll
@@ -390,12 +394,10 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
 #pragma unroll
   for (int l = 0; l < kLists; l++) {
     hx[l] = 0xffffffffu;
-    hy[l] = 0;
     if (cur[l] < end[l]) {
       GPC_TOUCH(&E[cur[l]], 8);
       const Ent e = E[cur[l]];
-      hx[l] = e.x;
-      hy[l] = e.y;
+      hx[l] = (e.x & ~15u) | (entry_pass(p, e.x, e.y) ? 0u : 1u);
     }
   }
   uint32_t last = 0xffffffffu;
@@ -405,13 +407,12 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   uint32_t win = 0;         // winner record offset (soft) when have == 1 and !use_h
   int use_h = 0;
   while (true) {
-    uint32_t bx = 0xffffffffu, by = 0;
+    uint32_t bx = 0xffffffffu;
     int bi = -1;
 #pragma unroll
     for (int l = 0; l < kLists; l++) {
       if (hx[l] < bx) {
         bx = hx[l];
-        by = hy[l];
         bi = l;
       }
     }
@@ -426,25 +427,21 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
         ne = end[l];
       }
     }
-    Ent nx;
-    nx.x = 0xffffffffu;
-    nx.y = 0u;
+    uint32_t nh = 0xffffffffu;
     if (nc < ne) {
       GPC_TOUCH(&E[nc], 8);
-      nx = E[nc];
+      const Ent nx = E[nc];
+      nh = (nx.x & ~15u) | (entry_pass(p, nx.x, nx.y) ? 0u : 1u);
     }
 #pragma unroll
     for (int l = 0; l < kLists; l++) {
-      if (l == bi) {
-        hx[l] = nx.x;
-        hy[l] = nx.y;
-      }
+      if (l == bi) hx[l] = nh;
     }
-    if (bx == last) continue;
-    last = bx;
-    GPC_STAT(4, 1);
-    if (!entry_pass(p, bx, by)) continue;
     const uint32_t off = bx & ~15u;
+    if (off == last) continue;
+    GPC_STAT(4, 1);
+    if (bx & 1u) continue;  // filtered out
+    last = off;
     const uint32_t* rec = im.blob + off;
     GPC_TOUCH(rec, 4 * kRecHdrWords);
     const uint32_t w1 = rec[1], w2 = rec[2];
@@ -498,40 +495,10 @@ GPC_HD uint32_t pack_verdict(uint32_t action, uint32_t table, uint32_t tier, uin
   return action | (table << 8) | (tier << 16) | (flags << 24);
 }
 
-// One policy stage: tables base+1..base+3 (base 0 egress, 3 ingress).
-GPC_HD VerdictOut eval_stage(const Img& im, uint32_t base, const Pkt& p, uint32_t* slot_out, int* counted_out) {
-  uint32_t flags = 0;
-  uint32_t conj = 0, tier = 0;  // reg5/reg6 after a Pass keeps the Pass rule's conj id
-  *counted_out = 0;
-  for (uint32_t i = 0; i < 3; i++) {
-    TableResult r = eval_table(im, base + 1 + i, p);
-    if (r.tie) flags |= 2;
-    if (r.verdict == RV_MISS) continue;
-    if (r.verdict == RV_PASS) {  // Pass: goto {Egress,Ingress}Rule (pipeline.go:1861-1886)
-      flags |= 1;
-      conj = r.conj;
-      tier = r.tier;
-      continue;
-    }
-    VerdictOut o;
-    uint32_t act = r.verdict;  // RV_* values 2..6 equal GPC_ACT_*
-    if (r.verdict != RV_ISO_DROP && r.verdict != RV_BYPASS) {
-      conj = r.conj;
-      tier = r.tier;
-    }
-    o.conj = conj;
-    o.packed = pack_verdict(act, i + 1, tier, flags);
-    *slot_out = r.slot;
-    *counted_out = r.counted && (act == RV_ALLOW || act == RV_DROP || act == RV_REJECT);
-    return o;
-  }
-  VerdictOut o;
-  o.conj = conj;
-  o.packed = pack_verdict(1 /*NO_MATCH*/, 0, tier, flags);
-  return o;
-}
-
-// Both stages of one packet (the kernel body). Returns verdicts; counted slots via out params.
+// Both stages of one packet (the kernel body): one loop over the six rule tables so the table
+// evaluation is instantiated once. Egress = tables 1-3, ingress = 4-6; per stage the walk is
+// AntreaPolicy*Rule -> *Rule -> *DefaultRule with miss = next and Pass = goto *Rule
+// (pipeline.go:1861-1886); reg5/reg6 after a Pass keep the Pass rule's conj id and tier.
 struct PacketOut {
   VerdictOut e, g;
   uint32_t eslot, gslot;
@@ -540,18 +507,54 @@ struct PacketOut {
 
 GPC_HD PacketOut classify_packet(const Img& im, const Pkt& p, uint32_t dest) {
   PacketOut o;
-  o.gslot = 0;
-  o.gcounted = 0;
-  o.e = eval_stage(im, 0, p, &o.eslot, &o.ecounted);
-  const uint32_t eact = o.e.packed & 0xffu;
-  if (eact == RV_DROP || eact == RV_REJECT || eact == RV_ISO_DROP) {
-    o.g.conj = 0;
-    o.g.packed = 0;  // GPC_ACT_NONE: the ingress stage is never reached
-  } else if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
-    o.g.conj = 0;
-    o.g.packed = RV_BYPASS;
-  } else {
-    o.g = eval_stage(im, 3, p, &o.gslot, &o.gcounted);
+  o.e.conj = o.g.conj = 0;
+  o.e.packed = o.g.packed = 0;
+  o.eslot = o.gslot = 0;
+  o.ecounted = o.gcounted = 0;
+  uint32_t flags = 0, conj = 0, tier = 0;
+  uint32_t t = 1;
+  while (true) {
+    const TableResult r = eval_table(im, t, p);
+    const uint32_t i = t <= 3 ? t - 1 : t - 4;  // position inside the stage
+    if (r.tie) flags |= 2;
+    uint32_t act = 0, slot = 0;
+    int counted = 0;
+    if (r.verdict == RV_PASS) {
+      flags |= 1;
+      conj = r.conj;
+      tier = r.tier;
+    } else if (r.verdict != RV_MISS) {
+      act = r.verdict;  // RV_* values 2..6 equal GPC_ACT_*
+      if (act != RV_ISO_DROP && act != RV_BYPASS) {
+        conj = r.conj;
+        tier = r.tier;
+      }
+      slot = r.slot;
+      counted = r.counted && (act == RV_ALLOW || act == RV_DROP || act == RV_REJECT);
+    }
+    if (act == 0 && i < 2) {
+      t++;
+      continue;
+    }
+    VerdictOut v;
+    v.conj = conj;
+    v.packed = act ? pack_verdict(act, i + 1, tier, flags) : pack_verdict(1 /*NO_MATCH*/, 0, tier, flags);
+    if (t >= 4) {
+      o.g = v;
+      o.gslot = slot;
+      o.gcounted = counted;
+      break;
+    }
+    o.e = v;
+    o.eslot = slot;
+    o.ecounted = counted;
+    if (act == RV_DROP || act == RV_REJECT || act == RV_ISO_DROP) break;  // ingress never reached (NONE)
+    if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
+      o.g.packed = RV_BYPASS;
+      break;
+    }
+    flags = conj = tier = 0;
+    t = 4;
   }
   return o;
 }

@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/exp
-run() {  # name, env, args
+run() {  # name, env...
   local name=$1; shift
   echo "== $name ($(date +%T))"
   env "$@" timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-traffic $EXTRA \
@@ -11,8 +11,7 @@ run() {  # name, env, args
   tail -1 gpurun_out/exp/$name.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernel_ms'], d['roofline']['lines_per_packet'])"
 }
 B=antrea_amd/_build
-run w4 GPC_LIB=$B/libgpc.so
-run w6 GPC_LIB=$B/libgpc_w6.so
-run w8 GPC_LIB=$B/libgpc_w8.so
-EXTRA=--no-count run w4_nocount GPC_LIB=$B/libgpc.so
+for v in ${VARIANTS:-w4}; do
+  if [ "$v" = w4 ]; then run w4 GPC_LIB=$B/libgpc.so; else run $v GPC_LIB=$B/libgpc_$v.so; fi
+done
 echo "== done"
