@@ -13,7 +13,7 @@
 namespace gpc {
 
 #ifndef GPC_WAVES_PER_EU
-#define GPC_WAVES_PER_EU 4
+#define GPC_WAVES_PER_EU 6
 #endif
 #ifndef GPC_BLOCK
 #define GPC_BLOCK 256

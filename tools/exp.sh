@@ -12,6 +12,6 @@ run() {  # name, env...
 }
 B=antrea_amd/_build
 for v in ${VARIANTS:-w4}; do
-  if [ "$v" = w4 ]; then run w4 GPC_LIB=$B/libgpc.so; else run $v GPC_LIB=$B/libgpc_$v.so; fi
+  if [ "$v" = base ]; then run base GPC_LIB=$B/libgpc.so; else run $v GPC_LIB=$B/libgpc_$v.so; fi
 done
 echo "== done"
