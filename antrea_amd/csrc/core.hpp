@@ -73,19 +73,22 @@ constexpr uint32_t kBoxWords = 7;
 constexpr int kMaxClauses = 3;
 constexpr int kIdxPerClause = 4;  // sub-indexes (axis, band) per driver clause (more -> always list)
 
-// Driver-index entry (8 B, uint2): x = record word offset | filter axis (low 4 bits; 15 = no IP
-// filter), y = Bloom filter of the rule's NON-driver clauses: bits 0-19 one IP / exact-axis clause
-// on axis (x & 15), bits 20-31 the service clause (proto class x 4096-port block of tp_dst).
-// A packet skips an entry without reading the record unless both parts intersect its own bits;
-// the filter is a necessary condition of the clauses, so skipping never changes a verdict.
-struct alignas(8) Ent {
-  uint32_t x, y;
+// Driver-index entry (16 B): a prefilter of the rule's NON-driver clauses, so that most candidates
+// are rejected without reading the record.
+//   x  = record offset / 16 << 8 | interval axis << 4 | Bloom axis          (15 = none)
+//   y  = Bloom bits: 0-19 one IP / exact-axis clause on the Bloom axis, 20-31 the service clause
+//        (protocol class x 4096-port block of tp_dst)
+//   lo, hi = hull of the most selective non-driver clause on the interval axis
+// Both tests are necessary conditions of the clauses, so skipping never changes a verdict.
+struct alignas(16) Ent {
+  uint32_t x, y, lo, hi;
 };
+GPC_HD uint32_t ent_off(uint32_t x) { return (x >> 8) << 4; }
 
 struct SubIdx {  // one (axis, band) bucket index of a driver clause
   uint8_t axis, band, bits, reserved;
   uint32_t off;  // word offset of 2^bits + 1 bucket offsets (in entries, relative to `ent`)
-  uint32_t ent;  // word offset (even) of the uint2 entries, ascending record offset per bucket
+  uint32_t ent;  // word offset (multiple of 4) of the Ent entries, ascending record offset per bucket
 };
 
 struct TableHdr {
@@ -167,8 +170,8 @@ GPC_HD uint64_t point_key(uint32_t table, uint32_t clause, uint32_t axis, uint32
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
 GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0x9e3779b97f4a7c15ull) >> 32) & mask; }
 
-// Entry filter bits. IP axes: band 1/2/3 = prefix length 8-15 / 16-23 / 24-32 keyed by the top
-// 8 / 16 / 24 address bits; exact axes (in_port, reg1, reg7, tun_id): band 4 keyed by the value.
+// Entry filter bits. IP axes: band 1/2/3/4 = prefix length 8-15 / 16-23 / 24-31 / 32 keyed by the
+// top 8 / 16 / 24 / 32 address bits; exact axes (in_port, reg1, reg7, tun_id): band 4 keyed by the value.
 constexpr uint32_t kFiltIpBits = 20, kFiltL4Shift = 20, kFiltL4Bits = 12;
 constexpr uint32_t kFiltNoAxis = 15u;
 constexpr uint32_t kFiltL4All = 0xfff00000u;
@@ -179,7 +182,9 @@ GPC_HD uint32_t filt_l4_bit(uint32_t pclass, uint32_t block) {
   return 1u << (kFiltL4Shift + uint32_t((uint64_t(mix32(((pclass << 4) | block) + 0x3c6ef372u)) * kFiltL4Bits) >> 32));
 }
 GPC_HD uint32_t filt_pkt_axis(uint32_t axis, uint32_t v) {
-  if (axis <= 3u) return filt_ip_bit(axis, 1, v >> 24) | filt_ip_bit(axis, 2, v >> 16) | filt_ip_bit(axis, 3, v >> 8);
+  if (axis <= 3u)
+    return filt_ip_bit(axis, 1, v >> 24) | filt_ip_bit(axis, 2, v >> 16) | filt_ip_bit(axis, 3, v >> 8) |
+           filt_ip_bit(axis, 4, v);
   return filt_ip_bit(axis, 4, v);
 }
 
@@ -304,10 +309,13 @@ GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint3
   return true;
 }
 
-GPC_HD bool entry_pass(const Pkt& p, uint32_t x, uint32_t y) {
-  if ((y & p.l4m) == 0u) return false;
-  const uint32_t ax = x & 15u;
-  return ax == kFiltNoAxis || (y & p.fm[ax & 7u]) != 0u;
+GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {
+  if ((e.y & p.l4m) == 0u) return false;
+  const uint32_t bax = e.x & 15u, iax = (e.x >> 4) & 15u;
+  if (bax != kFiltNoAxis && (e.y & p.fm[bax & 7u]) == 0u) return false;
+  if (iax == kFiltNoAxis) return true;
+  const uint32_t v = p.ax[iax < AX_N ? iax : 0];
+  return e.lo <= v && v <= e.hi;
 }
 
 constexpr int kLists = kIdxPerClause + 1;  // always list + sub-indexes of the driver clause
@@ -345,7 +353,11 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     }
   }
   const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
+#ifdef GPC_ABL_NOSOFT  // timing experiment only: skip the soft-rule evaluation
+  if (true) {
+#else
   if (n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
+#endif
     if (rH != th.end_off) res.verdict = uint8_t(hverdict);
     return res;
   }
@@ -360,8 +372,8 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
       const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
       const uint32_t* o = im.blob + si.off;
       GPC_TOUCH(o + b, 8);
-      lo0[i] = si.ent / 2 + o[b];
-      hi0[i] = si.ent / 2 + o[b + 1];
+      lo0[i] = si.ent / 4 + o[b];
+      hi0[i] = si.ent / 4 + o[b + 1];
       cnt0 += hi0[i] - lo0[i];
     }
     if (uint32_t(i) < n1) {
@@ -369,22 +381,28 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
       const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
       const uint32_t* o = im.blob + si.off;
       GPC_TOUCH(o + b, 8);
-      lo1[i] = si.ent / 2 + o[b];
-      hi1[i] = si.ent / 2 + o[b + 1];
+      lo1[i] = si.ent / 4 + o[b];
+      hi1[i] = si.ent / 4 + o[b + 1];
       cnt1 += hi1[i] - lo1[i];
     }
   }
   const bool d1 = cnt1 < cnt0;
+#ifdef GPC_ABL_NOMERGE  // timing experiment only: stop after the bucket lookups
+  if (cnt0 + cnt1 != 0xffffffffu) {
+    res.tie = uint8_t((cnt0 + cnt1) & 1u);
+    return res;
+  }
+#endif
   const uint32_t d = d1 ? 1u : 0u;
   GPC_STAT(0, 1);
   GPC_STAT(1, d1 ? cnt1 : cnt0);
   GPC_STAT(2, d1 ? cnt0 : cnt1);
   // k-way merge of the driver lists (ascending record offset = descending priority)
   const Ent* E = reinterpret_cast<const Ent*>(im.blob);
-  // head of each list: record offset | 1 if the entry filter already rejects it (low 4 bits of an
-  // entry's x hold the filter axis; offsets are multiples of 16, so ordering is unaffected)
+  // head of each list: entry x with the axis byte replaced by 1 if the prefilter rejects it
+  // (ordering by x = ordering by record offset)
   uint32_t cur[kLists], end[kLists], hx[kLists];
-  cur[0] = th.always_off[d] / 2;
+  cur[0] = th.always_off[d] / 4;
   end[0] = cur[0] + th.always_n[d];
 #pragma unroll
   for (int i = 0; i < kIdxPerClause; i++) {
@@ -395,9 +413,9 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   for (int l = 0; l < kLists; l++) {
     hx[l] = 0xffffffffu;
     if (cur[l] < end[l]) {
-      GPC_TOUCH(&E[cur[l]], 8);
+      GPC_TOUCH(&E[cur[l]], 16);
       const Ent e = E[cur[l]];
-      hx[l] = (e.x & ~15u) | (entry_pass(p, e.x, e.y) ? 0u : 1u);
+      hx[l] = (e.x & ~0xffu) | (entry_pass(p, e) ? 0u : 1u);
     }
   }
   uint32_t last = 0xffffffffu;
@@ -416,7 +434,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
         bi = l;
       }
     }
-    if (bi < 0 || (bx & ~15u) >= rH) break;
+    if (bi < 0 || ent_off(bx) >= rH) break;
     // advance the list the candidate came from: one load, selected by unrolled compares
     uint32_t nc = 0, ne = 0;
 #pragma unroll
@@ -429,15 +447,15 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     }
     uint32_t nh = 0xffffffffu;
     if (nc < ne) {
-      GPC_TOUCH(&E[nc], 8);
+      GPC_TOUCH(&E[nc], 16);
       const Ent nx = E[nc];
-      nh = (nx.x & ~15u) | (entry_pass(p, nx.x, nx.y) ? 0u : 1u);
+      nh = (nx.x & ~0xffu) | (entry_pass(p, nx) ? 0u : 1u);
     }
 #pragma unroll
     for (int l = 0; l < kLists; l++) {
       if (l == bi) hx[l] = nh;
     }
-    const uint32_t off = bx & ~15u;
+    const uint32_t off = ent_off(bx);
     if (off == last) continue;
     GPC_STAT(4, 1);
     if (bx & 1u) continue;  // filtered out
@@ -452,7 +470,13 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
       level_done = 0;
     }
     GPC_STAT(3, 1);
-    if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, p)) continue;
+#ifdef GPC_ABL_NOVERIFY  // timing experiment only: read the record header, skip the clauses
+    if (w2 != 0xffffffffu) continue;
+#endif
+    if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, p)) {
+      GPC_STAT(5, 1);
+      continue;
+    }
     level_done++;
     if (have) {  // a second completion at the winning level
       res.tie = 1;

@@ -9,6 +9,7 @@
 #include "image.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <random>
 
@@ -349,8 +350,8 @@ bool filt_term_ip(const Term& t, uint32_t* bit) {
     if (!is_prefix(t.mask)) return false;
     int L = leading_ones(t.mask);
     if (L < 8) return false;
-    uint32_t band = L < 16 ? 1 : L < 24 ? 2 : 3;
-    uint32_t shift = band == 1 ? 24 : band == 2 ? 16 : 8;
+    uint32_t band = L < 16 ? 1 : L < 24 ? 2 : L < 32 ? 3 : 4;
+    uint32_t shift = band == 1 ? 24 : band == 2 ? 16 : band == 3 ? 8 : 0;
     *bit = filt_ip_bit(t.axis, band, t.val >> shift);
     return true;
   }
@@ -411,10 +412,39 @@ bool filt_clause_l4(const std::vector<Atom>& atoms, uint32_t* bits) {
   return true;
 }
 
-// Driver entry of rule r for driver clause d at record offset `off`.
-std::pair<uint32_t, uint32_t> entry_of(const RuleB& r, int d, uint32_t off) {
+// Hull of one clause on `axis` (every atom needs a term on it): any value matching v/m lies in
+// [v & m, (v & m) | ~m], so the hull is a necessary condition of the clause.
+bool clause_hull(const std::vector<Atom>& atoms, uint8_t axis, uint32_t* lo, uint32_t* hi) {
+  if (atoms.empty()) return false;
+  uint32_t l = 0xffffffffu, h = 0;
+  for (auto& a : atoms) {
+    const Term* tm = nullptr;
+    for (auto& t : a.t)
+      if (t.axis == axis) tm = &t;
+    if (!tm) return false;
+    l = std::min(l, tm->val & tm->mask);
+    h = std::max(h, (tm->val & tm->mask) | ~tm->mask);
+  }
+  *lo = l;
+  *hi = h;
+  return true;
+}
+
+// Fraction of the axis' value space the hull covers (the interval prefilter keeps the smallest).
+double hull_coverage(uint8_t axis, uint32_t lo, uint32_t hi, const uint64_t* span) {
+  double len = double(hi) - double(lo) + 1.0;
+  if (axis == AX_L4D || axis == AX_L4S) return (lo >> 16) == (hi >> 16) ? len / 65536.0 : 1.0;
+  if (axis <= AX_TUN) return span[axis] ? std::min(1.0, len / double(span[axis])) : 1.0;  // IP and exact axes
+  return 1.0;
+}
+
+// Driver entry (core.hpp Ent) of rule r for driver clause d at record offset `off`; `span` = value
+// span of each exact axis over the table's atoms.
+std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint64_t* span) {
   uint32_t axis = kFiltNoAxis, ipbits = 0, l4bits = kFiltL4All;
   bool have_ip = false, have_l4 = false;
+  uint32_t iax = kFiltNoAxis, ilo = 0, ihi = 0;
+  double best = 0.5;  // an interval covering more than half of its axis is not worth a check
   for (int c = 0; c < r.n; c++) {
     if (c == d) continue;
     uint32_t ax, b;
@@ -426,8 +456,21 @@ std::pair<uint32_t, uint32_t> entry_of(const RuleB& r, int d, uint32_t off) {
       ipbits = b;
       have_ip = true;
     }
+    if (r.clause[c].empty()) continue;
+    for (auto& t : r.clause[c][0].t) {
+      if (t.axis >= AX_CTST) continue;
+      uint32_t lo, hi;
+      if (!clause_hull(r.clause[c], t.axis, &lo, &hi)) continue;
+      double cov = hull_coverage(t.axis, lo, hi, span);
+      if (cov < best) {
+        best = cov;
+        iax = t.axis;
+        ilo = lo;
+        ihi = hi;
+      }
+    }
   }
-  return {off | axis, ipbits | l4bits};
+  return {((off >> 4) << 8) | (iax << 4) | axis, ipbits | l4bits, ilo, ihi};
 }
 
 bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vector<uint64_t>* tab) {
@@ -633,6 +676,10 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       rec[2] = flags | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
       rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0;
       rec[4] = uint32_t(r.tier) | (rid << 8);
+      if (base >= (1u << 28)) {  // Ent.x holds record offset / 16 in 24 bits
+        out->error = "rule records exceed 1 GiB";
+        return -GPC_ENOMEM;
+      }
       rec_off[rank] = base;
       B.w.insert(B.w.end(), rec.begin(), rec.end());
       if (r.hard) hard_offs.push_back(base);
@@ -644,14 +691,29 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
     th.n_hard = uint32_t(hard_offs.size());
     th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
+    // value span of the exact axes over this table's soft rules (interval prefilter selectivity)
+    uint64_t span[AX_N] = {0};
+    {
+      uint32_t mn[AX_N], mx[AX_N];
+      for (int a = 0; a < AX_N; a++) mn[a] = 0xffffffffu, mx[a] = 0;
+      for (RuleB* rp : rs)
+        if (!rp->hard)
+          for (int c = 0; c < rp->n; c++)
+            for (auto& at : rp->clause[c])
+              for (auto& t : at.t) {
+                mn[t.axis] = std::min(mn[t.axis], t.val & t.mask);
+                mx[t.axis] = std::max(mx[t.axis], (t.val & t.mask) | ~t.mask);
+              }
+      for (int a = 0; a < AX_N; a++) span[a] = mx[a] >= mn[a] ? uint64_t(mx[a]) - mn[a] + 1 : 0;
+    }
     // driver indexes for clauses 0 and 1 of the soft rules; entries carry the non-driver filter
     for (int k = 0; k < 2; k++) {
-      std::vector<std::pair<uint32_t, uint32_t>> always;  // (x, y)
-      std::map<std::pair<uint8_t, uint8_t>, std::vector<std::pair<AtomKey, std::pair<uint32_t, uint32_t>>>> sub;
+      std::vector<std::array<uint32_t, 4>> always;
+      std::map<std::pair<uint8_t, uint8_t>, std::vector<std::pair<AtomKey, std::array<uint32_t, 4>>>> sub;
       for (size_t rank = 0; rank < rs.size(); rank++) {
         RuleB& r = *rs[rank];
         if (r.hard || k >= r.n) continue;
-        std::pair<uint32_t, uint32_t> ent = entry_of(r, k, rec_off[rank]);
+        std::array<uint32_t, 4> ent = entry_of(r, k, rec_off[rank], span);
         for (auto& a : r.clause[k]) {
           AtomKey key;
           if (!atom_key(a, &key)) {
@@ -680,7 +742,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
           bits = 10;
           while (bits < 22 && (1ull << bits) < 2 * ent) bits++;
         }
-        std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> be;  // (bucket, entry)
+        std::vector<std::pair<uint32_t, std::array<uint32_t, 4>>> be;  // (bucket, entry)
         for (auto& e : v) {
           atom_bucket_list(e.first, bits, &bks);
           for (uint32_t b : bks) be.push_back({b, e.second});
@@ -688,13 +750,11 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
         std::sort(be.begin(), be.end());
         be.erase(std::unique(be.begin(), be.end()), be.end());
         uint32_t nb = 1u << bits;
-        std::vector<uint32_t> offs(size_t(nb) + 1, 0), ents(2 * be.size());
+        std::vector<uint32_t> offs(size_t(nb) + 1, 0), ents;
+        ents.reserve(4 * be.size());
         for (auto& e : be) offs[e.first + 1]++;
         for (uint32_t b = 0; b < nb; b++) offs[b + 1] += offs[b];
-        for (size_t j = 0; j < be.size(); j++) {
-          ents[2 * j] = be[j].second.first;
-          ents[2 * j + 1] = be[j].second.second;
-        }
+        for (auto& e : be) ents.insert(ents.end(), e.second.begin(), e.second.end());
         SubIdx& si = th.idx[k][th.n_idx[k]++];
         si.axis = axis;
         si.band = band;
@@ -705,10 +765,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       std::sort(always.begin(), always.end());
       always.erase(std::unique(always.begin(), always.end()), always.end());
       std::vector<uint32_t> aw;
-      for (auto& e : always) {
-        aw.push_back(e.first);
-        aw.push_back(e.second);
-      }
+      for (auto& e : always) aw.insert(aw.end(), e.begin(), e.end());
       th.always_n[k] = uint32_t(always.size());
       th.always_off[k] = always.empty() ? 0 : B.put(aw.data(), aw.size(), 16);
     }
