@@ -397,99 +397,94 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   GPC_STAT(0, 1);
   GPC_STAT(1, d1 ? cnt1 : cnt0);
   GPC_STAT(2, d1 ? cnt0 : cnt1);
-  // k-way merge of the driver lists (ascending record offset = descending priority)
+  // Candidate scan. The driver lists (0 = always list, 1.. = sub-index buckets) are walked as one
+  // flattened sequence: every entry is loaded and prefiltered with a branch-free body, and only the
+  // two smallest passing record offsets (= the two best-ranked candidates) are kept. They are then
+  // verified in rank order; if more candidates passed and no decision was reached, the lists are
+  // rescanned above the last verified offset. Same result as a k-way merge in rank order.
   const Ent* E = reinterpret_cast<const Ent*>(im.blob);
-  // head of each list: entry x with the axis byte replaced by 1 if the prefilter rejects it
-  // (ordering by x = ordering by record offset)
-  uint32_t cur[kLists], end[kLists], hx[kLists];
-  cur[0] = th.always_off[d] / 4;
-  end[0] = cur[0] + th.always_n[d];
+  uint32_t base[kLists], upto[kLists];  // first entry index; cumulative end in the flattened scan
+  base[0] = th.always_off[d] / 4;
+  upto[0] = th.always_n[d];
 #pragma unroll
   for (int i = 0; i < kIdxPerClause; i++) {
-    cur[i + 1] = d1 ? lo1[i] : lo0[i];
-    end[i + 1] = d1 ? hi1[i] : hi0[i];
+    const uint32_t lo = d1 ? lo1[i] : lo0[i], hi = d1 ? hi1[i] : hi0[i];
+    base[i + 1] = lo;
+    upto[i + 1] = upto[i] + (hi - lo);
   }
-#pragma unroll
-  for (int l = 0; l < kLists; l++) {
-    hx[l] = 0xffffffffu;
-    if (cur[l] < end[l]) {
-      GPC_TOUCH(&E[cur[l]], 16);
-      const Ent e = E[cur[l]];
-      hx[l] = (e.x & ~0xffu) | (entry_pass(p, e) ? 0u : 1u);
-    }
-  }
-  uint32_t last = 0xffffffffu;
+  const uint32_t total = upto[kLists - 1];
+  uint32_t after = 0;       // rescan bound (exclusive); record offsets are > 0
   int have = 0;             // result found
   uint32_t level = 0xffffffffu;
   uint32_t level_done = 0;  // completed conjunctions at the current level
   uint32_t win = 0;         // winner record offset (soft) when have == 1 and !use_h
   int use_h = 0;
-  while (true) {
-    uint32_t bx = 0xffffffffu;
-    int bi = -1;
+  bool done = total == 0;
+  while (!done) {
+    uint32_t c0 = 0xffffffffu, c1 = 0xffffffffu;
+    bool more = false;
+    for (uint32_t j = 0; j < total; j++) {
+      uint32_t idx = base[0] + j;
 #pragma unroll
-    for (int l = 0; l < kLists; l++) {
-      if (hx[l] < bx) {
-        bx = hx[l];
-        bi = l;
+      for (int l = 1; l < kLists; l++)
+        if (j >= upto[l - 1]) idx = base[l] + (j - upto[l - 1]);
+      GPC_TOUCH(&E[idx], 16);
+      const Ent e = E[idx];
+      const uint32_t off = ent_off(e.x);
+      GPC_STAT(4, 1);
+      if (off <= after || off >= rH || !entry_pass(p, e)) continue;
+      if (off < c0) {
+        more |= c1 != 0xffffffffu;
+        c1 = c0;
+        c0 = off;
+      } else if (off != c0 && off < c1) {
+        more |= c1 != 0xffffffffu;
+        c1 = off;
+      } else if (off != c0 && off != c1) {
+        more = true;
       }
     }
-    if (bi < 0 || ent_off(bx) >= rH) break;
-    // advance the list the candidate came from: one load, selected by unrolled compares
-    uint32_t nc = 0, ne = 0;
 #pragma unroll
-    for (int l = 0; l < kLists; l++) {
-      if (l == bi) {
-        cur[l]++;
-        nc = cur[l];
-        ne = end[l];
+    for (int q = 0; q < 2; q++) {
+      const uint32_t off = q ? c1 : c0;
+      if (off == 0xffffffffu || done) break;
+      after = off;
+      const uint32_t* rec = im.blob + off;
+      GPC_TOUCH(rec, 4 * kRecHdrWords);
+      const uint32_t w1 = rec[1], w2 = rec[2];
+      const uint32_t prio = w1 & 0xffffu;
+      if (prio != level) {
+        if (have) {  // winning level finished
+          done = true;
+          break;
+        }
+        level = prio;
+        level_done = 0;
       }
-    }
-    uint32_t nh = 0xffffffffu;
-    if (nc < ne) {
-      GPC_TOUCH(&E[nc], 16);
-      const Ent nx = E[nc];
-      nh = (nx.x & ~0xffu) | (entry_pass(p, nx) ? 0u : 1u);
-    }
-#pragma unroll
-    for (int l = 0; l < kLists; l++) {
-      if (l == bi) hx[l] = nh;
-    }
-    const uint32_t off = ent_off(bx);
-    if (off == last) continue;
-    GPC_STAT(4, 1);
-    if (bx & 1u) continue;  // filtered out
-    last = off;
-    const uint32_t* rec = im.blob + off;
-    GPC_TOUCH(rec, 4 * kRecHdrWords);
-    const uint32_t w1 = rec[1], w2 = rec[2];
-    const uint32_t prio = w1 & 0xffffu;
-    if (prio != level) {
-      if (have) break;  // winning level finished
-      level = prio;
-      level_done = 0;
-    }
-    GPC_STAT(3, 1);
+      GPC_STAT(3, 1);
 #ifdef GPC_ABL_NOVERIFY  // timing experiment only: read the record header, skip the clauses
-    if (w2 != 0xffffffffu) continue;
+      if (w2 != 0xffffffffu) continue;
 #endif
-    if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, p)) {
-      GPC_STAT(5, 1);
-      continue;
+      if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, p)) {
+        GPC_STAT(5, 1);
+        continue;
+      }
+      level_done++;
+      if (have) {  // a second completion at the winning level
+        res.tie = 1;
+        done = true;
+        break;
+      }
+      if (rec_has_act(w2)) {
+        have = 1;
+        use_h = (rH != th.end_off && hprio > (w1 >> 16)) ? 1 : 0;
+        win = off;
+      } else if (rH != th.end_off) {
+        have = 1;
+        use_h = 1;
+      }
     }
-    level_done++;
-    if (have) {  // a second completion at the winning level
-      res.tie = 1;
-      break;
-    }
-    if (rec_has_act(w2)) {
-      have = 1;
-      use_h = (rH != th.end_off && hprio > (w1 >> 16)) ? 1 : 0;
-      win = off;
-    } else if (rH != th.end_off) {
-      have = 1;
-      use_h = 1;
-    }
+    if (!more) done = true;
   }
   if (have && !use_h) {
     const uint32_t* rec = im.blob + win;
