@@ -23,6 +23,12 @@
 #else
 #define GPC_HD inline
 #endif
+// Wave-uniform loop condition: any lane of the wavefront still has work (host emulation: this lane).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GPC_WAVE_ANY(c) __any(c)
+#else
+#define GPC_WAVE_ANY(c) (c)
+#endif
 
 namespace gpc {
 
@@ -309,13 +315,13 @@ GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint3
   return true;
 }
 
-GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {
-  if ((e.y & p.l4m) == 0u) return false;
+GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
   const uint32_t bax = e.x & 15u, iax = (e.x >> 4) & 15u;
-  if (bax != kFiltNoAxis && (e.y & p.fm[bax & 7u]) == 0u) return false;
-  if (iax == kFiltNoAxis) return true;
+  const bool l4 = (e.y & p.l4m) != 0u;
+  const bool bl = (bax == kFiltNoAxis) | ((e.y & p.fm[bax & 7u]) != 0u);
   const uint32_t v = p.ax[iax < AX_N ? iax : 0];
-  return e.lo <= v && v <= e.hi;
+  const bool iv = (iax == kFiltNoAxis) | ((e.lo <= v) & (v <= e.hi));
+  return l4 & bl & iv;
 }
 
 constexpr int kLists = kIdxPerClause + 1;  // always list + sub-indexes of the driver clause
@@ -423,26 +429,25 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   while (!done) {
     uint32_t c0 = 0xffffffffu, c1 = 0xffffffffu;
     bool more = false;
-    for (uint32_t j = 0; j < total; j++) {
+    // wave-uniform trip count (the wave's longest candidate list); finished lanes read the zero
+    // entry at index 0 (offset 0 is never a record), so the body has no divergent branches
+    for (uint32_t j = 0; GPC_WAVE_ANY(j < total); j++) {
       uint32_t idx = base[0] + j;
 #pragma unroll
       for (int l = 1; l < kLists; l++)
         if (j >= upto[l - 1]) idx = base[l] + (j - upto[l - 1]);
+      idx = j < total ? idx : 0u;
       GPC_TOUCH(&E[idx], 16);
       const Ent e = E[idx];
       const uint32_t off = ent_off(e.x);
-      GPC_STAT(4, 1);
-      if (off <= after || off >= rH || !entry_pass(p, e)) continue;
-      if (off < c0) {
-        more |= c1 != 0xffffffffu;
-        c1 = c0;
-        c0 = off;
-      } else if (off != c0 && off < c1) {
-        more |= c1 != 0xffffffffu;
-        c1 = off;
-      } else if (off != c0 && off != c1) {
-        more = true;
-      }
+      GPC_STAT(4, j < total ? 1 : 0);
+      const bool pass = (off > after) & (off < rH) & entry_pass(p, e);
+      const uint32_t v = pass ? off : 0xffffffffu;
+      const bool fresh = (v != 0xffffffffu) & (v != c0) & (v != c1);
+      more |= fresh & (c1 != 0xffffffffu);  // a third distinct survivor: one of them is dropped
+      const bool lt0 = fresh & (v < c0), lt1 = fresh & (v < c1);
+      c1 = lt0 ? c0 : (lt1 ? v : c1);
+      c0 = lt0 ? v : c0;
     }
 #pragma unroll
     for (int q = 0; q < 2; q++) {
