@@ -336,6 +336,11 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   }
   out->n_flows = ctx->last.n_flows;
   out->n_counter_slots = uint32_t(ctx->slot_conj.size());
+  out->bytes_records = ctx->last.bytes_records;
+  out->bytes_ext = ctx->last.bytes_ext;
+  out->bytes_bucket_offsets = ctx->last.bytes_bucket_offsets;
+  out->bytes_entries = ctx->last.bytes_entries;
+  out->bytes_hash = ctx->last.bytes_hash;
   return GPC_OK;
 }
 

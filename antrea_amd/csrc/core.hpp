@@ -77,7 +77,7 @@ constexpr uint32_t kRecHdrWords = 5;
 constexpr uint32_t kBoxWords = 7;
 
 constexpr int kMaxClauses = 3;
-constexpr int kIdxPerClause = 4;  // sub-indexes (axis, band) per driver clause (more -> always list)
+constexpr int kIdxPerClause = 5;  // sub-indexes (axis, band) per driver clause (more -> always list)
 
 // Driver-index entry (16 B): a prefilter of the rule's NON-driver clauses, so that most candidates
 // are rejected without reading the record.
@@ -157,14 +157,18 @@ GPC_HD uint32_t proto_class(uint32_t proto) {
     default: return 0;
   }
 }
-// Bands: IP axes 0 = prefix len 0..16 (top-16 bits, exact), 1 = 17..24 (hash of top-24),
-// 2 = 25..32 (hash of the address); exact axes (in_port, reg1, reg7, tun) band 0 = low `bits`
-// bits of the value; L4 axes band 0 = proto class x port/8.
+// Bands of the IP axes, by prefix length L: 0 = L 4..12 keyed by the top 12 bits (direct),
+// 1 = L 13..16 by the top 16 (direct), 2 = L 17..24 by a hash of the top 20, 3 = L 25..32 by a
+// hash of the top 28. An atom is listed under every key its prefix covers (at most 2^8, 2^3, 2^3,
+// 2^3 keys); longer prefixes than the key share their key's bucket and are checked on
+// verification. Exact axes (in_port, reg1, reg7, tun) band 0 = low `bits` bits of the value;
+// L4 axes band 0 = proto class x port/8.
+constexpr uint32_t kIpBands = 4;
+GPC_HD uint32_t ip_band_shift(uint32_t band) { return band == 0 ? 20u : band == 1 ? 16u : band == 2 ? 12u : 4u; }
 GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t bits, uint32_t v) {
   if (axis <= AX_CTDST) {
-    if (band == 0) return v >> 16;
-    if (band == 1) return mix32(v >> 8) >> (32 - bits);
-    return mix32(v) >> (32 - bits);
+    const uint32_t key = v >> ip_band_shift(band);
+    return band < 2 ? key : mix32(key) >> (32 - bits);
   }
   if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
   return v & ((1u << bits) - 1u);

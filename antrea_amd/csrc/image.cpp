@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 
@@ -301,8 +303,8 @@ bool atom_key(const Atom& a, AtomKey* k) {
   k->lo = pt->val & cov;
   k->hi = k->lo | ~cov;
   if (pt->axis <= AX_CTDST) {
-    k->band = L <= 16 ? 0 : L <= 24 ? 1 : 2;
-    if (k->band == 0 && (uint64_t(k->hi >> 16) - (k->lo >> 16) + 1) > kMaxBucketsPerAtom) return false;
+    if (L < 4) return false;  // /0../3: always list
+    k->band = L <= 12 ? 0 : L <= 16 ? 1 : L <= 24 ? 2 : 3;
   } else if (pt->axis == AX_L4D || pt->axis == AX_L4S) {
     k->band = 0;
     if ((k->lo >> 16) != (k->hi >> 16)) return false;
@@ -316,8 +318,8 @@ bool atom_key(const Atom& a, AtomKey* k) {
 
 uint64_t atom_span(const AtomKey& k) {  // number of bucket-key values the atom covers
   if (k.axis <= AX_CTDST) {
-    if (k.band == 0) return (k.hi >> 16) - (k.lo >> 16) + 1;
-    if (k.band == 1) return (k.hi >> 8) - (k.lo >> 8) + 1;
+    const uint32_t sh = ip_band_shift(k.band);
+    return uint64_t(k.hi >> sh) - (k.lo >> sh) + 1;
   }
   if (k.axis == AX_L4D || k.axis == AX_L4S) return ((k.hi & 0xffffu) >> 3) - ((k.lo & 0xffffu) >> 3) + 1;
   return uint64_t(k.hi) - k.lo + 1;
@@ -326,13 +328,8 @@ uint64_t atom_span(const AtomKey& k) {  // number of bucket-key values the atom 
 void atom_bucket_list(const AtomKey& k, uint32_t bits, std::vector<uint32_t>* out) {
   out->clear();
   if (k.axis <= AX_CTDST) {
-    if (k.band == 0) {
-      for (uint32_t b = k.lo >> 16; b <= (k.hi >> 16); b++) out->push_back(b);
-    } else if (k.band == 1) {
-      for (uint32_t t = k.lo >> 8; t <= (k.hi >> 8); t++) out->push_back(bucket_of(k.axis, 1, bits, t << 8));
-    } else {
-      for (uint64_t v = k.lo; v <= k.hi; v++) out->push_back(bucket_of(k.axis, 2, bits, uint32_t(v)));
-    }
+    const uint32_t sh = ip_band_shift(k.band);
+    for (uint64_t t = k.lo >> sh; t <= (k.hi >> sh); t++) out->push_back(bucket_of(k.axis, k.band, bits, uint32_t(t << sh)));
   } else if (k.axis == AX_L4D || k.axis == AX_L4S) {
     uint32_t b0 = bucket_of(k.axis, 0, 16, k.lo), b1 = bucket_of(k.axis, 0, 16, k.hi);
     for (uint32_t b = b0; b <= b1; b++) out->push_back(b);
@@ -632,6 +629,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     th.n_rules = uint32_t(rs.size());
     // records (rank order), then this table's external data
     std::vector<uint32_t> rec_off(rs.size());
+    const uint32_t tbl_start = uint32_t(B.w.size());
     std::vector<uint32_t> ext;
     std::vector<std::pair<uint32_t, uint32_t>> abs_patches;  // (absolute record word, ext offset)
     std::vector<uint32_t> hard_offs;
@@ -687,6 +685,8 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     B.align(16);
     th.end_off = uint32_t(B.w.size()) + 1;
     uint32_t ext_base = uint32_t(B.w.size());
+    out->bytes_records += 4ull * (ext_base - tbl_start);
+    out->bytes_ext += 4ull * ext.size();
     B.w.insert(B.w.end(), ext.begin(), ext.end());
     for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
     th.n_hard = uint32_t(hard_offs.size());
@@ -736,11 +736,14 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
         }
         uint8_t axis = order[i].second.first, band = order[i].second.second;
         uint32_t bits = 16;
-        if (axis <= AX_CTDST && band > 0) {  // hashed bands: ~2 buckets per entry
-          uint64_t ent = 0;
-          for (auto& e : v) ent += atom_span(e.first);
-          bits = 10;
-          while (bits < 22 && (1ull << bits) < 2 * ent) bits++;
+        if (axis <= AX_CTDST) {
+          if (band == 0) bits = 12;
+          if (band >= 2) {  // hashed bands: about one bucket per entry
+            uint64_t ent = 0;
+            for (auto& e : v) ent += atom_span(e.first);
+            bits = 10;
+            while (bits < 22 && (1ull << bits) < ent) bits++;
+          }
         }
         std::vector<std::pair<uint32_t, std::array<uint32_t, 4>>> be;  // (bucket, entry)
         for (auto& e : v) {
@@ -761,6 +764,11 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
         si.bits = uint8_t(bits);
         si.off = B.put(offs.data(), offs.size(), 16);
         si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
+        out->bytes_bucket_offsets += 4ull * offs.size();
+        if (std::getenv("GPC_IMAGE_DEBUG"))
+          std::fprintf(stderr, "table %d clause %d axis %u band %u bits %u atoms %zu entries %zu\n", t, k, axis, band, bits,
+                       v.size(), be.size());
+        out->bytes_entries += 4ull * ents.size();
       }
       std::sort(always.begin(), always.end());
       always.erase(std::unique(always.begin(), always.end()), always.end());
@@ -768,6 +776,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       for (auto& e : always) aw.insert(aw.end(), e.begin(), e.end());
       th.always_n[k] = uint32_t(always.size());
       th.always_off[k] = always.empty() ? 0 : B.put(aw.data(), aw.size(), 16);
+      out->bytes_entries += 4ull * aw.size();
     }
     out->n_rules[t - 1] = th.n_rules;
     out->n_hard[t - 1] = th.n_hard;
@@ -783,6 +792,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
   }
   out->hdr.hash_log2 = lg;
   out->hdr.hash_off = B.put(tab.data(), tab.size(), 16);
+  out->bytes_hash = 8ull * tab.size();
   out->hdr.n_slots = slots.size();
   B.align(16);
   out->blob = std::move(B.w);

@@ -15,6 +15,7 @@ struct HostImage {
   std::vector<uint32_t> blob;        // hdr offsets index this (uint32 words)
   uint32_t n_rules[6] = {0}, n_hard[6] = {0};
   uint32_t n_flows = 0;
+  uint64_t bytes_records = 0, bytes_ext = 0, bytes_bucket_offsets = 0, bytes_entries = 0, bytes_hash = 0;
   std::string error;                 // non-empty: unsupported flow shape
 };
 

@@ -79,7 +79,9 @@ class gpc_rule_metric(C.Structure):
 
 class gpc_image_stats(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("device_bytes", C.c_uint64), ("n_rules", C.c_uint32 * 6),
-                ("n_hard", C.c_uint32 * 6), ("n_flows", C.c_uint32), ("n_counter_slots", C.c_uint32)]
+                ("n_hard", C.c_uint32 * 6), ("n_flows", C.c_uint32), ("n_counter_slots", C.c_uint32),
+                ("bytes_records", C.c_uint64), ("bytes_ext", C.c_uint64), ("bytes_bucket_offsets", C.c_uint64),
+                ("bytes_entries", C.c_uint64), ("bytes_hash", C.c_uint64)]
 
 
 EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "gpc_batch_install",
@@ -378,4 +380,6 @@ class Classifier:
         st = gpc_image_stats()
         _check(self.lib.gpc_get_image_stats(self.h, C.byref(st)), "gpc_get_image_stats")
         return {"epoch": st.epoch, "device_bytes": st.device_bytes, "n_rules": list(st.n_rules),
-                "n_hard": list(st.n_hard), "n_flows": st.n_flows, "n_counter_slots": st.n_counter_slots}
+                "n_hard": list(st.n_hard), "n_flows": st.n_flows, "n_counter_slots": st.n_counter_slots,
+                "bytes": {"records": st.bytes_records, "ext": st.bytes_ext, "bucket_offsets": st.bytes_bucket_offsets,
+                          "entries": st.bytes_entries, "hash": st.bytes_hash}}

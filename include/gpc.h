@@ -218,6 +218,11 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint32_t n_hard[6];
   uint32_t n_flows;
   uint32_t n_counter_slots;
+  uint64_t bytes_records;        /* rule records (headers + inline clauses)                   */
+  uint64_t bytes_ext;            /* out-of-line clause data                                    */
+  uint64_t bytes_bucket_offsets; /* driver-index bucket offset arrays                          */
+  uint64_t bytes_entries;        /* driver-index entries (16 B each) incl. always lists        */
+  uint64_t bytes_hash;           /* image-wide point hash                                      */
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */
