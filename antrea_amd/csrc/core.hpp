@@ -55,6 +55,7 @@ enum Axis : uint8_t {
 //   w2 flags byte (RecFlags) | off0 << 8 | off1 << 16 | off2 << 24   (word offsets of the clauses)
 //   w3 counter slot
 //   w4 tier | rid << 8                                               (rid: image-wide rule id)
+//   w5 clauses decided exactly by a passing driver entry: bits 0-2 (driver clause 0), 3-5 (1)
 // clause k at word off_k: nseg, then nseg segments, each a tag word kind | axis << 4 | n << 8
 // followed by its data:
 //   SK_IVAL  2n words, sorted disjoint [lo,hi]     SK_XIVAL  1 word: offset of the 2n words
@@ -73,7 +74,7 @@ GPC_HD uint32_t rec_has_act(uint32_t w2) { return (w2 >> 4) & 1u; }
 GPC_HD uint32_t rec_counted(uint32_t w2) { return (w2 >> 5) & 1u; }
 GPC_HD uint32_t rec_nclauses(uint32_t w2) { return (w2 >> 6) & 3u; }
 GPC_HD uint32_t rec_off(uint32_t w2, uint32_t k) { return (w2 >> (8 + 8 * k)) & 0xffu; }
-constexpr uint32_t kRecHdrWords = 5;
+constexpr uint32_t kRecHdrWords = 6;
 constexpr uint32_t kBoxWords = 7;
 
 constexpr int kMaxClauses = 3;
@@ -307,13 +308,15 @@ GPC_HD bool clause_match(const Img& im, uint32_t table, uint32_t k, uint32_t rid
 
 // All clauses of a record; clause `last` (the driver, already a likely hit) is checked last
 // (last >= n_clauses: natural order). One clause_match call site keeps the code small.
+// `skip`: clauses already decided (the entry's exact interval test).
 GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint32_t w2, uint32_t rid, uint32_t last,
-                       const Pkt& p) {
+                       uint32_t skip, const Pkt& p) {
   const uint32_t ncl = rec_nclauses(w2);
   const uint32_t first = last < ncl ? last + 1 : 0;
   for (uint32_t j = 0; j < ncl; j++) {
     uint32_t k = first + j;
     if (k >= ncl) k -= ncl;
+    if ((skip >> k) & 1u) continue;
     if (!clause_match(im, table, k, rid, rec + rec_off(w2, k), p)) return false;
   }
   return true;
@@ -353,10 +356,10 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
     if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
       if ((w1 & 0xffffu) != hprio) break;
-      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, p)) res.tie = 1;
+      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, 0, p)) res.tie = 1;
       continue;
     }
-    if (rule_match(im, table, rec, w2, rid, 3, p)) {
+    if (rule_match(im, table, rec, w2, rid, 3, 0, p)) {
       rH = off;
       hprio = w1 & 0xffffu;
       hverdict = rec_verdict(w2);
@@ -474,7 +477,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
 #ifdef GPC_ABL_NOVERIFY  // timing experiment only: read the record header, skip the clauses
       if (w2 != 0xffffffffu) continue;
 #endif
-      if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, p)) {
+      if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, (rec[5] >> (3 * d)) & 7u, p)) {
         GPC_STAT(5, 1);
         continue;
       }

@@ -435,13 +435,68 @@ double hull_coverage(uint8_t axis, uint32_t lo, uint32_t hi, const uint64_t* spa
   return 1.0;
 }
 
+// True if the clause's match set is exactly [lo, hi] on `axis` (single-term atoms whose ranges
+// merge into one interval), so a passing interval test decides the clause.
+bool clause_is_interval(const std::vector<Atom>& atoms, uint8_t axis, uint32_t lo, uint32_t hi) {
+  std::vector<std::pair<uint32_t, uint32_t>> iv;
+  for (auto& a : atoms) {
+    if (a.t.size() != 1 || a.t[0].axis != axis || !is_prefix(a.t[0].mask)) return false;
+    uint32_t l = a.t[0].val & a.t[0].mask;
+    iv.push_back({l, l | ~a.t[0].mask});
+  }
+  std::sort(iv.begin(), iv.end());
+  uint32_t cur = iv[0].first;
+  if (cur != lo) return false;
+  uint64_t reach = iv[0].second;
+  for (auto& x : iv) {
+    if (uint64_t(x.first) > reach + 1) return false;
+    reach = std::max<uint64_t>(reach, x.second);
+  }
+  return reach == hi;
+}
+
+struct IvalChoice {
+  int clause = -1;
+  uint32_t axis = kFiltNoAxis, lo = 0, hi = 0;
+  bool exact = false;
+};
+
+// The non-driver clause whose hull covers the smallest fraction of its axis (entry interval test).
+IvalChoice choose_interval(const RuleB& r, int d, const uint64_t* span) {
+  IvalChoice ch;
+  double best = 0.5;  // an interval covering more than half of its axis is not worth a check
+  for (int c = 0; c < r.n; c++) {
+    if (c == d || r.clause[c].empty()) continue;
+    for (auto& t : r.clause[c][0].t) {
+      if (t.axis >= AX_CTST) continue;
+      uint32_t lo, hi;
+      if (!clause_hull(r.clause[c], t.axis, &lo, &hi)) continue;
+      double cov = hull_coverage(t.axis, lo, hi, span);
+      if (cov < best) {
+        best = cov;
+        ch.clause = c;
+        ch.axis = t.axis;
+        ch.lo = lo;
+        ch.hi = hi;
+      }
+    }
+  }
+  if (ch.clause >= 0) ch.exact = clause_is_interval(r.clause[ch.clause], uint8_t(ch.axis), ch.lo, ch.hi);
+  return ch;
+}
+
+// Clauses a passing entry of driver d has already decided (record word 5, core.hpp).
+uint32_t skip_mask(const RuleB& r, int d, const uint64_t* span) {
+  if (d >= r.n) return 0;
+  IvalChoice ch = choose_interval(r, d, span);
+  return ch.exact ? (1u << ch.clause) : 0u;
+}
+
 // Driver entry (core.hpp Ent) of rule r for driver clause d at record offset `off`; `span` = value
-// span of each exact axis over the table's atoms.
+// span of each IP / exact axis over the table's atoms.
 std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint64_t* span) {
   uint32_t axis = kFiltNoAxis, ipbits = 0, l4bits = kFiltL4All;
   bool have_ip = false, have_l4 = false;
-  uint32_t iax = kFiltNoAxis, ilo = 0, ihi = 0;
-  double best = 0.5;  // an interval covering more than half of its axis is not worth a check
   for (int c = 0; c < r.n; c++) {
     if (c == d) continue;
     uint32_t ax, b;
@@ -453,21 +508,9 @@ std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint
       ipbits = b;
       have_ip = true;
     }
-    if (r.clause[c].empty()) continue;
-    for (auto& t : r.clause[c][0].t) {
-      if (t.axis >= AX_CTST) continue;
-      uint32_t lo, hi;
-      if (!clause_hull(r.clause[c], t.axis, &lo, &hi)) continue;
-      double cov = hull_coverage(t.axis, lo, hi, span);
-      if (cov < best) {
-        best = cov;
-        iax = t.axis;
-        ilo = lo;
-        ihi = hi;
-      }
-    }
   }
-  return {((off >> 4) << 8) | (iax << 4) | axis, ipbits | l4bits, ilo, ihi};
+  IvalChoice ch = choose_interval(r, d, span);
+  return {((off >> 4) << 8) | (ch.axis << 4) | axis, ipbits | l4bits, ch.lo, ch.hi};
 }
 
 bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vector<uint64_t>* tab) {
@@ -627,6 +670,22 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     });
     TableHdr& th = out->hdr.t[t - 1];
     th.n_rules = uint32_t(rs.size());
+    // value span of the exact axes over this table's soft rules (interval prefilter selectivity)
+    uint64_t span[AX_N] = {0};
+    {
+      uint32_t mn[AX_N], mx[AX_N];
+      for (int a = 0; a < AX_N; a++) mn[a] = 0xffffffffu, mx[a] = 0;
+      for (RuleB* rp : rs)
+        if (!rp->hard)
+          for (int c = 0; c < rp->n; c++)
+            for (auto& at : rp->clause[c])
+              for (auto& t : at.t) {
+                mn[t.axis] = std::min(mn[t.axis], t.val & t.mask);
+                mx[t.axis] = std::max(mx[t.axis], (t.val & t.mask) | ~t.mask);
+              }
+      for (int a = 0; a < AX_N; a++) span[a] = mx[a] >= mn[a] ? uint64_t(mx[a]) - mn[a] + 1 : 0;
+    }
+
     // records (rank order), then this table's external data
     std::vector<uint32_t> rec_off(rs.size());
     const uint32_t tbl_start = uint32_t(B.w.size());
@@ -674,6 +733,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       rec[2] = flags | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
       rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0;
       rec[4] = uint32_t(r.tier) | (rid << 8);
+      rec[5] = r.hard ? 0u : (skip_mask(r, 0, span) | (skip_mask(r, 1, span) << 3));
       if (base >= (1u << 28)) {  // Ent.x holds record offset / 16 in 24 bits
         out->error = "rule records exceed 1 GiB";
         return -GPC_ENOMEM;
@@ -691,21 +751,6 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
     th.n_hard = uint32_t(hard_offs.size());
     th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
-    // value span of the exact axes over this table's soft rules (interval prefilter selectivity)
-    uint64_t span[AX_N] = {0};
-    {
-      uint32_t mn[AX_N], mx[AX_N];
-      for (int a = 0; a < AX_N; a++) mn[a] = 0xffffffffu, mx[a] = 0;
-      for (RuleB* rp : rs)
-        if (!rp->hard)
-          for (int c = 0; c < rp->n; c++)
-            for (auto& at : rp->clause[c])
-              for (auto& t : at.t) {
-                mn[t.axis] = std::min(mn[t.axis], t.val & t.mask);
-                mx[t.axis] = std::max(mx[t.axis], (t.val & t.mask) | ~t.mask);
-              }
-      for (int a = 0; a < AX_N; a++) span[a] = mx[a] >= mn[a] ? uint64_t(mx[a]) - mn[a] + 1 : 0;
-    }
     // driver indexes for clauses 0 and 1 of the soft rules; entries carry the non-driver filter
     for (int k = 0; k < 2; k++) {
       std::vector<std::array<uint32_t, 4>> always;
