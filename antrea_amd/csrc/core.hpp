@@ -332,6 +332,10 @@ GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
 }
 
 constexpr int kLists = kIdxPerClause + 1;  // always list + sub-indexes of the driver clause
+#ifndef GPC_SCAN_UNROLL
+#define GPC_SCAN_UNROLL 4
+#endif
+constexpr int kScanUnroll = GPC_SCAN_UNROLL;  // entry loads in flight per lane in the candidate scan
 
 // One rule table (table = 1..6). All per-list merge state is indexed with compile-time indices
 // only (unrolled), so it stays in VGPRs.
@@ -437,24 +441,34 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     uint32_t c0 = 0xffffffffu, c1 = 0xffffffffu;
     bool more = false;
     // wave-uniform trip count (the wave's longest candidate list); finished lanes read the zero
-    // entry at index 0 (offset 0 is never a record), so the body has no divergent branches
-    for (uint32_t j = 0; GPC_WAVE_ANY(j < total); j++) {
-      uint32_t idx = base[0] + j;
+    // entry at index 0 (offset 0 is never a record), so the body has no divergent branches.
+    // kScanUnroll entries are loaded before any is used: that many loads in flight per lane.
+    for (uint32_t j0 = 0; GPC_WAVE_ANY(j0 < total); j0 += kScanUnroll) {
+      Ent ev[kScanUnroll];
 #pragma unroll
-      for (int l = 1; l < kLists; l++)
-        if (j >= upto[l - 1]) idx = base[l] + (j - upto[l - 1]);
-      idx = j < total ? idx : 0u;
-      GPC_TOUCH(&E[idx], 16);
-      const Ent e = E[idx];
-      const uint32_t off = ent_off(e.x);
-      GPC_STAT(4, j < total ? 1 : 0);
-      const bool pass = (off > after) & (off < rH) & entry_pass(p, e);
-      const uint32_t v = pass ? off : 0xffffffffu;
-      const bool fresh = (v != 0xffffffffu) & (v != c0) & (v != c1);
-      more |= fresh & (c1 != 0xffffffffu);  // a third distinct survivor: one of them is dropped
-      const bool lt0 = fresh & (v < c0), lt1 = fresh & (v < c1);
-      c1 = lt0 ? c0 : (lt1 ? v : c1);
-      c0 = lt0 ? v : c0;
+      for (int u = 0; u < kScanUnroll; u++) {
+        const uint32_t j = j0 + u;
+        uint32_t idx = base[0] + j;
+#pragma unroll
+        for (int l = 1; l < kLists; l++)
+          if (j >= upto[l - 1]) idx = base[l] + (j - upto[l - 1]);
+        idx = j < total ? idx : 0u;
+        GPC_TOUCH(&E[idx], 16);
+        GPC_STAT(4, j < total ? 1 : 0);
+        ev[u] = E[idx];
+      }
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; u++) {
+        const Ent& e = ev[u];
+        const uint32_t off = ent_off(e.x);
+        const bool pass = (off > after) & (off < rH) & entry_pass(p, e);
+        const uint32_t v = pass ? off : 0xffffffffu;
+        const bool fresh = (v != 0xffffffffu) & (v != c0) & (v != c1);
+        more |= fresh & (c1 != 0xffffffffu);  // a third distinct survivor: one of them is dropped
+        const bool lt0 = fresh & (v < c0), lt1 = fresh & (v < c1);
+        c1 = lt0 ? c0 : (lt1 ? v : c1);
+        c0 = lt0 ? v : c0;
+      }
     }
 #pragma unroll
     for (int q = 0; q < 2; q++) {
