@@ -21,7 +21,7 @@ LIB = os.path.join(OUT, "libgpc.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-HOST_SRCS = ["compiler.cpp", "image.cpp"]
+HOST_SRCS = ["compiler.cpp", "image.cpp", "flowtext.cpp"]
 HIP_SRCS = ["classify.hip", "api.cpp"]
 HEADERS = ["model.hpp", "compiler.hpp", "core.hpp", "image.hpp", "launch.hpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]

@@ -5,7 +5,10 @@
 
 #include <atomic>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -16,12 +19,60 @@
 
 using namespace gpc;
 
-struct DevEpoch {
+// Device memory of the epochs is allocated and freed stream-ordered on the context's upload stream
+// (non-blocking), so a commit never waits for classification launches in flight on other streams.
+static hipError_t dev_alloc(void** p, size_t bytes, hipStream_t s) {
+  hipError_t e = hipMallocAsync(p, bytes, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    e = hipMalloc(p, bytes);
+  }
+  return e;
+}
+static void dev_free(void* p, hipStream_t s) {
+  if (p && hipFreeAsync(p, s) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(p);
+  }
+}
+
+struct DevImage {  // one uploaded image (freed when the last epoch using it retires)
   ImageHdr* d_hdr = nullptr;
   uint32_t* d_blob = nullptr;
   size_t bytes = 0;
-  uint64_t epoch = 0;
+  hipStream_t s = nullptr;
+  ~DevImage() {
+    dev_free(d_hdr, s);
+    dev_free(d_blob, s);
+  }
 };
+
+struct DevEpoch {
+  std::shared_ptr<DevImage> base, ovl;  // base shared by the delta epochs built on it
+  uint32_t* d_dead = nullptr;           // tombstones over base rule ids (delta epochs)
+  uint64_t epoch = 0;
+  std::map<hipStream_t, hipEvent_t> last_use;  // last launch on each stream that used this epoch
+};
+
+struct RetiredEpoch {
+  DevEpoch e;
+  bool drained() const {
+    for (auto& kv : e.last_use)
+      if (hipEventQuery(kv.second) == hipErrorNotReady) return false;
+    return true;
+  }
+  void release(hipStream_t s) {
+    for (auto& kv : e.last_use) (void)hipEventDestroy(kv.second);
+    dev_free(e.d_dead, s);
+    e = DevEpoch();
+  }
+};
+
+// Delta commits: rules changed since the last full build are rebuilt into an overlay image and
+// tombstoned in the base. A full rebuild (compaction) happens when the changed set exceeds
+// max(kDeltaMinRules, base rules / kDeltaFraction).
+constexpr size_t kDeltaMinRules = 2048;
+constexpr size_t kDeltaFraction = 32;
 
 struct gpc_ctx {
   gpc_config cfg;
@@ -29,23 +80,51 @@ struct gpc_ctx {
   std::mutex data;   // epoch pointer swap vs. kernel launch
   FeatureNP np;
   SlotMap slots;
-  HostImage last;    // last committed host image: shadow state for device re-upload + debug export
+  HostImage last;    // base image of the current epoch: shadow state for re-upload + debug export
+  HostImage ovl;     // overlay of the current epoch (empty blob: none)
+  std::vector<uint32_t> dead;            // tombstone bitmap of the current epoch (host copy)
+  std::set<uint32_t> pending_conj;       // rules changed since the last full build
+  uint8_t pending_hard = 0;              // rule tables whose hard flows changed since then
   DevEpoch cur;
+  std::vector<RetiredEpoch> retired;
+  hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
   unsigned long long* d_counters = nullptr;
   size_t counter_cap = 0;  // slots
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
-  uint64_t epoch = 0;
+  uint64_t epoch = 0, n_full = 0, n_delta = 0;
   explicit gpc_ctx(const gpc_config& c) : cfg(c), np(c) {}
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : -GPC_EDEV; }
 
-static void free_epoch(DevEpoch& e) {
-  if (e.d_hdr) (void)hipFree(e.d_hdr);
-  if (e.d_blob) (void)hipFree(e.d_blob);
-  e = DevEpoch();
+static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevImage>* out) {
+  auto d = std::make_shared<DevImage>();
+  d->s = s;
+  d->bytes = h.blob.size() * 4;
+  if (hip_ok(dev_alloc((void**)&d->d_blob, d->bytes, s)) || hip_ok(dev_alloc((void**)&d->d_hdr, sizeof(ImageHdr), s)) ||
+      hip_ok(hipMemcpyAsync(d->d_blob, h.blob.data(), d->bytes, hipMemcpyHostToDevice, s)) ||
+      hip_ok(hipMemcpyAsync(d->d_hdr, &h.hdr, sizeof(ImageHdr), hipMemcpyHostToDevice, s)))
+    return -GPC_EDEV;
+  *out = std::move(d);
+  return GPC_OK;
 }
+
+static void collect_retired(gpc_ctx* ctx, bool wait) {
+  if (wait && !ctx->retired.empty()) (void)hipDeviceSynchronize();
+  size_t k = 0;
+  for (size_t i = 0; i < ctx->retired.size(); i++) {
+    if (wait || ctx->retired[i].drained()) {
+      ctx->retired[i].release(ctx->ustream);
+    } else {
+      if (k != i) ctx->retired[k] = std::move(ctx->retired[i]);
+      k++;
+    }
+  }
+  ctx->retired.resize(k);
+}
+
+static int commit_impl(gpc_ctx* ctx, bool force_full);
 
 extern "C" {
 
@@ -78,11 +157,16 @@ int gpc_create(const gpc_config* cfg, gpc_ctx** out) {
 
 void gpc_destroy(gpc_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->cur.d_blob || ctx->d_counters) {
+  if (ctx->cur.base || ctx->d_counters || !ctx->retired.empty()) {
     (void)hipSetDevice(ctx->cfg.device);
     (void)hipDeviceSynchronize();
-    free_epoch(ctx->cur);
+    ctx->retired.push_back(RetiredEpoch{std::move(ctx->cur)});
+    collect_retired(ctx, true);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->ustream) {
+      (void)hipStreamSynchronize(ctx->ustream);
+      (void)hipStreamDestroy(ctx->ustream);
+    }
   }
   delete ctx;
 }
@@ -147,6 +231,44 @@ int gpc_reassign_priorities(gpc_ctx* ctx, const uint16_t* from, const uint16_t* 
   return ctx->np.reassign_priorities(from, to, n, table);
 }
 
+int gpc_load_flows(gpc_ctx* ctx, const char* text, size_t len, int32_t replace, size_t* n_loaded, size_t* n_skipped,
+                   size_t* err_line) {
+  if (!ctx || (!text && len)) return -GPC_EINVAL;
+  std::vector<Flow> flows;
+  size_t loaded = 0, skipped = 0, line_no = 0;
+  size_t pos = 0;
+  while (pos < len) {
+    size_t e = pos;
+    while (e < len && text[e] != '\n') e++;
+    std::string line(text + pos, e - pos);
+    pos = e + 1;
+    line_no++;
+    Flow f;
+    std::string err;
+    int r = parse_flow_text(line, &f, &err);
+    if (r < 0) {
+      if (err_line) *err_line = line_no;
+      return r;
+    }
+    if (r == 0) {
+      if (line.find_first_not_of(" \t\r") != std::string::npos) skipped++;
+      continue;
+    }
+    flows.push_back(std::move(f));
+    loaded++;
+  }
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  try {
+    int rc = ctx->np.load_flows(flows, replace != 0);
+    if (rc) return rc;
+  } catch (...) {
+    return -GPC_ENOMEM;
+  }
+  if (n_loaded) *n_loaded = loaded;
+  if (n_skipped) *n_skipped = skipped;
+  return GPC_OK;
+}
+
 int gpc_get_policy_info(gpc_ctx* ctx, uint32_t rule_id, gpc_policy_info* out) {
   if (!ctx || !out) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
@@ -166,77 +288,23 @@ int gpc_dump_flows(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   return GPC_OK;
 }
 
-int gpc_commit(gpc_ctx* ctx) {
-  if (!ctx) return -GPC_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->ctl);
-  HostImage img;
-  int rc;
-  try {
-    rc = build_image(ctx->np, ctx->slots, &img);
-  } catch (...) {
-    return -GPC_ENOMEM;
-  }
-  if (rc) return rc;
-  ctx->slot_conj = ctx->slots.slot_conj();
-  ctx->last = std::move(img);
-  const HostImage& himg = ctx->last;
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  DevEpoch ne;
-  size_t bytes = himg.blob.size() * 4;
-  if (hip_ok(hipMalloc(&ne.d_blob, bytes)) || hip_ok(hipMalloc(&ne.d_hdr, sizeof(ImageHdr)))) {
-    free_epoch(ne);
-    return -GPC_EDEV;
-  }
-  if (hip_ok(hipMemcpy(ne.d_blob, himg.blob.data(), bytes, hipMemcpyHostToDevice)) ||
-      hip_ok(hipMemcpy(ne.d_hdr, &himg.hdr, sizeof(ImageHdr), hipMemcpyHostToDevice))) {
-    free_epoch(ne);
-    return -GPC_EDEV;
-  }
-  ne.bytes = bytes;
-  ne.epoch = ++ctx->epoch;
-  // counters: grow to the slot count, zero released slots (their Metric flows were deleted)
-  size_t need = ctx->slots.size() ? ctx->slots.size() : 1;
-  unsigned long long* nc = ctx->d_counters;
-  bool grow = need > ctx->counter_cap;
-  if (grow) {
-    size_t cap = std::max(need, ctx->counter_cap * 2);
-    if (hip_ok(hipMalloc(&nc, cap * kCounterBytes)) || hip_ok(hipMemset(nc, 0, cap * kCounterBytes))) {
-      free_epoch(ne);
-      return -GPC_EDEV;
-    }
-    if (ctx->d_counters) {
-      (void)hipDeviceSynchronize();
-      (void)hipMemcpy(nc, ctx->d_counters, ctx->counter_cap * kCounterBytes, hipMemcpyDeviceToDevice);
-    }
-  }
-  DevEpoch old;
-  unsigned long long* old_counters = nullptr;
-  {
-    std::lock_guard<std::mutex> d(ctx->data);
-    old = ctx->cur;
-    ctx->cur = ne;
-    if (grow) {
-      old_counters = ctx->d_counters;
-      ctx->d_counters = nc;
-      ctx->counter_cap = std::max(need, ctx->counter_cap * 2);
-    }
-  }
-  (void)hipDeviceSynchronize();  // in-flight launches of the previous epoch drain here
-  free_epoch(old);
-  if (old_counters) (void)hipFree(old_counters);
-  for (uint32_t s : ctx->released_slots)
-    if (s < ctx->counter_cap) (void)hipMemset(ctx->d_counters + kCounterWords * size_t(s), 0, kCounterBytes);
-  ctx->released_slots.clear();
-  return GPC_OK;
-}
+int gpc_commit(gpc_ctx* ctx) { return commit_impl(ctx, false); }
+int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
 
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
   if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
   if (n && (!pk->src || !pk->dst || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
-  if (!ctx->cur.d_blob) return -GPC_EINVAL;  // nothing committed yet
+  if (!ctx->cur.base) return -GPC_EINVAL;  // nothing committed yet
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  return launch_classify(ctx->cur.d_hdr, ctx->cur.d_blob, *pk, n, out, ctx->d_counters, count, (hipStream_t)stream);
+  EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.d_dead, ctx->cur.ovl ? ctx->cur.ovl->d_hdr : nullptr,
+               ctx->cur.ovl ? ctx->cur.ovl->d_blob : nullptr};
+  hipStream_t st = (hipStream_t)stream;
+  int rc = launch_classify(ep, *pk, n, out, ctx->d_counters, count, st);
+  if (rc || n == 0) return rc;
+  hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained
+  if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
+  return hip_ok(hipEventRecord(ev, st));
 }
 
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count) {
@@ -329,7 +397,12 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   std::lock_guard<std::mutex> g(ctx->ctl);
   std::memset(out, 0, sizeof *out);
   out->epoch = ctx->epoch;
-  out->device_bytes = ctx->cur.bytes;
+  out->device_bytes = ctx->cur.base ? ctx->cur.base->bytes : 0;
+  out->overlay_bytes = ctx->cur.ovl ? ctx->cur.ovl->bytes : 0;
+  for (int i = 0; i < 6; i++) out->n_overlay_rules += ctx->ovl.n_rules[i];
+  for (uint32_t w : ctx->dead) out->n_tombstones += uint32_t(__builtin_popcount(w));
+  out->n_full_builds = ctx->n_full;
+  out->n_delta_builds = ctx->n_delta;
   for (int i = 0; i < 6; i++) {
     out->n_rules[i] = ctx->last.n_rules[i];
     out->n_hard[i] = ctx->last.n_hard[i];
@@ -354,4 +427,130 @@ int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const 
   return GPC_OK;
 }
 
+int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** oblob, size_t* on_words, const void** ohdr, const uint32_t** dead,
+                    size_t* dead_words) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  const bool has = !ctx->ovl.blob.empty();
+  if (oblob) *oblob = has ? ctx->ovl.blob.data() : nullptr;
+  if (on_words) *on_words = ctx->ovl.blob.size();
+  if (ohdr) *ohdr = has ? &ctx->ovl.hdr : nullptr;
+  if (dead) *dead = ctx->dead.empty() ? nullptr : ctx->dead.data();
+  if (dead_words) *dead_words = ctx->dead.size();
+  return GPC_OK;
+}
+
 }  // extern "C"
+
+// Builds the next epoch (full or delta) on the host, uploads it and publishes it atomically.
+// Host shadow state (last / ovl / dead) is updated before the upload, so tests on a host without a
+// device still see the image (the call then returns GPC_EDEV).
+static int commit_impl(gpc_ctx* ctx, bool force_full) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  FeatureNP::Dirty dirty = ctx->np.take_dirty();
+  ctx->pending_conj.insert(dirty.conj.begin(), dirty.conj.end());
+  ctx->pending_hard |= dirty.hard_tables;
+  const bool have_base = !ctx->last.blob.empty();
+  bool full = force_full || !have_base || ctx->last.any_noact || ctx->np.foreign() ||
+              ctx->pending_conj.size() > std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction);
+  HostImage ovl;
+  int rc = GPC_OK;
+  try {
+    if (!full) {
+      rc = build_overlay(ctx->np, ctx->slots, ctx->pending_conj, ctx->pending_hard, &ovl);
+      if (rc) return rc;
+      if (ovl.any_noact) full = true;
+    }
+    if (full) {
+      HostImage img;
+      rc = build_image(ctx->np, ctx->slots, &img);
+      if (rc) return rc;
+      ctx->last = std::move(img);
+      ctx->ovl = HostImage();
+      ctx->dead.clear();
+      ctx->pending_conj.clear();
+      ctx->pending_hard = 0;
+    } else {
+      std::vector<uint32_t> dead((ctx->last.n_rids + 31) / 32, 0u);
+      for (uint32_t c : ctx->pending_conj) {
+        auto it = ctx->last.conj_rid.find(c);
+        if (it != ctx->last.conj_rid.end()) dead[it->second >> 5] |= 1u << (it->second & 31u);
+      }
+      for (int t = 0; t < 6; t++)
+        if ((ctx->pending_hard >> t) & 1u)
+          for (uint32_t rid : ctx->last.hard_rids[t]) dead[rid >> 5] |= 1u << (rid & 31u);
+      uint32_t n_ovl = 0;
+      for (int t = 0; t < 6; t++) n_ovl += ovl.n_rules[t];
+      ctx->ovl = n_ovl ? std::move(ovl) : HostImage();
+      ctx->dead = std::move(dead);
+    }
+  } catch (...) {
+    return -GPC_ENOMEM;
+  }
+  ctx->slot_conj = ctx->slots.slot_conj();
+  if (full) ctx->n_full++;
+  else ctx->n_delta++;
+  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  if (!ctx->ustream && hip_ok(hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking))) return -GPC_EDEV;
+  hipStream_t us = ctx->ustream;
+  collect_retired(ctx, false);
+  DevEpoch ne;
+  if (full) {
+    if ((rc = upload_image(ctx->last, us, &ne.base))) return rc;
+  } else {
+    ne.base = ctx->cur.base;
+    if (!ne.base && (rc = upload_image(ctx->last, us, &ne.base))) return rc;
+    if (!ctx->ovl.blob.empty() && (rc = upload_image(ctx->ovl, us, &ne.ovl))) return rc;
+    if (!ctx->dead.empty()) {
+      size_t b = ctx->dead.size() * 4;
+      if (hip_ok(dev_alloc((void**)&ne.d_dead, b, us)) ||
+          hip_ok(hipMemcpyAsync(ne.d_dead, ctx->dead.data(), b, hipMemcpyHostToDevice, us))) {
+        RetiredEpoch{std::move(ne)}.release(us);
+        return -GPC_EDEV;
+      }
+    }
+  }
+  ne.epoch = ++ctx->epoch;
+  // counters: grow to the slot count, zero released slots (their Metric flows were deleted)
+  size_t need = ctx->slots.size() ? ctx->slots.size() : 1;
+  unsigned long long* nc = ctx->d_counters;
+  bool grow = need > ctx->counter_cap;
+  if (grow) {
+    size_t cap = std::max(need, ctx->counter_cap * 2);
+    if (hip_ok(hipMalloc(&nc, cap * kCounterBytes)) || hip_ok(hipMemset(nc, 0, cap * kCounterBytes))) {
+      RetiredEpoch{std::move(ne)}.release(us);
+      return -GPC_EDEV;
+    }
+    if (ctx->d_counters) {
+      (void)hipDeviceSynchronize();
+      (void)hipMemcpy(nc, ctx->d_counters, ctx->counter_cap * kCounterBytes, hipMemcpyDeviceToDevice);
+    }
+  }
+  if (hip_ok(hipStreamSynchronize(us))) {  // the new epoch is resident before it is published
+    RetiredEpoch{std::move(ne)}.release(us);
+    return -GPC_EDEV;
+  }
+  DevEpoch old;
+  unsigned long long* old_counters = nullptr;
+  {
+    std::lock_guard<std::mutex> d(ctx->data);
+    old = std::move(ctx->cur);
+    ctx->cur = std::move(ne);
+    if (grow) {
+      old_counters = ctx->d_counters;
+      ctx->d_counters = nc;
+      ctx->counter_cap = std::max(need, ctx->counter_cap * 2);
+    }
+  }
+  // the previous epoch is freed once every stream that launched on it has passed that launch
+  ctx->retired.push_back(RetiredEpoch{std::move(old)});
+  if (old_counters) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(old_counters);
+  }
+  for (uint32_t s : ctx->released_slots)
+    if (s < ctx->counter_cap) (void)hipMemsetAsync(ctx->d_counters + kCounterWords * size_t(s), 0, kCounterBytes, us);
+  ctx->released_slots.clear();
+  return GPC_OK;
+}

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <tuple>
 
 namespace gpc {
 
@@ -611,10 +612,80 @@ Flow FeatureNP::deny_metric_flow(uint32_t id, bool ingress) const {
 }
 
 // ---------------------------------------------------------------------------- OVS stand-in
+static bool is_rule_table(uint8_t t) { return t >= TB_AP_EGRESS && t <= TB_INGRESS_DEFAULT; }
+static bool is_hard_flow(const Flow& f) { return is_rule_table(f.table) && !f.m.has_conj && !f.is_soft(); }
+
+// Which image rule a flow belongs to (image.cpp gathers exactly these kinds).
+void FeatureNP::note_flow(const Flow& f) {
+  if (is_rule_table(f.table)) {
+    if (f.m.has_conj) {
+      dirty_.conj.insert(f.m.conj_id);
+    } else if (f.is_soft()) {
+      for (auto& a : f.acts) dirty_.conj.insert(a.a);
+    } else {
+      dirty_.hard_tables |= uint8_t(1u << (f.table - 1));
+    }
+  } else if (f.table == TB_EGRESS_METRIC || f.table == TB_INGRESS_METRIC) {
+    const Match& m = f.m;
+    if (m.has_ct_label) dirty_.conj.insert(f.table == TB_INGRESS_METRIC ? uint32_t(m.label_v & 0xffffffffu) : uint32_t(m.label_v >> 32));
+    if (m.reg_present & (1u << 3)) dirty_.conj.insert(m.reg_v[3]);
+  }
+}
+
+void FeatureNP::note_change(const Flow& old, const Flow& nw) {
+  if (is_rule_table(nw.table) && old.is_soft() && nw.is_soft()) {  // context flow: actions added / removed
+    auto key = [](const Action& a) { return std::make_tuple(a.a, a.b, a.c); };
+    std::set<std::tuple<uint32_t, uint32_t, uint32_t>> o, n;
+    for (auto& a : old.acts) o.insert(key(a));
+    for (auto& a : nw.acts) n.insert(key(a));
+    for (auto& k : o)
+      if (!n.count(k)) dirty_.conj.insert(std::get<0>(k));
+    for (auto& k : n)
+      if (!o.count(k)) dirty_.conj.insert(std::get<0>(k));
+    return;
+  }
+  note_flow(old);
+  note_flow(nw);
+}
+
 void FeatureNP::apply_bundle(std::vector<const Flow*> add, std::vector<const Flow*> del) {
-  for (auto* f : del) installed_.erase(f->identity());
-  for (auto* f : add) installed_[f->identity()] = *f;
+  for (auto* f : del) {
+    auto it = installed_.find(f->identity());
+    if (it == installed_.end()) continue;
+    note_flow(it->second);
+    if (is_hard_flow(it->second)) hard_.erase(it->first);
+    installed_.erase(it);
+  }
+  for (auto* f : add) {
+    std::string id = f->identity();
+    auto it = installed_.find(id);
+    if (it != installed_.end()) {
+      note_change(it->second, *f);
+      if (is_hard_flow(it->second)) hard_.erase(id);
+      it->second = *f;
+    } else {
+      note_flow(*f);
+      it = installed_.emplace(std::move(id), *f).first;
+    }
+    if (is_hard_flow(*f)) hard_[it->first] = *f;
+  }
   generation_++;
+}
+
+int FeatureNP::load_flows(const std::vector<Flow>& flows, bool replace) {
+  std::vector<const Flow*> add, del;
+  std::vector<Flow> old;
+  if (replace) {
+    old.reserve(installed_.size());
+    for (auto& kv : installed_) old.push_back(kv.second);
+    for (auto& f : old) del.push_back(&f);
+    global_cache_.clear();
+    policy_cache_.clear();
+  }
+  for (auto& f : flows) add.push_back(&f);
+  apply_bundle(add, del);
+  foreign_ = true;
+  return GPC_OK;
 }
 
 int FeatureNP::initialize() {  // skipPolicyRuleCheckFlows (network_policy.go:2167-2211)

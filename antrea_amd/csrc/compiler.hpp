@@ -8,6 +8,7 @@
 
 #include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -120,6 +121,27 @@ class FeatureNP {
   int policy_info(uint32_t id, gpc_policy_info* out) const;
 
   const std::map<std::string, Flow>& installed() const { return installed_; }
+  // Flow-text ingest: applies parsed flows as one bundle. replace = drop the
+  // realized NP tables and the compiler's rule caches first (the context then serves the loaded
+  // flows only). Loaded flows are not known to the compiler, so commits rebuild the whole image.
+  int load_flows(const std::vector<Flow>& flows, bool replace);
+  bool foreign() const { return foreign_; }
+  // Non-conjunctive, non-conj_id flows of the rule tables (drop / skip flows): the hard
+  // pseudo-rules of the image (image.cpp); mirrored here so a delta commit can rebuild them.
+  const std::map<std::string, Flow>& hard_flows() const { return hard_; }
+
+  // Change tracking for delta commits: the rules whose realized flows changed since the last
+  // take_dirty(). A soft flow whose conjunction actions changed dirties exactly the conj ids
+  // added or removed (a shared context gaining rule B does not dirty rule A).
+  struct Dirty {
+    std::set<uint32_t> conj;
+    uint8_t hard_tables = 0;  // bit t-1 for rule table t
+  };
+  Dirty take_dirty() {
+    Dirty d = std::move(dirty_);
+    dirty_ = Dirty();
+    return d;
+  }
   const std::map<uint32_t, ConjPtr>& policies() const { return policy_cache_; }
   std::string dump() const;
   uint64_t generation() const { return generation_; }
@@ -152,8 +174,17 @@ class FeatureNP {
   std::map<std::string, CtxPtr> global_cache_;
   std::map<uint32_t, ConjPtr> policy_cache_;
   std::map<std::string, Flow> installed_;
+  std::map<std::string, Flow> hard_;
+  Dirty dirty_;
+  bool foreign_ = false;
   uint64_t generation_ = 0;
+  void note_flow(const Flow& f);
+  void note_change(const Flow& old, const Flow& nw);
 };
+
+// ovs-ofctl flow text -> Flow (flowtext.cpp). 1 = parsed, 0 = skipped line (blank, header, table
+// outside the NP path), -GPC_EINVAL with *err set.
+int parse_flow_text(const std::string& line, Flow* f, std::string* err);
 
 // helpers shared with tests / image builder
 std::vector<std::pair<uint16_t, uint16_t>> bitwise_match(uint16_t start, uint16_t end);  // port_range.go:45

@@ -121,6 +121,18 @@ struct Pkt {
   uint32_t l4m;    // filter bit of (proto class, tp_dst block) (bits 20-31)
 };
 
+// Partial decision of one image for one table, packed (it is live across the table loop):
+//   h   = best hard match: priority | verdict << 16 | found << 24 | tie << 25
+//   s   = decided soft level: priority | have << 16 | noact << 17 | tie << 18 | image << 19
+//         (noact: decided by a completion without an IPv4 conj_id flow, so the hard match wins;
+//          tie: more than one completion at the level)
+//   win = record offset of the soft winner (have && !noact)
+struct TablePart {
+  uint32_t h, s, win;
+};
+constexpr uint32_t kHFound = 1u << 24, kHTie = 1u << 25;
+constexpr uint32_t kSHave = 1u << 16, kSNoAct = 1u << 17, kSTie = 1u << 18, kSImg = 1u << 19;
+
 struct TableResult {
   uint8_t verdict;  // RVerdict
   uint8_t tie;
@@ -213,6 +225,16 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 struct Img {
   const uint32_t* blob;
   const ImageHdr* hdr;
+  const uint32_t* dead;  // tombstone bitmap over this image's rule ids (delta epochs), or null
+};
+GPC_HD bool rule_dead(const Img& im, uint32_t rid) { return im.dead && ((im.dead[rid >> 5] >> (rid & 31u)) & 1u); }
+
+// One published epoch: the base image and, after delta commits, an overlay image holding the
+// current version of every rule changed since the base was built (the base copies are
+// tombstoned). Table verdict = the OVS decision over the union of both rule sets.
+struct View {
+  Img base, ovl;
+  uint32_t n_img;  // 1 or 2
 };
 
 GPC_HD bool hash_contains(const Img& im, uint64_t key) {
@@ -339,15 +361,11 @@ constexpr int kScanUnroll = GPC_SCAN_UNROLL;  // entry loads in flight per lane 
 
 // One rule table (table = 1..6). All per-list merge state is indexed with compile-time indices
 // only (unrolled), so it stays in VGPRs.
-GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
+GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   const TableHdr& th = im.hdr->t[table - 1];
-  TableResult res;
-  res.verdict = RV_MISS;
-  res.tie = 0;
-  res.tier = 0;
-  res.counted = 0;
-  res.conj = 0;
-  res.slot = 0;
+  TablePart res;
+  res.h = res.s = res.win = 0;
+  uint32_t htie = 0, noact = 0;
   // --- hard pseudo-rules (few): best hard match H
   uint32_t rH = th.end_off;
   uint32_t hprio = 0, hverdict = RV_MISS;
@@ -358,9 +376,10 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
     const uint32_t* rec = im.blob + off;
     GPC_TOUCH(rec, 4 * kRecHdrWords);
     const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
+    if (rule_dead(im, rid)) continue;
     if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
       if ((w1 & 0xffffu) != hprio) break;
-      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, 0, p)) res.tie = 1;
+      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, 0, p)) htie = kHTie;
       continue;
     }
     if (rule_match(im, table, rec, w2, rid, 3, 0, p)) {
@@ -375,7 +394,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
 #else
   if (n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
 #endif
-    if (rH != th.end_off) res.verdict = uint8_t(hverdict);
+    if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
     return res;
   }
   // --- driver clause: the one with fewer candidate records
@@ -406,7 +425,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   const bool d1 = cnt1 < cnt0;
 #ifdef GPC_ABL_NOMERGE  // timing experiment only: stop after the bucket lookups
   if (cnt0 + cnt1 != 0xffffffffu) {
-    res.tie = uint8_t((cnt0 + cnt1) & 1u);
+    res.s = (cnt0 + cnt1) & 1u;
     return res;
   }
 #endif
@@ -434,8 +453,7 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
   int have = 0;             // result found
   uint32_t level = 0xffffffffu;
   uint32_t level_done = 0;  // completed conjunctions at the current level
-  uint32_t win = 0;         // winner record offset (soft) when have == 1 and !use_h
-  int use_h = 0;
+  uint32_t win = 0;         // winner record offset (soft) when have == 1 and !noact
   bool done = total == 0;
   while (!done) {
     uint32_t c0 = 0xffffffffu, c1 = 0xffffffffu;
@@ -491,43 +509,107 @@ GPC_HD TableResult eval_table(const Img& im, uint32_t table, const Pkt& p) {
 #ifdef GPC_ABL_NOVERIFY  // timing experiment only: read the record header, skip the clauses
       if (w2 != 0xffffffffu) continue;
 #endif
-      if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, (rec[5] >> (3 * d)) & 7u, p)) {
+      const uint32_t rid = rec[4] >> 8;
+      if (rule_dead(im, rid) || !rule_match(im, table, rec, w2, rid, d, (rec[5] >> (3 * d)) & 7u, p)) {
         GPC_STAT(5, 1);
         continue;
       }
       level_done++;
       if (have) {  // a second completion at the winning level
-        res.tie = 1;
         done = true;
         break;
       }
       if (rec_has_act(w2)) {
         have = 1;
-        use_h = (rH != th.end_off && hprio > (w1 >> 16)) ? 1 : 0;
         win = off;
       } else if (rH != th.end_off) {
         have = 1;
-        use_h = 1;
+        noact = kSNoAct;
       }
     }
     if (!more) done = true;
   }
-  if (have && !use_h) {
-    const uint32_t* rec = im.blob + win;
-    const uint32_t w2 = rec[2];
-    res.verdict = uint8_t(rec_verdict(w2));
-    res.conj = rec[0];
-    res.tier = uint8_t(rec[4] & 0xffu);
-    res.counted = uint8_t(rec_counted(w2));
-    res.slot = rec[3];
-    if (level_done > 1) res.tie = 1;
-    return res;
-  }
-  if (rH != th.end_off) {
-    res.verdict = uint8_t(hverdict);
-    if (have && level_done > 1) res.tie = 1;
+  if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
+  if (have) {
+    res.s = level | kSHave | noact | (level_done > 1 ? kSTie : 0u);
+    res.win = win;
   }
   return res;
+}
+
+// Union of two images' rule sets for one table (base with tombstones + overlay). The best hard
+// match is the higher one (equal priorities: lower verdict, tie if they differ); a soft decision
+// survives only above the combined hard priority; equal levels tie and the lower conj id wins.
+GPC_HD TablePart combine_parts(const View& v, const TablePart& a, TablePart b) {
+  b.s |= b.s & kSHave ? kSImg : 0u;  // b is the overlay's part
+  TablePart r;
+  const uint32_t ah = a.h & 0xffffu, bh = b.h & 0xffffu;
+  const bool af = (a.h & kHFound) != 0, bf = (b.h & kHFound) != 0;
+  if (bf && (!af || bh > ah)) {
+    r.h = b.h;
+  } else if (bf && af && bh == ah) {
+    const uint32_t av = (a.h >> 16) & 0xffu, bv = (b.h >> 16) & 0xffu;
+    r.h = ah | ((av < bv ? av : bv) << 16) | kHFound | ((a.h | b.h) & kHTie) | (av != bv ? kHTie : 0u);
+  } else {
+    r.h = a.h;
+  }
+  const bool hf = (r.h & kHFound) != 0;
+  const uint32_t hp = r.h & 0xffffu;
+  const uint32_t al = a.s & 0xffffu, bl = b.s & 0xffffu;
+  const bool va = (a.s & kSHave) && (!hf || al > hp);
+  const bool vb = (b.s & kSHave) && (!hf || bl > hp);
+  if (va && vb && al == bl) {  // both decided at one level: a tie; the lower conj id wins
+    const uint32_t ca = (a.s & kSNoAct) ? 0xffffffffu : v.base.blob[a.win];
+    const uint32_t cb = (b.s & kSNoAct) ? 0xffffffffu : v.ovl.blob[b.win];
+    const TablePart& w = cb < ca ? b : a;
+    r.s = w.s | kSTie;
+    r.win = w.win;
+  } else if (vb && (!va || bl > al)) {
+    r.s = b.s;
+    r.win = b.win;
+  } else if (va) {
+    r.s = a.s;
+    r.win = a.win;
+  } else {
+    r.s = 0;
+    r.win = 0;
+  }
+  return r;
+}
+
+GPC_HD TableResult finish_part(const View& v, const TablePart& q) {
+  TableResult res;
+  res.verdict = RV_MISS;
+  res.tie = (q.h & kHTie) ? 1 : 0;
+  res.tier = 0;
+  res.counted = 0;
+  res.conj = 0;
+  res.slot = 0;
+  const bool hf = (q.h & kHFound) != 0, have = (q.s & kSHave) != 0;
+  if (have && !(q.s & kSNoAct)) {
+    const uint32_t* rec = ((q.s & kSImg) ? v.ovl.blob : v.base.blob) + q.win;
+    const uint32_t w2 = rec[2];
+    if (!(hf && (q.h & 0xffffu) > (rec[1] >> 16))) {  // the soft winner's action flow beats the hard match
+      res.verdict = uint8_t(rec_verdict(w2));
+      res.conj = rec[0];
+      res.tier = uint8_t(rec[4] & 0xffu);
+      res.counted = uint8_t(rec_counted(w2));
+      res.slot = rec[3];
+      if (q.s & kSTie) res.tie = 1;
+      return res;
+    }
+  }
+  if (hf) {
+    res.verdict = uint8_t((q.h >> 16) & 0xffu);
+    if (have && (q.s & kSTie)) res.tie = 1;
+  }
+  return res;
+}
+
+GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
+  TablePart acc = eval_part(v.base, table, p);
+  for (uint32_t s = 1; s < v.n_img; s++) acc = combine_parts(v, acc, eval_part(v.ovl, table, p));
+  return finish_part(v, acc);
 }
 
 // Verdict word layout (gpc_verdict): conj_id | action | table | tier | flags.
@@ -550,7 +632,7 @@ struct PacketOut {
   int ecounted, gcounted;
 };
 
-GPC_HD PacketOut classify_packet(const Img& im, const Pkt& p, uint32_t dest) {
+GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
   PacketOut o;
   o.e.conj = o.g.conj = 0;
   o.e.packed = o.g.packed = 0;

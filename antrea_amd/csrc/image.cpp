@@ -10,10 +10,12 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <set>
 
 namespace gpc {
 
@@ -557,89 +559,189 @@ bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vect
 
 }  // namespace
 
-int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
-  *out = HostImage();
-  // ---- 1. gather rules per table
+namespace {
+
+// GPC_IMAGE_TIMING=1: per-phase build times on stderr (rank/span, records, indexes, hash).
+struct PhaseTimer {
+  bool on = std::getenv("GPC_IMAGE_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  double acc[4] = {0, 0, 0, 0};
+  void lap(int i) {
+    if (!on) return;
+    auto n = std::chrono::steady_clock::now();
+    acc[i] += std::chrono::duration<double, std::milli>(n - t).count();
+    t = n;
+  }
+  void report(const char* what) {
+    if (on) std::fprintf(stderr, "%s ms: rank %.3f records %.3f index %.3f hash %.3f\n", what, acc[0], acc[1], acc[2], acc[3]);
+  }
+};
+
+// Flow -> rule gathering (step 1 of an image build).
+struct Gather {
   std::map<uint32_t, RuleB> soft[7];
   std::map<std::pair<int, int>, RuleB> hard[7];  // key (-priority, verdict)
   std::set<uint32_t> counted_allow, counted_deny;
-  for (auto& kv : np.installed()) {
-    const Flow& f = kv.second;
-    out->n_flows++;
-    if (f.table == TB_EGRESS_METRIC || f.table == TB_INGRESS_METRIC) {
-      const Match& m = f.m;
-      if (m.has_ct_label && m.has_ct_state && (m.ct_mask & 1) && (m.ct_data & 1) && (!m.has_dl || m.dl_type == kEthIP)) {
-        uint32_t id = f.table == TB_INGRESS_METRIC ? uint32_t(m.label_v & 0xffffffffu) : uint32_t(m.label_v >> 32);
-        counted_allow.insert(id);
-      } else if ((m.reg_present & (1u << 3)) && (m.reg_present & 1) && (m.reg_v[0] & 0x400)) {
-        counted_deny.insert(m.reg_v[3]);
-      }
-      continue;
-    }
-    if (f.table < TB_AP_EGRESS || f.table > TB_INGRESS_DEFAULT) continue;
-    if (f.m.has_conj) {  // conj action flow
-      Match rest = f.m;
-      rest.has_conj = false;
-      bool fam_ok = !rest.has_dl || rest.dl_type == kEthIP;
-      rest.has_dl = false;
-      if (rest.str(0) != "priority=0") {
-        out->error = "unsupported conj_id flow: " + f.str();
-        return -GPC_EINVAL;
-      }
-      bool ok;
-      uint8_t v = action_verdict(f, &ok);
-      if (!ok) {
-        out->error = "unsupported conj_id flow actions: " + f.str();
-        return -GPC_EINVAL;
-      }
-      RuleB& r = soft[f.table][f.m.conj_id];
-      r.conj_id = f.m.conj_id;
-      r.verdict = v;
-      if (fam_ok) {
-        if (!r.has_act || f.priority > r.act_prio) r.act_prio = f.priority;
-        r.has_act = true;
-      }
-      continue;
-    }
+  uint32_t n_flows = 0;
+  std::string error;
+  // only_conj != 0: take only that conjunction's actions of a soft flow (delta builds gather per rule).
+  int add(const Flow& f, uint32_t only_conj = 0);
+  // One conjunction(id, k/n) action of soft flow f (delta builds: the action comes from the
+  // context's action map, not from a scan of the flow's possibly long action list).
+  int add_soft(const Flow& f, uint32_t id, uint32_t k, uint32_t n) {
+    n_flows++;
     Atom a;
     int ar = atom_of(f.m, &a);
     if (ar < 0) {
-      out->error = "unsupported match: " + f.str();
+      error = "unsupported match: " + f.str();
       return -GPC_EINVAL;
     }
-    if (f.is_soft()) {
-      for (auto& act : f.acts) {
-        RuleB& r = soft[f.table][act.a];
-        r.conj_id = act.a;
-        if (act.c < 2 || act.c > kMaxClauses || act.b < 1 || act.b > act.c) {
-          out->error = "unsupported conjunction shape: " + f.str();
-          return -GPC_EINVAL;
-        }
-        if ((r.prio_set && r.prio != f.priority) || (r.n && r.n != act.c)) {
-          out->error = "conjunction clauses at different priorities / clause counts: " + f.str();
-          return -GPC_EINVAL;
-        }
-        r.prio_set = true;
-        r.prio = f.priority;
-        r.n = uint8_t(act.c);
-        if (ar == 0) r.clause[act.b - 1].push_back(a);
-      }
-    } else {
-      bool ok;
-      uint8_t v = action_verdict(f, &ok);
-      if (!ok) {
-        out->error = "unsupported flow actions: " + f.str();
-        return -GPC_EINVAL;
-      }
-      RuleB& r = hard[f.table][{-int(f.priority), int(v)}];
-      r.hard = true;
-      r.prio_set = true;
-      r.prio = f.priority;
-      r.n = 1;
-      r.verdict = v;
-      if (ar == 0) r.clause[0].push_back(a);
+    return add_clause_atom(f, ar == 0 ? &a : nullptr, id, k, n);
+  }
+  int add_clause_atom(const Flow& f, const Atom* a, uint32_t id, uint32_t k, uint32_t n) {
+    RuleB& r = soft[f.table][id];
+    r.conj_id = id;
+    if (n < 2 || n > uint32_t(kMaxClauses) || k < 1 || k > n) {
+      error = "unsupported conjunction shape: " + f.str();
+      return -GPC_EINVAL;
+    }
+    if ((r.prio_set && r.prio != f.priority) || (r.n && r.n != n)) {
+      error = "conjunction clauses at different priorities / clause counts: " + f.str();
+      return -GPC_EINVAL;
+    }
+    r.prio_set = true;
+    r.prio = f.priority;
+    r.n = uint8_t(n);
+    if (a) r.clause[k - 1].push_back(*a);
+    return GPC_OK;
+  }
+};
+
+int Gather::add(const Flow& f, uint32_t only_conj) {
+  n_flows++;
+  if (f.table == TB_EGRESS_METRIC || f.table == TB_INGRESS_METRIC) {
+    const Match& m = f.m;
+    if (m.has_ct_label && m.has_ct_state && (m.ct_mask & 1) && (m.ct_data & 1) && (!m.has_dl || m.dl_type == kEthIP)) {
+      uint32_t id = f.table == TB_INGRESS_METRIC ? uint32_t(m.label_v & 0xffffffffu) : uint32_t(m.label_v >> 32);
+      counted_allow.insert(id);
+    } else if ((m.reg_present & (1u << 3)) && (m.reg_present & 1) && (m.reg_v[0] & 0x400)) {
+      counted_deny.insert(m.reg_v[3]);
+    }
+    return GPC_OK;
+  }
+  if (f.table < TB_AP_EGRESS || f.table > TB_INGRESS_DEFAULT) return GPC_OK;
+  if (f.m.has_conj) {  // conj action flow
+    Match rest = f.m;
+    rest.has_conj = false;
+    bool fam_ok = !rest.has_dl || rest.dl_type == kEthIP;
+    rest.has_dl = false;
+    if (rest.str(0) != "priority=0") {
+      error = "unsupported conj_id flow: " + f.str();
+      return -GPC_EINVAL;
+    }
+    bool ok;
+    uint8_t v = action_verdict(f, &ok);
+    if (!ok) {
+      error = "unsupported conj_id flow actions: " + f.str();
+      return -GPC_EINVAL;
+    }
+    RuleB& r = soft[f.table][f.m.conj_id];
+    r.conj_id = f.m.conj_id;
+    r.verdict = v;
+    if (fam_ok) {
+      if (!r.has_act || f.priority > r.act_prio) r.act_prio = f.priority;
+      r.has_act = true;
+    }
+    return GPC_OK;
+  }
+  Atom a;
+  int ar = atom_of(f.m, &a);
+  if (ar < 0) {
+    error = "unsupported match: " + f.str();
+    return -GPC_EINVAL;
+  }
+  if (f.is_soft()) {
+    for (auto& act : f.acts) {
+      if (only_conj && act.a != only_conj) continue;
+      int rc = add_clause_atom(f, ar == 0 ? &a : nullptr, act.a, act.b, act.c);
+      if (rc) return rc;
+    }
+  } else {
+    bool ok;
+    uint8_t v = action_verdict(f, &ok);
+    if (!ok) {
+      error = "unsupported flow actions: " + f.str();
+      return -GPC_EINVAL;
+    }
+    RuleB& r = hard[f.table][{-int(f.priority), int(v)}];
+    r.hard = true;
+    r.prio_set = true;
+    r.prio = f.priority;
+    r.n = 1;
+    r.verdict = v;
+    if (ar == 0) r.clause[0].push_back(a);
+  }
+  return GPC_OK;
+}
+
+int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out);
+
+}  // namespace
+
+int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
+  *out = HostImage();
+  Gather G;
+  for (auto& kv : np.installed()) {
+    int rc = G.add(kv.second);
+    if (rc) {
+      out->error = G.error;
+      return rc;
     }
   }
+  return emit(G, np, slots, out);
+}
+
+int build_overlay(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, HostImage* out) {
+  PhaseTimer T_;
+  *out = HostImage();
+  Gather G;
+  int rc = GPC_OK;
+  for (uint32_t c : conj) {
+    auto it = np.policies().find(c);
+    if (it == np.policies().end()) continue;  // uninstalled: tombstone only
+    const Conjunction& cj = *it->second;
+    for (Clause* cl : cj.clauses())
+      for (auto& kv : cl->matches)
+        if (kv.second->flow && !rc) {
+          auto act = kv.second->actions.find(c);
+          if (act != kv.second->actions.end())
+            rc = G.add_soft(*kv.second->flow, c, act->second.clause_id, act->second.n_clause);
+        }
+    for (auto& f : cj.action_flows)
+      if (!rc) rc = G.add(f);
+    for (auto& f : cj.metric_flows)
+      if (!rc) rc = G.add(f);
+  }
+  for (auto& kv : np.hard_flows())
+    if (!rc && ((hard_tables >> (kv.second.table - 1)) & 1u)) rc = G.add(kv.second);
+  if (rc) {
+    out->error = G.error;
+    return rc;
+  }
+  T_.lap(0);
+  T_.report("overlay gather");  // (lap 0 = the whole gather)
+  return emit(G, np, slots, out);
+}
+
+namespace {
+
+int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
+  PhaseTimer T_;
+  auto& soft = G.soft;
+  auto& hard = G.hard;
+  auto& counted_allow = G.counted_allow;
+  auto& counted_deny = G.counted_deny;
+  out->n_flows = G.n_flows;
   // ---- 2. per table: rank, emit records, driver indexes
   Blob B;
   B.w.reserve(1 << 20);
@@ -686,6 +788,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       for (int a = 0; a < AX_N; a++) span[a] = mx[a] >= mn[a] ? uint64_t(mx[a]) - mn[a] + 1 : 0;
     }
 
+    T_.lap(0);
     // records (rank order), then this table's external data
     std::vector<uint32_t> rec_off(rs.size());
     const uint32_t tbl_start = uint32_t(B.w.size());
@@ -740,7 +843,13 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       }
       rec_off[rank] = base;
       B.w.insert(B.w.end(), rec.begin(), rec.end());
-      if (r.hard) hard_offs.push_back(base);
+      if (r.hard) {
+        hard_offs.push_back(base);
+        out->hard_rids[t - 1].push_back(rid);
+      } else {
+        out->conj_rid[r.conj_id] = rid;
+        if (!r.has_act) out->any_noact = true;
+      }
     }
     B.align(16);
     th.end_off = uint32_t(B.w.size()) + 1;
@@ -751,6 +860,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
     th.n_hard = uint32_t(hard_offs.size());
     th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
+    T_.lap(1);
     // driver indexes for clauses 0 and 1 of the soft rules; entries carry the non-driver filter
     for (int k = 0; k < 2; k++) {
       std::vector<std::array<uint32_t, 4>> always;
@@ -826,6 +936,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     out->n_rules[t - 1] = th.n_rules;
     out->n_hard[t - 1] = th.n_hard;
   }
+  T_.lap(2);
   // ---- 3. point hash
   std::sort(hash_keys.begin(), hash_keys.end());
   hash_keys.erase(std::unique(hash_keys.begin(), hash_keys.end()), hash_keys.end());
@@ -839,9 +950,14 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
   out->hdr.hash_off = B.put(tab.data(), tab.size(), 16);
   out->bytes_hash = 8ull * tab.size();
   out->hdr.n_slots = slots.size();
+  out->n_rids = next_rid;
+  T_.lap(3);
+  T_.report("emit");
   B.align(16);
   out->blob = std::move(B.w);
   return GPC_OK;
 }
+
+}  // namespace
 
 }  // namespace gpc

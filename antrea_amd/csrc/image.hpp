@@ -2,6 +2,8 @@
 #pragma once
 
 #include <map>
+#include <set>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -17,6 +19,11 @@ struct HostImage {
   uint32_t n_flows = 0;
   uint64_t bytes_records = 0, bytes_ext = 0, bytes_bucket_offsets = 0, bytes_entries = 0, bytes_hash = 0;
   std::string error;                 // non-empty: unsupported flow shape
+  // rule ids (record word 4 >> 8) for tombstoning this image's rules from a later delta epoch
+  uint32_t n_rids = 0;
+  std::unordered_map<uint32_t, uint32_t> conj_rid;  // soft rules
+  std::vector<uint32_t> hard_rids[6];                // hard pseudo-rules per table
+  bool any_noact = false;  // a soft rule without an IPv4 conj_id flow (delta combine needs none)
 };
 
 // Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
@@ -35,5 +42,8 @@ class SlotMap {
 };
 
 int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out);
+// Delta image of a subset: the rules of `conj` as currently installed (uninstalled ones are
+// skipped) plus every hard pseudo-rule of the tables in `hard_tables` (bit t-1 = table t).
+int build_overlay(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, HostImage* out);
 
 }  // namespace gpc

@@ -7,6 +7,14 @@
 #include "gpc.h"
 
 namespace gpc {
-int launch_classify(const ImageHdr* d_hdr, const uint32_t* d_blob, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
+// Device pointers of one published epoch (core.hpp View): base image + tombstones, optional overlay.
+struct EpochArgs {
+  const ImageHdr* hdr;
+  const uint32_t* blob;
+  const uint32_t* dead;   // null: no tombstones
+  const ImageHdr* ohdr;   // null: no overlay
+  const uint32_t* oblob;
+};
+int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
                     unsigned long long* counters, int count, hipStream_t stream);
 }

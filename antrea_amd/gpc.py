@@ -81,13 +81,15 @@ class gpc_image_stats(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("device_bytes", C.c_uint64), ("n_rules", C.c_uint32 * 6),
                 ("n_hard", C.c_uint32 * 6), ("n_flows", C.c_uint32), ("n_counter_slots", C.c_uint32),
                 ("bytes_records", C.c_uint64), ("bytes_ext", C.c_uint64), ("bytes_bucket_offsets", C.c_uint64),
-                ("bytes_entries", C.c_uint64), ("bytes_hash", C.c_uint64)]
+                ("bytes_entries", C.c_uint64), ("bytes_hash", C.c_uint64), ("overlay_bytes", C.c_uint64),
+                ("n_overlay_rules", C.c_uint32), ("n_tombstones", C.c_uint32), ("n_full_builds", C.c_uint64),
+                ("n_delta_builds", C.c_uint64)]
 
 
 EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "gpc_batch_install",
            "gpc_uninstall_rule", "gpc_add_rule_addrs", "gpc_del_rule_addrs", "gpc_reassign_priorities",
-           "gpc_get_policy_info", "gpc_metrics", "gpc_commit", "gpc_classify", "gpc_classify_host", "gpc_counters",
-           "gpc_reset_counters", "gpc_dump_flows", "gpc_get_image_stats", "gpc_debug_image", "gpc_strerror",
+           "gpc_get_policy_info", "gpc_metrics", "gpc_commit", "gpc_compact", "gpc_classify", "gpc_classify_host", "gpc_counters",
+           "gpc_reset_counters", "gpc_dump_flows", "gpc_get_image_stats", "gpc_debug_image", "gpc_debug_epoch", "gpc_load_flows", "gpc_strerror",
            "gpc_abi_version"]
 
 _lib = None
@@ -114,6 +116,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_get_policy_info.argtypes = [vp, C.c_uint32, C.POINTER(gpc_policy_info)]
     lib.gpc_metrics.argtypes = [vp, C.POINTER(gpc_rule_metric), sz, C.POINTER(sz)]
     lib.gpc_commit.argtypes = [vp]
+    lib.gpc_compact.argtypes = [vp]
     lib.gpc_classify.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32, vp]
     lib.gpc_classify_host.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32]
     lib.gpc_counters.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
@@ -121,6 +124,9 @@ def load(path: str = LIB_PATH):
     lib.gpc_dump_flows.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]
     lib.gpc_get_image_stats.argtypes = [vp, C.POINTER(gpc_image_stats)]
     lib.gpc_debug_image.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp), C.POINTER(sz)]
+    lib.gpc_debug_epoch.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp),
+                                    C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
+    lib.gpc_load_flows.argtypes = [vp, C.c_char_p, sz, i32, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -335,9 +341,24 @@ class Classifier:
         _check(self.lib.gpc_metrics(self.h, arr, n.value, C.byref(n)), "NetworkPolicyMetrics")
         return {arr[i].conj_id: (arr[i].packets, arr[i].bytes, arr[i].sessions) for i in range(n.value)}
 
+    def load_flows(self, lines, replace=True):
+        """Flow-text ingest (ovs-ofctl text, one flow per line). Returns (loaded, skipped)."""
+        text = ("\n".join(lines) if not isinstance(lines, (str, bytes)) else lines)
+        data = text.encode() if isinstance(text, str) else text
+        nl, ns, el = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        rc = self.lib.gpc_load_flows(self.h, data, len(data), int(replace), C.byref(nl), C.byref(ns), C.byref(el))
+        if rc:
+            raise GpcError(rc, "gpc_load_flows (line %d)" % el.value)
+        return nl.value, ns.value
+
     # --- data path
     def commit(self):
+        """Publish pending changes (a delta epoch when few rules changed, else a full rebuild)."""
         _check(self.lib.gpc_commit(self.h), "gpc_commit")
+
+    def compact(self):
+        """Publish with a full image rebuild (empties the overlay)."""
+        _check(self.lib.gpc_compact(self.h), "gpc_compact")
 
     def classify_host(self, cols: Dict[str, np.ndarray], count=False) -> np.ndarray:
         soa, keep, n = pkt_soa_host(cols)
@@ -376,10 +397,25 @@ class Classifier:
         _check(self.lib.gpc_debug_image(self.h, C.byref(b), C.byref(n), C.byref(h), C.byref(hb)), "gpc_debug_image")
         return C.cast(b, C.c_void_p).value, n.value, h.value, hb.value
 
+    def debug_epoch(self):
+        """(overlay blob pointer or None, overlay hdr pointer or None, dead bitmap pointer or None,
+        dead words) of the current epoch's host shadow."""
+        ob = C.POINTER(C.c_uint32)()
+        on = C.c_size_t()
+        oh = C.c_void_p()
+        d = C.POINTER(C.c_uint32)()
+        dn = C.c_size_t()
+        _check(self.lib.gpc_debug_epoch(self.h, C.byref(ob), C.byref(on), C.byref(oh), C.byref(d), C.byref(dn)),
+               "gpc_debug_epoch")
+        return C.cast(ob, C.c_void_p).value, oh.value, C.cast(d, C.c_void_p).value, dn.value
+
     def image_stats(self) -> dict:
         st = gpc_image_stats()
         _check(self.lib.gpc_get_image_stats(self.h, C.byref(st)), "gpc_get_image_stats")
         return {"epoch": st.epoch, "device_bytes": st.device_bytes, "n_rules": list(st.n_rules),
                 "n_hard": list(st.n_hard), "n_flows": st.n_flows, "n_counter_slots": st.n_counter_slots,
                 "bytes": {"records": st.bytes_records, "ext": st.bytes_ext, "bucket_offsets": st.bytes_bucket_offsets,
-                          "entries": st.bytes_entries, "hash": st.bytes_hash}}
+                          "entries": st.bytes_entries, "hash": st.bytes_hash},
+                "overlay_bytes": st.overlay_bytes, "n_overlay_rules": st.n_overlay_rules,
+                "n_tombstones": st.n_tombstones, "n_full_builds": st.n_full_builds,
+                "n_delta_builds": st.n_delta_builds}

@@ -1,6 +1,13 @@
 """Headline benchmark: Mpps classified (5-tuple -> rule verdict, both policy stages) @100k rules.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--packets 67108864]
+    python bench.py --config C5   # C3 + AddPolicyRuleAddress/DeletePolicyRuleAddress churn
+
+C5 (BASELINE config 5): the C3 rule set with address updates interleaved with
+classification. A control thread applies `--churn-rate` ops/s (alternating add / delete of /32
+peers on random rules, `--ops-per-commit` per gpc_commit, i.e. one delta epoch each) while the
+timed classification loop runs on its own stream; the line adds the update latency (ops + commit
+until the new epoch is published) percentiles next to the Mpps measured under churn.
 
 One process per GPU (torchrun for N > 1). Each rank builds the same rule set (C3 = 100k rules),
 classifies its own packet shard (weak scaling: `--packets` per GPU, inputs resident in HBM before
@@ -48,6 +55,36 @@ def _cpu_baseline(wl, seconds):
         return None
 
 
+def _churn_loop(clf, wl, rate, per_commit, stop, lat, seed):
+    """Control-plane thread of C5: address add/delete ops on random rules, one commit per batch."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    rules = [r for r in wl.rules if r.get("from")]
+    added = []
+    period = per_commit / float(rate)
+    nxt = time.perf_counter()
+    while not stop.is_set():
+        t0 = time.perf_counter()
+        for _ in range(per_commit):
+            if added and rng.random() < 0.5:
+                rid, a, prio = added.pop(int(rng.integers(len(added))))
+                clf.delete_policy_rule_address(rid, "src", [a], prio)
+            else:
+                r = rules[int(rng.integers(len(rules)))]
+                v = int(rng.integers(0, 1 << 32))
+                a = "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+                clf.add_policy_rule_address(r["flow_id"], "src", [a], r.get("priority"))
+                added.append((r["flow_id"], a, r.get("priority")))
+        clf.commit()
+        lat.append(time.perf_counter() - t0)
+        nxt += period
+        d = nxt - time.perf_counter()
+        if d > 0:
+            time.sleep(d)
+        else:
+            nxt = time.perf_counter()
+
+
 def _pmc_pass(counter, args):
     """One rocprofv3 PMC pass over a short child run of this bench (same workload and packet
     count, counters as configured); returns the mean per-launch counter value of classify_kernel.
@@ -92,7 +129,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
+    ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
+    ap.add_argument("--ops-per-commit", type=int, default=10, help="C5: address ops per gpc_commit")
     args = ap.parse_args()
+    churn = args.config == "C5"
+    if churn:
+        args.no_traffic = True
+        args.no_cpu_baseline = True
 
     import torch
     import torch.distributed as dist
@@ -122,7 +165,7 @@ def main():
         dist.barrier()
 
     t0 = time.time()
-    wl = workload.CONFIGS[args.config]()
+    wl = workload.CONFIGS["C3" if churn else args.config]()
     clf = gpc.Classifier(device=local)
     clf.initialize()
     clf.batch_install_policy_rule_flows(wl.rules)
@@ -134,7 +177,7 @@ def main():
     out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
     soa = gpc.pkt_soa_device(cols)
     count = not args.no_count
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev) if churn else torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     for _ in range(args.warmup):
         clf.classify_device(soa, n, out.data_ptr(), count=count, stream=sptr)
@@ -145,6 +188,16 @@ def main():
     torch.cuda.synchronize(dev)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    lat, th = [], None
+    if churn:
+        import threading
+        stop = threading.Event()
+        th = threading.Thread(target=_churn_loop, args=(clf, wl, args.churn_rate, args.ops_per_commit, stop, lat,
+                                                        1234 + rank), daemon=True)
+        th.start()
+        while len(lat) < 5:  # control loop running before the timed region
+            time.sleep(0.01)
+        lat.clear()
     t_start = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
@@ -155,6 +208,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    update = None
+    if churn:
+        stop.set()
+        th.join()
+        import numpy as np
+        ms = np.array(lat[:]) * 1e3
+        st = clf.image_stats()
+        update = {"ops": len(ms) * args.ops_per_commit, "commits": len(ms),
+                  "ops_per_s": round(len(ms) * args.ops_per_commit / elapsed, 1),
+                  "target_ops_per_s": args.churn_rate, "ops_per_commit": args.ops_per_commit,
+                  "commit_latency_ms": {"p50": round(float(np.percentile(ms, 50)), 3),
+                                        "p99": round(float(np.percentile(ms, 99)), 3),
+                                        "max": round(float(ms.max()), 3)} if len(ms) else None,
+                  "overlay_rules_end": st["n_overlay_rules"], "tombstones_end": st["n_tombstones"],
+                  "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"]}
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -213,6 +281,9 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if update is not None:
+        res["update"] = update
+        res["metric"] = "Mpps classified under AddPolicyRuleAddress/DeletePolicyRuleAddress churn @100k rules"
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

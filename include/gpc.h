@@ -223,6 +223,11 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint64_t bytes_bucket_offsets; /* driver-index bucket offset arrays                          */
   uint64_t bytes_entries;        /* driver-index entries (16 B each) incl. always lists        */
   uint64_t bytes_hash;           /* image-wide point hash                                      */
+  /* delta epochs (gpc_commit): rules changed since the last full build live in an overlay image */
+  uint64_t overlay_bytes;        /* device bytes of the current overlay (0: none)               */
+  uint32_t n_overlay_rules;      /* rules + hard pseudo-rules in the overlay                   */
+  uint32_t n_tombstones;         /* base rules superseded or removed                           */
+  uint64_t n_full_builds, n_delta_builds;
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */
@@ -253,9 +258,24 @@ int gpc_get_policy_info(gpc_ctx* ctx, uint32_t rule_id, gpc_policy_info* out);
  * Reads the per-rule device counters of this context. */
 int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n);
 
+/* Flow-text ingest: the realized flows as ovs-ofctl text, one flow per line -- FlowModToString
+ * (pkg/ovs/openflow/utils.go:1222-1241) or `ovs-ofctl dump-flows --names` lines -- applied as one
+ * bundle, the seam Bridge.AddFlowsInBundle (pkg/ovs/openflow/ofctrl_bridge.go:468) feeds OVS.
+ * Flows of tables outside the NetworkPolicy path are skipped. replace != 0 drops the realized NP
+ * tables and the compiler's rule caches first. On a parse error nothing is applied and *err_line
+ * (1-based) names the line. Publish with gpc_commit (always a full rebuild for loaded flows). */
+int gpc_load_flows(gpc_ctx* ctx, const char* text, size_t len, int32_t replace, size_t* n_loaded, size_t* n_skipped,
+                   size_t* err_line);
+
 /* ---------------------------------------------------------------------------- data path */
-/* Build the device image from the realized flow table and publish it atomically. */
+/* Publish the realized flow table to the device atomically (the bundle commit,
+ * ofctrl_bridge.go:468-539). Rules whose flows changed since the last full build are rebuilt
+ * into a small overlay image and their base copies tombstoned (a delta epoch: cost proportional
+ * to the changed rules); when the changed set exceeds max(2048, base rules / 32) the whole image
+ * is rebuilt. Launches already queued keep the epoch they were launched with. */
 int gpc_commit(gpc_ctx* ctx);
+/* Same, but always rebuilds the whole image (compaction: empties the overlay). */
+int gpc_compact(gpc_ctx* ctx);
 /* Classify n packets whose columns are DEVICE pointers; writes 2*n verdicts (device pointer).
  * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t. */
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
@@ -276,6 +296,9 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out);
  * device reset). Pointers stay valid until the next gpc_commit. Used by tests to verify the
  * image independently of the device. */
 int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes);
+/* The overlay image and tombstone bitmap of the current epoch (NULL / 0 when absent). */
+int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** overlay_blob, size_t* overlay_words, const void** overlay_hdr,
+                    const uint32_t** dead, size_t* dead_words);
 const char* gpc_strerror(int err);
 int gpc_abi_version(void);
 

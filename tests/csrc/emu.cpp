@@ -28,9 +28,11 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
 
 using namespace gpc;
 
-extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
+extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_t* oblob, const void* ohdr,
+                            const uint32_t* dead, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
                             unsigned long long* counters) {
-  Img im{blob, static_cast<const ImageHdr*>(hdr)};
+  View im{{blob, static_cast<const ImageHdr*>(hdr), dead}, {oblob, static_cast<const ImageHdr*>(ohdr), nullptr},
+          oblob ? 2u : 1u};
   for (size_t i = 0; i < n; i++) {
     Pkt p;
     const uint32_t src = pk->src[i], dst = pk->dst[i];

@@ -27,8 +27,8 @@ def load():
     _lib = C.CDLL(LIB)
     _lib.gpc_emu_stats_arr = (C.c_ulonglong * 8).in_dll(_lib, "gpc_emu_stats")
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
-    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p,
-                                  C.c_void_p]
+    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -37,19 +37,21 @@ def classify(clf: "gpc.Classifier", cols, counters=None):
     on a host without GPU: the host image is built before the upload). `counters`: optional
     uint64 array of n_slots x 3 {packets, bytes, sessions} accumulated like the kernel does."""
     blob, nw, hdr, _ = clf.debug_image()
+    oblob, ohdr, dead, _ = clf.debug_epoch()
     soa, keep, n = gpc.pkt_soa_host(cols)
     out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
     cptr = None
     if counters is not None:
         assert counters.dtype == np.uint64 and counters.flags.c_contiguous
         cptr = counters.ctypes.data
-    load().emu_classify(blob, hdr, C.byref(soa), n, out.ctypes.data, cptr)
+    load().emu_classify(blob, hdr, oblob, ohdr, dead, C.byref(soa), n, out.ctypes.data, cptr)
     return out.reshape(n, 2)
 
 
-def commit_host(clf: "gpc.Classifier"):
-    """gpc_commit that tolerates the missing device (image is still built)."""
-    rc = clf.lib.gpc_commit(clf.h)
+def commit_host(clf: "gpc.Classifier", full=False):
+    """gpc_commit (gpc_compact with full=True) that tolerates the missing device (the host image
+    and overlay are still built)."""
+    rc = (clf.lib.gpc_compact if full else clf.lib.gpc_commit)(clf.h)
     if rc not in (0, -gpc.GPC_EDEV):
         raise gpc.GpcError(rc, "gpc_commit")
 

@@ -1,0 +1,140 @@
+"""Delta epochs: gpc_commit rebuilds only the rules whose flows changed into an
+overlay image and tombstones their base copies. Two product classifiers run the same churn in lock
+step, one publishing delta epochs (gpc_commit) and one rebuilding the whole image every time
+(gpc_compact); the CPU emulation of the kernel body must give identical verdicts and per-rule
+counters for both after every step. The oracle side of the same churn is covered by
+test_churn.py, which also publishes through gpc_commit (delta epochs)."""
+import copy
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from tests import emu
+
+N_PKTS = 6000
+
+
+def _ip(v):
+    return "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+def _metrics(clf, counters):
+    _, slots = clf.counters()
+    out = {}
+    for s, conj in enumerate(slots):
+        if conj and s < len(counters):
+            out[conj] = tuple(int(x) for x in counters[s])
+    return out
+
+
+def _compare(a, b, cols, step):
+    emu.commit_host(a)
+    emu.commit_host(b, full=True)
+    ca = np.zeros((max(1, a.image_stats()["n_counter_slots"]), 3), np.uint64)
+    cb = np.zeros((max(1, b.image_stats()["n_counter_slots"]), 3), np.uint64)
+    va = emu.classify(a, cols, counters=ca)
+    vb = emu.classify(b, cols, counters=cb)
+    bad = np.nonzero(va != vb)[0]
+    assert len(bad) == 0, "%s: %d verdicts differ, first packet %d: delta %s full %s" % (
+        step, len(bad), bad[0], va[bad[0]], vb[bad[0]])
+    ma, mb = _metrics(a, ca), _metrics(b, cb)
+    assert {k: v for k, v in ma.items() if any(v)} == {k: v for k, v in mb.items() if any(v)}, step
+    return va
+
+
+def _churn(wl, seed, steps):
+    rng = np.random.default_rng(seed)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=seed)
+    cols["len"] = rng.integers(60, 1500, N_PKTS).astype(np.uint16)
+    a, b = gpc.Classifier(), gpc.Classifier()
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    by_id = {r["flow_id"]: r for r in rules}
+    ids = sorted(by_id)
+    kinds = []
+    for step in range(steps):
+        rid = int(rng.choice(ids))
+        r = by_id[rid]
+        prio = r.get("priority")
+        kind = ["add", "del", "add", "reinstall", "uninstall", "add"][step % 6]
+        side = "src" if r.get("from") else "dst"
+        lst = r.get("from") if side == "src" else r.get("to")
+        if kind == "add":
+            if lst is None:
+                continue
+            pick = rng.choice(N_PKTS, size=4, replace=False)
+            addrs = [_ip(int(cols[side][i])) for i in pick]
+            for c in (a, b):
+                c.add_policy_rule_address(rid, side, addrs, prio)
+            lst.extend(addrs)
+        elif kind == "del":
+            if not lst or len(lst) < 2:
+                continue
+            for c in (a, b):
+                c.delete_policy_rule_address(rid, side, [lst[0]], prio)
+            del lst[0]
+        elif kind == "uninstall":
+            for c in (a, b):
+                c.uninstall_policy_rule_flows(rid)
+            ids.remove(rid)
+        else:
+            for c in (a, b):
+                c.uninstall_policy_rule_flows(rid)
+            _compare(a, b, cols, "uninstall %d" % rid)
+            for c in (a, b):
+                c.install_policy_rule_flows(copy.deepcopy(r))
+        _compare(a, b, cols, "%s %d" % (kind, rid))
+        kinds.append(kind)
+    return a, b, cols, kinds
+
+
+@pytest.mark.parametrize("name,seed", [("C1", 21), ("C3s", 22)])
+def test_delta_epochs_equal_full_rebuild(name, seed):
+    wl = workload.config1(seed=seed) if name == "C1" else workload.config3(seed=seed, n_policies_per_dir=12,
+                                                                              rules_per_policy=25)
+    a, b, cols, kinds = _churn(wl, seed, 30)
+    assert {"add", "del", "uninstall", "reinstall"} <= set(kinds)
+    st = a.image_stats()
+    assert st["n_full_builds"] == 1 and st["n_delta_builds"] >= 30, st
+    assert st["n_tombstones"] > 0 and st["n_overlay_rules"] > 0, st
+    assert b.image_stats()["n_overlay_rules"] == 0
+    # compaction folds the overlay into a new base: same verdicts, empty overlay
+    before = emu.classify(a, cols)
+    emu.commit_host(a, full=True)
+    st = a.image_stats()
+    assert st["n_overlay_rules"] == 0 and st["n_tombstones"] == 0 and st["n_full_builds"] == 2
+    assert (emu.classify(a, cols) == before).all()
+
+
+def test_delta_reassign_priorities():
+    wl = workload.config3(seed=23, n_policies_per_dir=6, rules_per_policy=10)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=23)
+    a, b = gpc.Classifier(), gpc.Classifier()
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    for table in ("AntreaPolicyIngressRule", "AntreaPolicyEgressRule"):
+        used = sorted({r["priority"] for r in rules if r["table"] == table})
+        upd = {used[-1]: used[-2], used[-2]: used[-1], used[0]: max(used) + 7, used[3]: used[0]}
+        for c in (a, b):
+            c.reassign_flow_priorities(upd, table)
+        _compare(a, b, cols, "reassign %s" % table)
+    assert a.image_stats()["n_delta_builds"] == 2
+
+
+def test_delta_no_change_commit():
+    wl = workload.config1(seed=24)
+    a = gpc.Classifier()
+    a.initialize()
+    a.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    emu.commit_host(a)
+    emu.commit_host(a)
+    st = a.image_stats()
+    assert st["n_full_builds"] == 1 and st["n_delta_builds"] == 1
+    assert st["n_overlay_rules"] == 0 and st["n_tombstones"] == 0

@@ -82,3 +82,59 @@ def test_gpu_matches_image_emulation_large():
     got, c = _gpu(wl.rules, cols)
     want = emu.classify(c, cols)
     _cmp(got, want, cols)
+
+
+def _ip(v):
+    return "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+@pytest.mark.parametrize("name", ["C1", "C3"])
+def test_gpu_delta_epochs(name):
+    """Delta epochs on the device (overlay image + tombstones): after address churn, uninstall and
+    reinstall, each published through gpc_commit, the device verdicts and counters equal the host
+    emulation of the same epoch, and a compaction gives the same verdicts again."""
+    wl = workload.config1(seed=31) if name == "C1" else workload.config3()
+    n = 20000 if name == "C1" else 200_000
+    cols = workload.gen_packets(wl, n, seed=31)
+    rng = np.random.default_rng(31)
+    rules = copy.deepcopy(wl.rules)
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    c.commit()
+    by_id = {r["flow_id"]: r for r in rules}
+    ids = sorted(by_id)
+    for step in range(24):
+        rid = int(rng.choice(ids))
+        r = by_id[rid]
+        side = "src" if r.get("from") else "dst"
+        lst = r.get("from") if side == "src" else r.get("to")
+        if step % 8 == 7:
+            c.uninstall_policy_rule_flows(rid)
+            c.commit()
+            c.install_policy_rule_flows(copy.deepcopy(r))
+        elif step % 3 == 2 and lst and len(lst) > 1:
+            c.delete_policy_rule_address(rid, side, [lst[0]], r.get("priority"))
+            del lst[0]
+        elif lst is not None:
+            addrs = [_ip(int(cols[side][i])) for i in rng.choice(n, size=8, replace=False)]
+            c.add_policy_rule_address(rid, side, addrs, r.get("priority"))
+            lst.extend(addrs)
+        c.commit()
+    st = c.image_stats()
+    assert st["n_delta_builds"] >= 20 and st["n_overlay_rules"] > 0 and st["n_tombstones"] > 0, st
+    c.reset_counters()
+    got = c.classify_host(cols, count=True)
+    ns = st["n_counter_slots"]
+    want_cnt = np.zeros((max(1, ns), 3), np.uint64)
+    want = emu.classify(c, cols, counters=want_cnt)
+    _cmp(got, want, cols)
+    _, slots = c.counters()
+    got_m = {k: v for k, v in c.network_policy_metrics().items() if any(v)}
+    want_m = {slots[s]: (int(want_cnt[s][0]), int(want_cnt[s][1]), int(want_cnt[s][2]))
+              for s in range(ns) if slots[s] and want_cnt[s].any()}
+    assert got_m == want_m
+    c.compact()
+    assert c.image_stats()["n_overlay_rules"] == 0
+    again = c.classify_host(cols)
+    _cmp(again, want, cols)
