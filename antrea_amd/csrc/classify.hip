@@ -20,6 +20,9 @@ namespace gpc {
 #endif
 constexpr int kBlock = GPC_BLOCK;
 
+// kDelta = false: a base-only epoch (no tombstones, no overlay); the delta-epoch machinery folds
+// away at compile time so the common case pays nothing for it.
+template <bool kDelta>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out,
                                                           unsigned long long* __restrict__ counters, int count) {
   uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
@@ -30,7 +33,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
            pk.svc_group ? pk.svc_group[i] : 0u, pk.tun_id ? pk.tun_id[i] : 0u, pk.ct_src ? pk.ct_src[i] : src,
            pk.ct_dst ? pk.ct_dst[i] : dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
   const uint32_t dest = pk.dest ? pk.dest[i] : 0u;
-  View im{{ep.blob, ep.hdr, ep.dead}, {ep.oblob, ep.ohdr, nullptr}, ep.oblob ? 2u : 1u};
+  View im{{ep.blob, ep.hdr, kDelta ? ep.dead : nullptr}, {ep.oblob, ep.ohdr, nullptr}, (kDelta && ep.oblob) ? 2u : 1u};
   PacketOut o = classify_packet(im, p, dest);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
@@ -44,8 +47,12 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
                     unsigned long long* counters, int count, hipStream_t stream) {
   if (n == 0) return 0;
   uint64_t blocks = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(classify_kernel, dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), counters, count);
+  if (ep.dead || ep.oblob)
+    hipLaunchKernelGGL(classify_kernel<true>, dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                       reinterpret_cast<uint4*>(out), counters, count);
+  else
+    hipLaunchKernelGGL(classify_kernel<false>, dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                       reinterpret_cast<uint4*>(out), counters, count);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

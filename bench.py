@@ -5,9 +5,9 @@
 
 C5 (BASELINE config 5): the C3 rule set with address updates interleaved with
 classification. A control thread applies `--churn-rate` ops/s (alternating add / delete of /32
-peers on random rules, `--ops-per-commit` per gpc_commit, i.e. one delta epoch each) while the
-timed classification loop runs on its own stream; the line adds the update latency (ops + commit
-until the new epoch is published) percentiles next to the Mpps measured under churn.
+peers on random rules; every op due so far is applied and published with one gpc_commit, i.e. one
+delta epoch) while the timed classification loop runs on its own stream; the line adds the update
+latency (op due -> commit returned) percentiles next to the Mpps measured under churn.
 
 One process per GPU (torchrun for N > 1). Each rank builds the same rule set (C3 = 100k rules),
 classifies its own packet shard (weak scaling: `--packets` per GPU, inputs resident in HBM before
@@ -55,17 +55,25 @@ def _cpu_baseline(wl, seconds):
         return None
 
 
-def _churn_loop(clf, wl, rate, per_commit, stop, lat, seed):
-    """Control-plane thread of C5: address add/delete ops on random rules, one commit per batch."""
+def _churn_loop(clf, wl, rate, max_batch, stop, rec, seed):
+    """Control-plane thread of C5. Address ops (alternating add / delete of /32 peers on random
+    rules) become due at `rate` per second; each pass applies every op due so far (at most
+    `max_batch`) and publishes them with one gpc_commit. Per op, the update latency is the time
+    from the op being due to the commit that made it visible returning; rec gets
+    (ops, commit_seconds, [latencies]) per commit."""
     import numpy as np
     rng = np.random.default_rng(seed)
     rules = [r for r in wl.rules if r.get("from")]
     added = []
-    period = per_commit / float(rate)
-    nxt = time.perf_counter()
+    t0 = time.perf_counter()
+    issued = 0
     while not stop.is_set():
-        t0 = time.perf_counter()
-        for _ in range(per_commit):
+        due = int((time.perf_counter() - t0) * rate) - issued
+        if due <= 0:
+            time.sleep(0.0002)
+            continue
+        due = min(due, max_batch)
+        for _ in range(due):
             if added and rng.random() < 0.5:
                 rid, a, prio = added.pop(int(rng.integers(len(added))))
                 clf.delete_policy_rule_address(rid, "src", [a], prio)
@@ -75,14 +83,12 @@ def _churn_loop(clf, wl, rate, per_commit, stop, lat, seed):
                 a = "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
                 clf.add_policy_rule_address(r["flow_id"], "src", [a], r.get("priority"))
                 added.append((r["flow_id"], a, r.get("priority")))
+        tc = time.perf_counter()
         clf.commit()
-        lat.append(time.perf_counter() - t0)
-        nxt += period
-        d = nxt - time.perf_counter()
-        if d > 0:
-            time.sleep(d)
-        else:
-            nxt = time.perf_counter()
+        done = time.perf_counter()
+        due_t = t0 + (issued + np.arange(due)) / rate
+        rec.append((due, done - tc, done - due_t))
+        issued += due
 
 
 def _pmc_pass(counter, args):
@@ -130,7 +136,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
-    ap.add_argument("--ops-per-commit", type=int, default=10, help="C5: address ops per gpc_commit")
+    ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
     args = ap.parse_args()
     churn = args.config == "C5"
     if churn:
@@ -192,7 +198,7 @@ def main():
     if churn:
         import threading
         stop = threading.Event()
-        th = threading.Thread(target=_churn_loop, args=(clf, wl, args.churn_rate, args.ops_per_commit, stop, lat,
+        th = threading.Thread(target=_churn_loop, args=(clf, wl, args.churn_rate, args.max_batch, stop, lat,
                                                         1234 + rank), daemon=True)
         th.start()
         while len(lat) < 5:  # control loop running before the timed region
@@ -213,14 +219,17 @@ def main():
         stop.set()
         th.join()
         import numpy as np
-        ms = np.array(lat[:]) * 1e3
+        rec = lat[:]
+        ops = sum(r[0] for r in rec)
+        op_ms = np.concatenate([r[2] for r in rec]) * 1e3 if rec else np.zeros(0)
+        commit_ms = np.array([r[1] for r in rec]) * 1e3
         st = clf.image_stats()
-        update = {"ops": len(ms) * args.ops_per_commit, "commits": len(ms),
-                  "ops_per_s": round(len(ms) * args.ops_per_commit / elapsed, 1),
-                  "target_ops_per_s": args.churn_rate, "ops_per_commit": args.ops_per_commit,
-                  "commit_latency_ms": {"p50": round(float(np.percentile(ms, 50)), 3),
-                                        "p99": round(float(np.percentile(ms, 99)), 3),
-                                        "max": round(float(ms.max()), 3)} if len(ms) else None,
+        pct = lambda a, q: round(float(np.percentile(a, q)), 3) if len(a) else None
+        update = {"ops": int(ops), "commits": len(rec), "ops_per_s": round(ops / elapsed, 1),
+                  "target_ops_per_s": args.churn_rate, "ops_per_commit_mean": round(ops / max(1, len(rec)), 1),
+                  "op_latency_ms": {"p50": pct(op_ms, 50), "p99": pct(op_ms, 99),
+                                    "max": round(float(op_ms.max()), 3) if len(op_ms) else None},
+                  "commit_ms": {"p50": pct(commit_ms, 50), "p99": pct(commit_ms, 99)},
                   "overlay_rules_end": st["n_overlay_rules"], "tombstones_end": st["n_tombstones"],
                   "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"]}
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
