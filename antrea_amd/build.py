@@ -21,9 +21,9 @@ LIB = os.path.join(OUT, "libgpc.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-HOST_SRCS = ["compiler.cpp", "image.cpp", "flowtext.cpp"]
+HOST_SRCS = ["compiler.cpp", "image.cpp", "flowtext.cpp", "service.cpp"]
 HIP_SRCS = ["classify.hip", "api.cpp"]
-HEADERS = ["model.hpp", "compiler.hpp", "core.hpp", "image.hpp", "launch.hpp"]
+HEADERS = ["model.hpp", "compiler.hpp", "core.hpp", "image.hpp", "launch.hpp", "service.hpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 

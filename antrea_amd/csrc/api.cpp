@@ -16,6 +16,7 @@
 #include "gpc.h"
 #include "image.hpp"
 #include "launch.hpp"
+#include "service.hpp"
 
 using namespace gpc;
 
@@ -49,6 +50,7 @@ struct DevImage {  // one uploaded image (freed when the last epoch using it ret
 
 struct DevEpoch {
   std::shared_ptr<DevImage> base, ovl;  // base shared by the delta epochs built on it
+  std::shared_ptr<DevImage> svc;        // Service image (d_hdr unused), shared until Services change
   uint32_t* d_dead = nullptr;           // tombstones over base rule ids (delta epochs)
   uint64_t epoch = 0;
   std::map<hipStream_t, hipEvent_t> last_use;  // last launch on each stream that used this epoch
@@ -79,6 +81,9 @@ struct gpc_ctx {
   std::mutex ctl;    // control plane (conjMatchFlowLock + replayMutex role)
   std::mutex data;   // epoch pointer swap vs. kernel launch
   FeatureNP np;
+  FeatureService svc;
+  std::vector<uint32_t> svc_blob;        // host copy of the Service image (empty: no Services)
+  uint64_t svc_gen = ~0ull;              // FeatureService generation the image was built from
   SlotMap slots;
   HostImage last;    // base image of the current epoch: shadow state for re-upload + debug export
   HostImage ovl;     // overlay of the current epoch (empty blob: none)
@@ -93,7 +98,7 @@ struct gpc_ctx {
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
   uint64_t epoch = 0, n_full = 0, n_delta = 0;
-  explicit gpc_ctx(const gpc_config& c) : cfg(c), np(c) {}
+  explicit gpc_ctx(const gpc_config& c) : cfg(c), np(c), svc(c) {}
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : -GPC_EDEV; }
@@ -105,6 +110,17 @@ static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevIm
   if (hip_ok(dev_alloc((void**)&d->d_blob, d->bytes, s)) || hip_ok(dev_alloc((void**)&d->d_hdr, sizeof(ImageHdr), s)) ||
       hip_ok(hipMemcpyAsync(d->d_blob, h.blob.data(), d->bytes, hipMemcpyHostToDevice, s)) ||
       hip_ok(hipMemcpyAsync(d->d_hdr, &h.hdr, sizeof(ImageHdr), hipMemcpyHostToDevice, s)))
+    return -GPC_EDEV;
+  *out = std::move(d);
+  return GPC_OK;
+}
+
+static int upload_words(const std::vector<uint32_t>& w, hipStream_t s, std::shared_ptr<DevImage>* out) {
+  auto d = std::make_shared<DevImage>();
+  d->s = s;
+  d->bytes = w.size() * 4;
+  if (hip_ok(dev_alloc((void**)&d->d_blob, d->bytes, s)) ||
+      hip_ok(hipMemcpyAsync(d->d_blob, w.data(), d->bytes, hipMemcpyHostToDevice, s)))
     return -GPC_EDEV;
   *out = std::move(d);
   return GPC_OK;
@@ -269,6 +285,60 @@ int gpc_load_flows(gpc_ctx* ctx, const char* text, size_t len, int32_t replace, 
   return GPC_OK;
 }
 
+#define GPC_SVC_CALL(expr)                       \
+  do {                                           \
+    if (!ctx) return -GPC_EINVAL;                \
+    std::lock_guard<std::mutex> g(ctx->ctl);     \
+    try {                                        \
+      return (expr);                             \
+    } catch (...) {                              \
+      return -GPC_ENOMEM;                        \
+    }                                            \
+  } while (0)
+
+int gpc_install_service_group(gpc_ctx* ctx, uint32_t group_id, int32_t aff, const gpc_endpoint* eps, size_t n) {
+  if (!eps && n) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.install_service_group(group_id, aff != 0, eps, n));
+}
+int gpc_uninstall_service_group(gpc_ctx* ctx, uint32_t group_id) { GPC_SVC_CALL(ctx->svc.uninstall_service_group(group_id)); }
+int gpc_install_endpoint_flows(gpc_ctx* ctx, uint8_t protocol, uint8_t family, const gpc_endpoint* eps, size_t n) {
+  if (!eps && n) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.install_endpoint_flows(protocol, family, eps, n));
+}
+int gpc_uninstall_endpoint_flows(gpc_ctx* ctx, uint8_t protocol, uint8_t family, const gpc_endpoint* eps, size_t n) {
+  if (!eps && n) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.uninstall_endpoint_flows(protocol, family, eps, n));
+}
+int gpc_install_service_flows(gpc_ctx* ctx, const gpc_service_config* cfg) {
+  if (!cfg) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.install_service_flows(*cfg));
+}
+int gpc_uninstall_service_flows(gpc_ctx* ctx, const uint8_t* ip, uint8_t family, uint16_t port, uint8_t protocol) {
+  if (!ip) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.uninstall_service_flows(ip, family, port, protocol));
+}
+int gpc_install_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family, uint32_t ofport) {
+  if (!ip) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.install_pod(ip, family, ofport));
+}
+int gpc_uninstall_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family) {
+  if (!ip) return -GPC_EINVAL;
+  GPC_SVC_CALL(ctx->svc.uninstall_pod(ip, family));
+}
+
+int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed) {
+  if (!ctx) return -GPC_EINVAL;
+  std::string s;
+  {
+    std::lock_guard<std::mutex> g(ctx->ctl);
+    s = ctx->svc.dump_groups();
+  }
+  if (needed) *needed = s.size() + 1;
+  if (!buf || cap < s.size() + 1) return -GPC_ERANGE;
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return GPC_OK;
+}
+
 int gpc_get_policy_info(gpc_ctx* ctx, uint32_t rule_id, gpc_policy_info* out) {
   if (!ctx || !out) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
@@ -281,6 +351,12 @@ int gpc_dump_flows(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   {
     std::lock_guard<std::mutex> g(ctx->ctl);
     s = ctx->np.dump();
+    std::string sv = ctx->svc.dump_flows();
+    if (!sv.empty()) {
+      if (!s.empty() && s.back() != '\n') s += "\n";
+      s += sv;
+      if (!s.empty() && s.back() == '\n') s.pop_back();
+    }
   }
   if (needed) *needed = s.size() + 1;
   if (!buf || cap < s.size() + 1) return -GPC_ERANGE;
@@ -292,15 +368,20 @@ int gpc_commit(gpc_ctx* ctx) { return commit_impl(ctx, false); }
 int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
 
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
+  return gpc_classify_lb(ctx, pk, n, out, nullptr, count, stream);
+}
+
+int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, gpc_lb_result* lb_out, int32_t count,
+                    void* stream) {
   if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
   if (n && (!pk->src || !pk->dst || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
   if (!ctx->cur.base) return -GPC_EINVAL;  // nothing committed yet
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
   EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.d_dead, ctx->cur.ovl ? ctx->cur.ovl->d_hdr : nullptr,
-               ctx->cur.ovl ? ctx->cur.ovl->d_blob : nullptr};
+               ctx->cur.ovl ? ctx->cur.ovl->d_blob : nullptr, ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr};
   hipStream_t st = (hipStream_t)stream;
-  int rc = launch_classify(ep, *pk, n, out, ctx->d_counters, count, st);
+  int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count, st);
   if (rc || n == 0) return rc;
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained
   if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
@@ -308,6 +389,11 @@ int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out
 }
 
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count) {
+  return gpc_classify_host_lb(ctx, pk, n, out, nullptr, count);
+}
+
+int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
+                         int32_t count) {
   if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
   if (n == 0) return GPC_OK;
@@ -340,11 +426,15 @@ int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict
   up(pk->dest, 1, (const void**)&d.dest);
   up(pk->len, 2, (const void**)&d.len);
   void* dout = nullptr;
+  void* dlb = nullptr;
   if (!rc && hip_ok(hipMalloc(&dout, n * 2 * sizeof(gpc_verdict)))) rc = -GPC_EDEV;
-  if (!rc) rc = gpc_classify(ctx, &d, n, (gpc_verdict*)dout, count, nullptr);
+  if (!rc && lb_out && hip_ok(hipMalloc(&dlb, n * sizeof(gpc_lb_result)))) rc = -GPC_EDEV;
+  if (!rc) rc = gpc_classify_lb(ctx, &d, n, (gpc_verdict*)dout, (gpc_lb_result*)dlb, count, nullptr);
   if (!rc && hip_ok(hipDeviceSynchronize())) rc = -GPC_EDEV;
   if (!rc && hip_ok(hipMemcpy(out, dout, n * 2 * sizeof(gpc_verdict), hipMemcpyDeviceToHost))) rc = -GPC_EDEV;
+  if (!rc && lb_out && hip_ok(hipMemcpy(lb_out, dlb, n * sizeof(gpc_lb_result), hipMemcpyDeviceToHost))) rc = -GPC_EDEV;
   if (dout) (void)hipFree(dout);
+  if (dlb) (void)hipFree(dlb);
   for (void* p : allocs) (void)hipFree(p);
   return rc;
 }
@@ -427,6 +517,14 @@ int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const 
   return GPC_OK;
 }
 
+int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  if (blob) *blob = ctx->svc_blob.empty() ? nullptr : ctx->svc_blob.data();
+  if (n_words) *n_words = ctx->svc_blob.size();
+  return GPC_OK;
+}
+
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** oblob, size_t* on_words, const void** ohdr, const uint32_t** dead,
                     size_t* dead_words) {
   if (!ctx) return -GPC_EINVAL;
@@ -488,6 +586,14 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   } catch (...) {
     return -GPC_ENOMEM;
   }
+  const bool svc_changed = ctx->svc.generation() != ctx->svc_gen;
+  if (svc_changed) {
+    std::string err;
+    std::vector<uint32_t> sb;
+    if (!ctx->svc.empty() && (rc = ctx->svc.build_image(&sb, &err))) return rc;
+    ctx->svc_blob = std::move(sb);
+    ctx->svc_gen = ctx->svc.generation();
+  }
   ctx->slot_conj = ctx->slots.slot_conj();
   if (full) ctx->n_full++;
   else ctx->n_delta++;
@@ -511,6 +617,8 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       }
     }
   }
+  if (!svc_changed) ne.svc = ctx->cur.svc;
+  else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, us, &ne.svc))) return rc;
   ne.epoch = ++ctx->epoch;
   // counters: grow to the slot count, zero released slots (their Metric flows were deleted)
   size_t need = ctx->slots.size() ? ctx->slots.size() : 1;

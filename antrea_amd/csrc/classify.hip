@@ -20,19 +20,36 @@ namespace gpc {
 #endif
 constexpr int kBlock = GPC_BLOCK;
 
-// kDelta = false: a base-only epoch (no tombstones, no overlay); the delta-epoch machinery folds
-// away at compile time so the common case pays nothing for it.
-template <bool kDelta>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out,
-                                                          unsigned long long* __restrict__ counters, int count) {
+// kDelta = false: a base-only epoch (no tombstones, no overlay); kSvc = false: no Services. The
+// machinery of either folds away at compile time so the common case pays nothing for it.
+template <bool kDelta, bool kSvc>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
+    EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
+    unsigned long long* __restrict__ counters, int count) {
   uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= n) return;
+  const uint32_t src = pk.src[i];
+  uint32_t dst = pk.dst[i], dport = pk.dport[i];
+  const uint32_t sport = pk.sport[i], proto = pk.proto[i];
+  uint32_t out_port = pk.out_port[i];
+  uint32_t svc_group = pk.svc_group ? pk.svc_group[i] : 0u;
+  uint32_t dest = pk.dest ? pk.dest[i] : 0u;
+  const uint32_t ct_src = pk.ct_src ? pk.ct_src[i] : src;
+  const uint32_t ct_dst = pk.ct_dst ? pk.ct_dst[i] : dst;  // pre-NAT destination
+  if (kSvc) {
+    uint32_t lb[4];
+    const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
+    if (lb_out) lb_out[i] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+    if (f & GPC_LB_NO_ENDPOINT) {  // EndpointDNAT serviceNoEndpointFlow: rejected before the policy stages
+      out[i] = make_uint4(0u, pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0), 0u, 0u);
+      return;
+    }
+  } else if (lb_out) {
+    lb_out[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   Pkt p;
-  const uint32_t src = pk.src[i], dst = pk.dst[i];
-  make_pkt(p, src, dst, pk.sport[i], pk.dport[i], pk.proto[i], pk.out_port[i], pk.in_port ? pk.in_port[i] : 0u,
-           pk.svc_group ? pk.svc_group[i] : 0u, pk.tun_id ? pk.tun_id[i] : 0u, pk.ct_src ? pk.ct_src[i] : src,
-           pk.ct_dst ? pk.ct_dst[i] : dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
-  const uint32_t dest = pk.dest ? pk.dest[i] : 0u;
+  make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
+           pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
   View im{{ep.blob, ep.hdr, kDelta ? ep.dead : nullptr}, {ep.oblob, ep.ohdr, nullptr}, (kDelta && ep.oblob) ? 2u : 1u};
   PacketOut o = classify_packet(im, p, dest);
   if (count && (o.ecounted || o.gcounted)) {
@@ -43,16 +60,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   out[i] = make_uint4(e.conj, e.packed, g.conj, g.packed);
 }
 
-int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
+template <bool kDelta, bool kSvc>
+static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
+                   unsigned long long* counters, int count, hipStream_t stream) {
+  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((classify_kernel<kDelta, kSvc>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                     reinterpret_cast<uint4*>(out), lb_out, counters, count);
+}
+
+int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, hipStream_t stream) {
   if (n == 0) return 0;
-  uint64_t blocks = (n + kBlock - 1) / kBlock;
-  if (ep.dead || ep.oblob)
-    hipLaunchKernelGGL(classify_kernel<true>, dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                       reinterpret_cast<uint4*>(out), counters, count);
-  else
-    hipLaunchKernelGGL(classify_kernel<false>, dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                       reinterpret_cast<uint4*>(out), counters, count);
+  if ((n + kBlock - 1) / kBlock > 0xffffffffull) return -GPC_EINVAL;
+  const bool delta = ep.dead || ep.oblob, svc = ep.svc != nullptr;
+  if (delta && svc) launch<true, true>(ep, pk, n, out, lb_out, counters, count, stream);
+  else if (delta) launch<true, false>(ep, pk, n, out, lb_out, counters, count, stream);
+  else if (svc) launch<false, true>(ep, pk, n, out, lb_out, counters, count, stream);
+  else launch<false, false>(ep, pk, n, out, lb_out, counters, count, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

@@ -23,7 +23,11 @@ static const char* kTableNames[TB_COUNT] = {"",
                                             "IngressMetric",
                                             "L3Forwarding",
                                             "ConntrackCommit",
-                                            "Output"};
+                                            "Output",
+                                            "ServiceLB",
+                                            "EndpointDNAT",
+                                            "SNATMark",
+                                            "SNAT"};
 
 const char* table_name(uint8_t t) { return t < TB_COUNT ? kTableNames[t] : "?"; }
 
@@ -179,8 +183,28 @@ std::string Action::str() const {  // utils.go:600-760 (the subset NP flows use)
     case ACT_GOTO: return std::string("goto_table:") + table_name(uint8_t(a));
     case ACT_GROUP: return "group:" + std::to_string(a);
     case ACT_DROP: return "drop";
+    case ACT_CT_DNAT:  // endpointDNATFlow, pipeline.go:2511-2528
+      std::snprintf(buf, sizeof buf,
+                    "ct(commit,table=%s,zone=%u,nat(dst=%u.%u.%u.%u:%u),exec(set_field:0x10/0x10->ct_mark,"
+                    "move:NXM_NX_REG0[0..3]->NXM_NX_CT_MARK[0..3]))",
+                    table_name(uint8_t(a)), b, c >> 24, (c >> 16) & 255u, (c >> 8) & 255u, c & 255u, unsigned(lv));
+      return buf;
+    case ACT_CT_HAIRPIN:  // podHairpinSNATFlow, pipeline.go:3052-3064
+      std::snprintf(buf, sizeof buf, "ct(commit,table=%s,zone=%u,exec(set_field:0x20/0x20->ct_mark,set_field:0x40/0x40->ct_mark))",
+                    table_name(uint8_t(a)), b);
+      return buf;
+    case ACT_RESUBMIT: return std::string("resubmit:") + table_name(uint8_t(a));
   }
   return "";
+}
+
+std::string Group::str() const {  // ofctrl group text as the reference tests print it (client_test.go:1024-1090)
+  std::string s = "group_id=" + std::to_string(id) + ",type=select";
+  for (auto& b : buckets) {
+    s += ",bucket=bucket_id:" + std::to_string(b.id) + ",weight:" + std::to_string(b.weight) + ",actions=";
+    for (size_t i = 0; i < b.acts.size(); i++) s += (i ? "," : "") + b.acts[i].str();
+  }
+  return s;
 }
 
 std::string Flow::str() const {  // FlowModToString, utils.go:1222-1224

@@ -612,6 +612,87 @@ GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
   return finish_part(v, acc);
 }
 
+// ------------------------------------------------------------------------------ Service image
+// AntreaProxy stage in front of the policy tables, resolved at build time from the
+// realized ServiceLB flows, select groups, EndpointDNAT flows and the Pod map (service.cpp):
+//   SvcHdr at word 0; a key -> service hash (2-choice, 8-way buckets: 16 words of uint64 keys
+//   (1 << 63 | proto << 48 | port << 32 | ip), 8 words of values = service index, 8 pad);
+//   service records {first endpoint, n_ep | slot_log2 << 24, group id, flags};
+//   endpoint records {ip, port | flags << 16, out_port (reg1), destination class}.
+struct SvcHdr {
+  uint32_t hash_off, hash_log2, svc_off, n_svc, ep_off, n_ep, reserved[2];
+};
+constexpr uint32_t kSvcBucketWords = 32;
+constexpr uint32_t kSvcLoadReg7 = 1u;  // service flag: the ServiceLB flow loads reg7 = group id
+// endpoint flags (port word >> 16): GPC_LB_DNAT / GPC_LB_REMOTE values
+GPC_HD uint64_t svc_key(uint32_t proto, uint32_t ip, uint32_t port) {
+  return (1ull << 63) | (uint64_t(proto & 0xffu) << 48) | (uint64_t(port & 0xffffu) << 32) | ip;
+}
+// Endpoint selection of the select group. OVS picks a bucket by dp_hash over a symmetric L4 hash
+// with a 64-slot table for equal weights (OVS-internal, not in the reference: parity unpinned);
+// restated: symmetric hash of (src ^ dst, sport ^ dport, proto), slot table of 2^slot_log2 >= 64
+// entries, slot s -> bucket s mod n (Antrea gives every bucket weight 100).
+GPC_HD uint32_t lb_hash(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto) {
+  return mix32((src ^ dst) ^ (mix32(((sport ^ dport) << 8) | (proto & 0xffu)) * 0x9e3779b1u));
+}
+// Index into the service records, or 0xffffffff.
+GPC_HD uint32_t svc_lookup(const uint32_t* sv, uint32_t proto, uint32_t ip, uint32_t port) {
+  const SvcHdr* h = reinterpret_cast<const SvcHdr*>(sv);
+  const uint64_t key = svc_key(proto, ip, port);
+  const uint32_t mask = (1u << h->hash_log2) - 1u;
+  const uint32_t bs[2] = {hash_b1(key, mask), hash_b2(key, mask)};
+  uint32_t r = 0xffffffffu;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint32_t* b = sv + h->hash_off + size_t(bs[c]) * kSvcBucketWords;
+    GPC_TOUCH(b, 96);
+    const uint64_t* k = reinterpret_cast<const uint64_t*>(b);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if (k[i] == key) r = b[16 + i];
+  }
+  return r;
+}
+
+// The Service stage of one packet (ServiceLB -> group bucket -> EndpointDNAT -> L3Forwarding):
+// rewrites dst / dport (DNAT), reg7, reg1 and the destination class; o[0..3] = gpc_lb_result
+// words {endpoint ip, port | flags << 16, group id, out_port}. Returns the GPC_LB_* flags (0: the
+// packet is not addressed to a Service). ct_nw_dst keeps the pre-NAT destination: the caller
+// takes it before this call.
+GPC_HD uint32_t lb_stage(const uint32_t* sv, uint32_t src, uint32_t& dst, uint32_t sport, uint32_t& dport, uint32_t proto,
+                         uint32_t& svc_group, uint32_t& out_port, uint32_t& dest, uint32_t* o) {
+  o[0] = o[1] = o[2] = o[3] = 0;
+  if (proto != 6 && proto != 17 && proto != 132) return 0;
+  const uint32_t si = svc_lookup(sv, proto, dst, dport);
+  if (si == 0xffffffffu) return 0;
+  const SvcHdr* h = reinterpret_cast<const SvcHdr*>(sv);
+  const uint32_t* s = sv + h->svc_off + 4 * si;
+  GPC_TOUCH(s, 16);
+  const uint32_t n = s[1] & 0xffffffu, lg = s[1] >> 24;
+  uint32_t flags = GPC_LB_HIT;
+  o[2] = s[2];
+  if (s[3] & kSvcLoadReg7) svc_group = s[2];
+  if (n == 0) {
+    flags |= GPC_LB_NO_ENDPOINT;
+    o[1] = flags << 16;
+    return flags;
+  }
+  const uint32_t slot = lb_hash(src, dst, sport, dport, proto) & ((1u << lg) - 1u);
+  const uint32_t* e = sv + h->ep_off + 4 * (s[0] + slot % n);
+  GPC_TOUCH(e, 16);
+  flags |= e[1] >> 16;
+  o[0] = e[0];
+  o[1] = (e[1] & 0xffffu) | (flags << 16);
+  o[3] = e[2];
+  if (flags & GPC_LB_DNAT) {
+    dst = e[0];
+    dport = e[1] & 0xffffu;
+  }
+  out_port = e[2];
+  dest = e[3];
+  return flags;
+}
+
 // Verdict word layout (gpc_verdict): conj_id | action | table | tier | flags.
 struct VerdictOut {
   uint32_t conj;

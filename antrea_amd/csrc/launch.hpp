@@ -14,7 +14,8 @@ struct EpochArgs {
   const uint32_t* dead;   // null: no tombstones
   const ImageHdr* ohdr;   // null: no overlay
   const uint32_t* oblob;
+  const uint32_t* svc;    // null: no Services (AntreaProxy stage skipped)
 };
-int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
+int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, hipStream_t stream);
 }

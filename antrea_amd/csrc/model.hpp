@@ -31,7 +31,12 @@ enum TableId : uint8_t {
   TB_L3_FORWARDING = 9,
   TB_CONNTRACK_COMMIT = 10,
   TB_OUTPUT = 11,
-  TB_COUNT = 12
+  // AntreaProxy tables (pipeline.go ServiceLB / EndpointDNAT / SNATMark)
+  TB_SERVICE_LB = 12,
+  TB_ENDPOINT_DNAT = 13,
+  TB_SNAT_MARK = 14,
+  TB_SNAT = 15,
+  TB_COUNT = 16
 };
 const char* table_name(uint8_t t);
 inline bool is_egress_table(uint8_t t) { return t == TB_AP_EGRESS || t == TB_EGRESS || t == TB_EGRESS_DEFAULT || t == TB_EGRESS_METRIC; }
@@ -93,7 +98,12 @@ struct Match {
   std::string str(uint16_t priority) const;  // "priority=...,..." (getFlowModMatch)
 };
 
-enum ActKind : uint8_t { ACT_CONJ, ACT_SET_REG, ACT_CT_COMMIT, ACT_GOTO, ACT_GROUP, ACT_DROP };
+enum ActKind : uint8_t {
+  ACT_CONJ, ACT_SET_REG, ACT_CT_COMMIT, ACT_GOTO, ACT_GROUP, ACT_DROP,
+  ACT_CT_DNAT,     // ct(commit,table=a,zone=b,nat(dst=c:lv),exec(ServiceCTMark, reg0[0..3]->ct_mark))
+  ACT_CT_HAIRPIN,  // ct(commit,table=a,zone=b,exec(ConnSNATCTMark, HairpinCTMark))
+  ACT_RESUBMIT     // resubmit:a (group buckets)
+};
 
 struct Action {
   ActKind kind;
@@ -117,6 +127,17 @@ struct Flow {
       if (a.kind != ACT_CONJ) return false;
     return true;
   }
+};
+
+// OpenFlow group (select type): what serviceEndpointGroup builds (pipeline.go:2553-2592).
+struct Bucket {
+  uint32_t id = 0, weight = 100;
+  std::vector<Action> acts;
+};
+struct Group {
+  uint32_t id = 0;
+  std::vector<Bucket> buckets;
+  std::string str() const;  // "group_id=100,type=select,bucket=bucket_id:0,weight:100,actions=..."
 };
 
 }  // namespace gpc

@@ -30,6 +30,10 @@ ACT_NAMES = ["NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "B
 
 # verdict dtype: gpc_verdict (8 B)
 VERDICT_DTYPE = np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"), ("flags", "u1")])
+LB_DTYPE = np.dtype([("endpoint_ip", "<u4"), ("endpoint_port", "<u2"), ("flags", "u1"), ("reserved", "u1"),
+                     ("group_id", "<u4"), ("out_port", "<u4")])
+LB_HIT, LB_NO_ENDPOINT, LB_DNAT, LB_REMOTE = 1, 2, 4, 8
+VTABLE_ENDPOINT_DNAT = 4
 
 
 class gpc_config(C.Structure):
@@ -86,10 +90,25 @@ class gpc_image_stats(C.Structure):
                 ("n_delta_builds", C.c_uint64)]
 
 
+class gpc_endpoint(C.Structure):
+    _fields_ = [("family", C.c_uint8), ("is_local", C.c_uint8), ("has_node_name", C.c_uint8), ("is_node_ip", C.c_uint8),
+                ("port", C.c_uint16), ("reserved", C.c_uint16), ("ip", C.c_uint8 * 16)]
+
+
+class gpc_service_config(C.Structure):
+    _fields_ = [("family", C.c_uint8), ("protocol", C.c_uint8), ("port", C.c_uint16), ("cluster_group_id", C.c_uint32),
+                ("local_group_id", C.c_uint32), ("traffic_policy_local", C.c_uint8), ("is_external", C.c_uint8),
+                ("is_nodeport", C.c_uint8), ("is_nested", C.c_uint8), ("is_dsr", C.c_uint8), ("reserved", C.c_uint8),
+                ("affinity_timeout", C.c_uint16), ("ip", C.c_uint8 * 16)]
+
+
 EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "gpc_batch_install",
            "gpc_uninstall_rule", "gpc_add_rule_addrs", "gpc_del_rule_addrs", "gpc_reassign_priorities",
            "gpc_get_policy_info", "gpc_metrics", "gpc_commit", "gpc_compact", "gpc_classify", "gpc_classify_host", "gpc_counters",
            "gpc_reset_counters", "gpc_dump_flows", "gpc_get_image_stats", "gpc_debug_image", "gpc_debug_epoch", "gpc_load_flows", "gpc_strerror",
+           "gpc_install_service_group", "gpc_uninstall_service_group", "gpc_install_endpoint_flows",
+           "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
+           "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
            "gpc_abi_version"]
 
 _lib = None
@@ -127,6 +146,19 @@ def load(path: str = LIB_PATH):
     lib.gpc_debug_epoch.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp),
                                     C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
     lib.gpc_load_flows.argtypes = [vp, C.c_char_p, sz, i32, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
+    u8p = C.POINTER(C.c_uint8)
+    lib.gpc_install_service_group.argtypes = [vp, C.c_uint32, i32, C.POINTER(gpc_endpoint), sz]
+    lib.gpc_uninstall_service_group.argtypes = [vp, C.c_uint32]
+    lib.gpc_install_endpoint_flows.argtypes = [vp, C.c_uint8, C.c_uint8, C.POINTER(gpc_endpoint), sz]
+    lib.gpc_uninstall_endpoint_flows.argtypes = [vp, C.c_uint8, C.c_uint8, C.POINTER(gpc_endpoint), sz]
+    lib.gpc_install_service_flows.argtypes = [vp, C.POINTER(gpc_service_config)]
+    lib.gpc_uninstall_service_flows.argtypes = [vp, u8p, C.c_uint8, C.c_uint16, C.c_uint8]
+    lib.gpc_install_pod.argtypes = [vp, u8p, C.c_uint8, C.c_uint32]
+    lib.gpc_uninstall_pod.argtypes = [vp, u8p, C.c_uint8]
+    lib.gpc_dump_groups.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]
+    lib.gpc_classify_lb.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32, vp]
+    lib.gpc_classify_host_lb.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32]
+    lib.gpc_debug_service_image.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -185,6 +217,30 @@ def _service(s: dict) -> gpc_service:
         out.has_group_address = 1
         out.group_address[:] = list(ipaddress.ip_address(s["group_address"]).packed)
     return out
+
+
+def _ip_bytes(ip):
+    a = ipaddress.ip_address(ip)
+    buf = (C.c_uint8 * 16)()
+    buf[:len(a.packed)] = list(a.packed)
+    return a.version, buf
+
+
+def _endpoints(eps):
+    """proxy.Endpoint dicts: {"ip", "port", "is_local", "node_name", "is_node_ip"}."""
+    arr = (gpc_endpoint * max(1, len(eps)))()
+    for i, e in enumerate(eps):
+        fam, b = _ip_bytes(e["ip"])
+        arr[i].family = fam
+        arr[i].ip[:] = list(b)
+        arr[i].port = int(e["port"])
+        arr[i].is_local = int(bool(e.get("is_local")))
+        arr[i].has_node_name = int(bool(e.get("node_name")))
+        arr[i].is_node_ip = int(bool(e.get("is_node_ip")))
+    return arr
+
+
+SVC_PROTOCOLS = {"TCP": 1, "UDP": 2, "SCTP": 3}
 
 
 class RuleBuf:
@@ -351,6 +407,64 @@ class Classifier:
             raise GpcError(rc, "gpc_load_flows (line %d)" % el.value)
         return nl.value, ns.value
 
+    # --- AntreaProxy surface (client.go:710-815)
+    def install_service_group(self, group_id, endpoints, with_session_affinity=False):
+        _check(self.lib.gpc_install_service_group(self.h, group_id, int(with_session_affinity), _endpoints(endpoints),
+                                                  len(endpoints)), "InstallServiceGroup")
+
+    def uninstall_service_group(self, group_id):
+        _check(self.lib.gpc_uninstall_service_group(self.h, group_id), "UninstallServiceGroup")
+
+    def install_endpoint_flows(self, protocol, endpoints, family=4):
+        _check(self.lib.gpc_install_endpoint_flows(self.h, SVC_PROTOCOLS[protocol], family, _endpoints(endpoints),
+                                                   len(endpoints)), "InstallEndpointFlows")
+
+    def uninstall_endpoint_flows(self, protocol, endpoints, family=4):
+        _check(self.lib.gpc_uninstall_endpoint_flows(self.h, SVC_PROTOCOLS[protocol], family, _endpoints(endpoints),
+                                                     len(endpoints)), "UninstallEndpointFlows")
+
+    def install_service_flows(self, cfg: dict):
+        """types.ServiceConfig as a dict: ip, port, protocol, cluster_group_id, local_group_id,
+        traffic_policy_local, is_external, is_nodeport, is_nested, is_dsr, affinity_timeout."""
+        c = gpc_service_config()
+        fam, b = _ip_bytes(cfg["ip"])
+        c.family = fam
+        c.ip[:] = list(b)
+        c.protocol = SVC_PROTOCOLS[cfg["protocol"]]
+        c.port = int(cfg["port"])
+        c.cluster_group_id = int(cfg.get("cluster_group_id", 0))
+        c.local_group_id = int(cfg.get("local_group_id", 0))
+        for f in ("traffic_policy_local", "is_external", "is_nodeport", "is_nested", "is_dsr"):
+            setattr(c, f, int(bool(cfg.get(f))))
+        c.affinity_timeout = int(cfg.get("affinity_timeout", 0))
+        _check(self.lib.gpc_install_service_flows(self.h, C.byref(c)), "InstallServiceFlows")
+
+    def uninstall_service_flows(self, ip, port, protocol):
+        fam, b = _ip_bytes(ip)
+        _check(self.lib.gpc_uninstall_service_flows(self.h, b, fam, int(port), SVC_PROTOCOLS[protocol]),
+               "UninstallServiceFlows")
+
+    def install_pod(self, ip, ofport):
+        fam, b = _ip_bytes(ip)
+        _check(self.lib.gpc_install_pod(self.h, b, fam, int(ofport)), "InstallPodFlows")
+
+    def uninstall_pod(self, ip):
+        fam, b = _ip_bytes(ip)
+        _check(self.lib.gpc_uninstall_pod(self.h, b, fam), "UninstallPodFlows")
+
+    def dump_groups(self) -> List[str]:
+        need = C.c_size_t()
+        self.lib.gpc_dump_groups(self.h, None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value)
+        _check(self.lib.gpc_dump_groups(self.h, buf, need.value, C.byref(need)), "gpc_dump_groups")
+        return [l for l in buf.value.decode().split("\n") if l]
+
+    def debug_service_image(self):
+        b = C.POINTER(C.c_uint32)()
+        n = C.c_size_t()
+        _check(self.lib.gpc_debug_service_image(self.h, C.byref(b), C.byref(n)), "gpc_debug_service_image")
+        return C.cast(b, C.c_void_p).value
+
     # --- data path
     def commit(self):
         """Publish pending changes (a delta epoch when few rules changed, else a full rebuild)."""
@@ -360,14 +474,18 @@ class Classifier:
         """Publish with a full image rebuild (empties the overlay)."""
         _check(self.lib.gpc_compact(self.h), "gpc_compact")
 
-    def classify_host(self, cols: Dict[str, np.ndarray], count=False) -> np.ndarray:
+    def classify_host(self, cols: Dict[str, np.ndarray], count=False, lb=False):
+        """Verdicts (n, 2); with lb=True also the Service stage results (n,) of LB_DTYPE."""
         soa, keep, n = pkt_soa_host(cols)
         out = np.zeros(2 * n, dtype=VERDICT_DTYPE)
-        _check(self.lib.gpc_classify_host(self.h, C.byref(soa), n, out.ctypes.data, int(count)), "gpc_classify_host")
-        return out.reshape(n, 2)
+        lbo = np.zeros(n, dtype=LB_DTYPE) if lb else None
+        _check(self.lib.gpc_classify_host_lb(self.h, C.byref(soa), n, out.ctypes.data,
+                                             lbo.ctypes.data if lb else None, int(count)), "gpc_classify_host")
+        return (out.reshape(n, 2), lbo) if lb else out.reshape(n, 2)
 
-    def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0):
-        _check(self.lib.gpc_classify(self.h, C.byref(soa), n, out_ptr, int(count), stream or None), "gpc_classify")
+    def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, lb_ptr: int = 0):
+        _check(self.lib.gpc_classify_lb(self.h, C.byref(soa), n, out_ptr, lb_ptr or None, int(count), stream or None),
+               "gpc_classify")
 
     def counters(self):
         p = C.POINTER(C.c_uint64)()

@@ -220,7 +220,68 @@ def config3(seed=RULE_SEED, n_policies_per_dir=500, rules_per_policy=100) -> Wor
     return _acnp_config("C3", n_policies_per_dir, rules_per_policy, peers, svc, seed)
 
 
-CONFIGS = {"C1": config1, "C2": config2, "C3": config3}
+# ------------------------------------------------------------------------------ AntreaProxy (C4)
+SVC_PROTOS = (("TCP", 6), ("UDP", 17), ("SCTP", 132))
+
+
+def add_services(wl: Workload, n_services: int, eps_per_service: int, seed=RULE_SEED + 4, remote_frac=0.7,
+                 noep_frac=0.02, local_policy_frac=0.1, svc_frac=0.5) -> Workload:
+    """ClusterIP Services (10.96.0.0/12) with `eps_per_service` Endpoints each: local Endpoints are
+    the workload's local Pods (ofports known to the Pod map), remote ones are Pods on other Nodes
+    (10.128.0.0/9). A fraction of Services has no Endpoints, a fraction Local traffic policy.
+    `svc_frac` of the generated packets are aimed at a Service (ip, port, protocol)."""
+    rng = np.random.default_rng(seed)
+    base = int(ipaddress.ip_address("10.96.0.0"))
+    ips = base + 1 + rng.choice(1 << 20, size=n_services, replace=False)
+    ports = rng.integers(1, 65536, size=n_services)
+    pk = rng.choice(3, size=n_services, p=[0.8, 0.15, 0.05])
+    wl.services, wl.groups, wl.endpoint_flows = [], {}, []
+    wl.pods = {int(ip): int(port) for ip, port in zip(wl.local_ips, wl.local_ports)}
+    for i in range(n_services):
+        proto = SVC_PROTOS[pk[i]][0]
+        n_ep = 0 if rng.random() < noep_frac else eps_per_service
+        eps = []
+        for _ in range(n_ep):
+            if rng.random() < remote_frac:
+                ip = int(ipaddress.ip_address("10.128.0.0")) + int(rng.integers(1, 1 << 23))
+                eps.append({"ip": _ip(ip), "port": int(rng.integers(1024, 65536)), "is_local": False,
+                            "node_name": "node%d" % int(rng.integers(1, 64))})
+            else:
+                j = int(rng.integers(0, len(wl.local_ips)))
+                eps.append({"ip": _ip(wl.local_ips[j]), "port": int(rng.integers(1024, 65536)), "is_local": True,
+                            "node_name": "node0"})
+        local = rng.random() < local_policy_frac
+        cgid, lgid = 2 * i + 1, 2 * i + 2
+        wl.groups[lgid if local else cgid] = eps
+        if eps:
+            wl.endpoint_flows.append((proto, eps))
+        wl.services.append({"ip": _ip(ips[i]), "port": int(ports[i]), "protocol": proto, "cluster_group_id": cgid,
+                            "local_group_id": lgid, "traffic_policy_local": bool(local)})
+    wl.svc_meta = {"ip": ips.astype(np.uint32), "port": ports.astype(np.uint16),
+                   "proto": np.array([SVC_PROTOS[k][1] for k in pk], np.uint8)}
+    wl.svc_frac = svc_frac
+    return wl
+
+
+def install_services(clf, wl: Workload):
+    """The AntreaProxy calls for wl's Services (client.go:710-815 order: groups, Endpoint flows,
+    Service flows) plus the Pod map."""
+    for ip, port in wl.pods.items():
+        clf.install_pod(_ip(ip), port)
+    for gid, eps in wl.groups.items():
+        clf.install_service_group(gid, eps)
+    for proto, eps in wl.endpoint_flows:
+        clf.install_endpoint_flows(proto, eps)
+    for cfg in wl.services:
+        clf.install_service_flows(cfg)
+
+
+def config4(seed=RULE_SEED) -> Workload:
+    """C3 + 10k Services x 10 Endpoints (AntreaProxy ServiceLB / EndpointDNAT in front of policy)."""
+    return add_services(config3(seed), 10000, 10)
+
+
+CONFIGS = {"C1": config1, "C2": config2, "C3": config3, "C4": config4}
 
 
 # ------------------------------------------------------------------------------------- packets
@@ -257,6 +318,14 @@ def gen_packets(wl: Workload, n: int, seed=PKT_SEED) -> Dict[str, np.ndarray]:
     sport = np.where(icmp, rng.choice([0, 3, 8, 11], size=n), sport).astype(np.uint16)
     dport = np.where(icmp, 0, dport).astype(np.uint16)
     length = rng.integers(64, 1500, size=n).astype(np.uint16)
+    if getattr(wl, "svc_meta", None) is not None:  # aim svc_frac of the packets at a Service
+        sm = wl.svc_meta
+        k = rng.integers(0, len(sm["ip"]), size=n)
+        to_svc = rng.random(n) < wl.svc_frac
+        dst = np.where(to_svc, sm["ip"][k], dst).astype(np.uint32)
+        dport = np.where(to_svc, sm["port"][k], dport).astype(np.uint16)
+        proto = np.where(to_svc, sm["proto"][k], proto).astype(np.uint8)
+        sport = np.where(to_svc, rng.integers(1024, 65536, size=n), sport).astype(np.uint16)
     return {"src": src, "dst": dst, "sport": sport, "dport": dport, "proto": proto, "out_port": out_port,
             "len": length}
 
@@ -299,6 +368,13 @@ def gen_packets_torch(wl: Workload, n: int, seed=PKT_SEED, device="cuda"):
     sport = torch.where(icmp, types, sport)
     dport = torch.where(icmp, torch.zeros_like(dport), dport)
     length = torch.randint(64, 1500, (n,), generator=g, device=device)
+    if getattr(wl, "svc_meta", None) is not None:
+        sm = {k: torch.as_tensor(v.astype(np.int64), device=device) for k, v in wl.svc_meta.items()}
+        k = torch.randint(0, len(wl.svc_meta["ip"]), (n,), generator=g, device=device)
+        to_svc = frac() < wl.svc_frac
+        dst = torch.where(to_svc, sm["ip"][k], dst)
+        dport = torch.where(to_svc, sm["port"][k], dport)
+        proto = torch.where(to_svc, sm["proto"][k], proto)
     u32 = lambda t: (t & 0xFFFFFFFF).to(torch.int64).to(torch.uint32) if hasattr(torch, "uint32") else t.to(torch.int32)
     return {"src": u32(src), "dst": u32(dst), "sport": sport.to(torch.int16), "dport": dport.to(torch.int16),
             "proto": proto.to(torch.uint8), "out_port": u32(out_port), "len": length.to(torch.int16)}

@@ -139,6 +139,8 @@ def main():
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
     args = ap.parse_args()
     churn = args.config == "C5"
+    if args.config == "C4":  # the C oracle has no AntreaProxy stage: no CPU leg for C4
+        args.no_cpu_baseline = True
     if churn:
         args.no_traffic = True
         args.no_cpu_baseline = True
@@ -175,6 +177,8 @@ def main():
     clf = gpc.Classifier(device=local)
     clf.initialize()
     clf.batch_install_policy_rule_flows(wl.rules)
+    if getattr(wl, "services", None):
+        workload.install_services(clf, wl)
     clf.commit()
     t_build = time.time() - t0
 
@@ -262,7 +266,7 @@ def main():
         mix[stage] = {names[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
 
     lbar = _lbar(wl, clf)
-    b_in, b_out = 17, 16
+    b_in, b_out = (19 if getattr(wl, "services", None) else 17), 16  # +2 B len for C4
     b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
     pps_kernel = n / (kern_ms / 1e3)
     achieved = pps_kernel * b_alg / 1e9
@@ -290,6 +294,11 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if getattr(wl, "services", None):
+        res["metric"] = "Mpps classified (AntreaProxy ServiceLB/EndpointDNAT + policy) @100k rules, 10k Services"
+        res["config"]["services"] = len(wl.services)
+        res["config"]["endpoints"] = sum(len(e) for e in wl.groups.values())
+        res["config"]["to_service_frac"] = wl.svc_frac
     if update is not None:
         res["update"] = update
         res["metric"] = "Mpps classified under AddPolicyRuleAddress/DeletePolicyRuleAddress churn @100k rules"

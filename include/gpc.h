@@ -194,6 +194,46 @@ typedef struct gpc_verdict {     /* 8 bytes; gpc_classify writes 2 per packet: [
   uint8_t flags;                 /* GPC_VFLAG_* */
 } gpc_verdict;
 
+/* AntreaProxy. proxy.Endpoint (pkg/agent/proxy/types) as serviceEndpointGroup and
+ * endpointDNATFlow read it (pipeline.go:2553-2592, 2502-2528). */
+typedef struct gpc_endpoint {
+  uint8_t family;                /* 4 or 6 */
+  uint8_t is_local;              /* Endpoint.GetIsLocal() */
+  uint8_t has_node_name;         /* Endpoint.GetNodeName() != "" */
+  uint8_t is_node_ip;            /* nodeIPChecker.IsNodeIP(endpoint IP) (hostNetwork Endpoint) */
+  uint16_t port;
+  uint16_t reserved;
+  uint8_t ip[16];
+} gpc_endpoint;
+
+typedef struct gpc_service_config { /* types.ServiceConfig (pkg/agent/types/service.go:24-40) */
+  uint8_t family;
+  uint8_t protocol;              /* gpc_protocol: TCP, UDP or SCTP */
+  uint16_t port;                 /* ServicePort */
+  uint32_t cluster_group_id, local_group_id;
+  uint8_t traffic_policy_local, is_external, is_nodeport, is_nested, is_dsr;
+  uint8_t reserved;
+  uint16_t affinity_timeout;
+  uint8_t ip[16];                /* ServiceIP */
+} gpc_service_config;
+
+/* Per-packet load-balancing result (optional output of gpc_classify_lb), 16 bytes. */
+typedef struct gpc_lb_result {
+  uint32_t endpoint_ip;          /* selected Endpoint (reg3), host byte order; 0 if none      */
+  uint16_t endpoint_port;        /* reg4[0..15]                                               */
+  uint8_t flags;                 /* GPC_LB_*                                                  */
+  uint8_t reserved;
+  uint32_t group_id;             /* Service group (reg7 ServiceGroupIDField)                   */
+  uint32_t out_port;             /* reg1 after L3Forwarding to the Endpoint (local Pod ofport) */
+} gpc_lb_result;
+#define GPC_LB_HIT 0x1           /* the packet matched a ServiceLB flow                        */
+#define GPC_LB_NO_ENDPOINT 0x2   /* ... of a Service without Endpoints (rejected, pipeline.go
+                                    serviceNoEndpointFlow -> SvcReject packet-in)               */
+#define GPC_LB_DNAT 0x4          /* an EndpointDNAT flow rewrote the destination               */
+#define GPC_LB_REMOTE 0x8        /* RemoteEndpointRegMark: the Endpoint is on another Node      */
+/* gpc_verdict.table value of the egress verdict of a packet rejected by EndpointDNAT (no Endpoint). */
+#define GPC_VTABLE_ENDPOINT_DNAT 4
+
 typedef struct gpc_policy_info { /* GetPolicyInfoFromConjunction result */
   int32_t found;
   uint8_t policy_type;
@@ -267,6 +307,29 @@ int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n);
 int gpc_load_flows(gpc_ctx* ctx, const char* text, size_t len, int32_t replace, size_t* n_loaded, size_t* n_skipped,
                    size_t* err_line);
 
+/* ---------------------------------------------------------------------------- AntreaProxy surface */
+/* InstallServiceGroup(groupID, withSessionAffinity, endpoints) error       client.go:710 */
+int gpc_install_service_group(gpc_ctx* ctx, uint32_t group_id, int32_t with_session_affinity, const gpc_endpoint* eps,
+                              size_t n);
+/* UninstallServiceGroup(groupID) error                                      client.go:729 */
+int gpc_uninstall_service_group(gpc_ctx* ctx, uint32_t group_id);
+/* InstallEndpointFlows(protocol, endpoints) error                           client.go:750 */
+int gpc_install_endpoint_flows(gpc_ctx* ctx, uint8_t protocol, uint8_t family, const gpc_endpoint* eps, size_t n);
+/* UninstallEndpointFlows(protocol, endpoints) error                         client.go:772 */
+int gpc_uninstall_endpoint_flows(gpc_ctx* ctx, uint8_t protocol, uint8_t family, const gpc_endpoint* eps, size_t n);
+/* InstallServiceFlows(*types.ServiceConfig) error                           client.go:790
+ * Supported: ClusterIP / LoadBalancer / ExternalIP Services (optionally Local traffic policy)
+ * without session affinity, NodePort, DSR or multi-cluster nesting; other configs -GPC_EINVAL. */
+int gpc_install_service_flows(gpc_ctx* ctx, const gpc_service_config* cfg);
+/* UninstallServiceFlows(svcIP, svcPort, protocol) error                     client.go:809 */
+int gpc_uninstall_service_flows(gpc_ctx* ctx, const uint8_t* ip, uint8_t family, uint16_t port, uint8_t protocol);
+/* InstallPodFlows NP-relevant part (client.go:~600): Pod IP -> ofport, the L3Forwarding result
+ * (reg1 TargetOFPortField) for traffic DNATed to a local Endpoint. */
+int gpc_install_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family, uint32_t ofport);
+int gpc_uninstall_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family);
+/* ovs-ofctl dump-groups style text of the realized groups, '\n' separated. */
+int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed);
+
 /* ---------------------------------------------------------------------------- data path */
 /* Publish the realized flow table to the device atomically (the bundle commit,
  * ofctrl_bridge.go:468-539). Rules whose flows changed since the last full build are rebuilt
@@ -279,8 +342,18 @@ int gpc_compact(gpc_ctx* ctx);
 /* Classify n packets whose columns are DEVICE pointers; writes 2*n verdicts (device pointer).
  * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t. */
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
+/* gpc_classify plus the AntreaProxy stage in front of the policy tables: packets to a Service
+ * (ServiceLB flow hit) get an Endpoint from the group (select bucket by a symmetric L4 hash of the
+ * 5-tuple), are DNATed by the EndpointDNAT flow and continue to the policy stages with nw_dst /
+ * tp_dst = the Endpoint, ct_nw_dst = the Service IP, reg7 = the group id and reg1 / destination
+ * from the Pod map. lb_out (device, n entries, may be NULL) receives the selection. gpc_classify
+ * runs the same stage (it just does not write lb_out). */
+int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
+                    int32_t count, void* stream);
 /* Same with HOST pointers (copies in and out; synchronous). */
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
+int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
+                         int32_t count);
 /* Per-rule counters as a device buffer of n_slots x {packets, bytes, sessions} uint64 (for an
  * RCCL all-reduce by the caller), plus the slot -> conj id map (host, valid until the next commit).
  * Sessions as the Metric flows count them: ct_state=+new packets for allow rules, every packet for
@@ -296,6 +369,8 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out);
  * device reset). Pointers stay valid until the next gpc_commit. Used by tests to verify the
  * image independently of the device. */
 int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes);
+/* The host copy of the committed Service image (NULL / 0 when no Services). */
+int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words);
 /* The overlay image and tombstone bitmap of the current epoch (NULL / 0 when absent). */
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** overlay_blob, size_t* overlay_words, const void** overlay_hdr,
                     const uint32_t** dead, size_t* dead_words);

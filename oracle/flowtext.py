@@ -80,16 +80,19 @@ def parse_actions(s: str):
                 acts.append(("set_reg", int(dst[3:]), v, m))
         elif a.startswith("ct("):
             inner = a[3:-1]
-            table, labels = None, []
+            table, labels, nat = None, [], None
             for part in _split_top(inner):
                 if part.startswith("table="):
                     table = part[6:]
+                elif part.startswith("nat(dst=") and part.endswith(")"):
+                    ip, _, port = part[len("nat(dst="):-1].rpartition(":")
+                    nat = (int(ipaddress.ip_address(ip)), int(port))
                 elif part.startswith("exec("):
                     for ea in _split_top(part[5:-1]):
                         if ea.startswith("set_field:") and ea.endswith("->ct_label"):
                             v, m = _vm(ea[len("set_field:"):-len("->ct_label")])
                             labels.append((v, m))
-            acts.append(("ct_commit", table, labels))
+            acts.append(("ct_commit", table, labels, nat))
         elif a.startswith("goto_table:"):
             acts.append(("goto_table", a[len("goto_table:"):]))
         elif a.startswith("resubmit(,") or a.startswith("resubmit:"):
@@ -100,6 +103,20 @@ def parse_actions(s: str):
         else:
             acts.append(("other", a))
     return acts
+
+
+def parse_group(line: str) -> dict:
+    """`group_id=G,type=select,bucket=bucket_id:B,weight:W,actions=...,bucket=...` (the text the
+    reference tests print for a binding.Group, client_test.go:1024-1090)."""
+    head, *buckets = line.strip().split(",bucket=")
+    gid = int(head.split(",")[0].split("=")[1])
+    out = {"id": gid, "buckets": []}
+    for b in buckets:
+        meta, _, acts = b.partition(",actions=")
+        kv = dict(x.split(":", 1) for x in meta.split(","))
+        out["buckets"].append({"id": int(kv["bucket_id"]), "weight": int(kv["weight"]),
+                               "actions": parse_actions(acts)})
+    return out
 
 
 def parse_flow(line: str) -> dict:

@@ -21,7 +21,7 @@ from __future__ import annotations
 from collections import defaultdict
 from typing import Dict, List, Optional
 
-from .flowtext import parse_flow
+from .flowtext import parse_flow, parse_group
 
 # verdict action codes (must equal include/gpc.h GPC_ACT_*)
 ACT_NONE, ACT_NO_MATCH, ACT_ALLOW, ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP, ACT_BYPASS = range(7)
@@ -30,7 +30,37 @@ FLAG_PASS, FLAG_TIE = 1, 2
 DEST_POD, DEST_GATEWAY, DEST_TUNNEL, DEST_UPLINK = 0, 1, 2, 3
 CT_NEW, CT_EST, CT_REL, CT_RPL, CT_TRK = 1, 2, 4, 8, 32
 
+TABLE_ENDPOINT_DNAT = 4  # verdict table code of a Service without Endpoints (gpc.h GPC_VTABLE_ENDPOINT_DNAT)
+LB_HIT, LB_NO_ENDPOINT, LB_DNAT, LB_REMOTE = 1, 2, 4, 8
+EP_TO_SELECT, SVC_NO_EP, REMOTE_EP = 0x10000, 1 << 14, 1 << 26  # fields.go reg marks
+
 EGRESS = ("AntreaPolicyEgressRule", "EgressRule", "EgressDefaultRule", "EgressMetric")
+
+
+def _mix32(x):
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def lb_hash(src, dst, sport, dport, proto):
+    """Select-group bucket hash (OVS dp_hash over a symmetric L4 hash: OVS-internal, parity unpinned;
+    restated as in antrea_amd/csrc/core.hpp lb_hash)."""
+    return _mix32((src ^ dst) ^ ((_mix32(((sport ^ dport) << 8) | (proto & 0xFF)) * 0x9E3779B1) & 0xFFFFFFFF))
+
+
+def select_bucket(buckets, pkt):
+    """Bucket of a select group with equal weights: a 2^k >= 64 slot table, slot s -> bucket s mod n."""
+    n = len(buckets)
+    lg = 6
+    while (1 << lg) < n:
+        lg += 1
+    slot = lb_hash(pkt["src"], pkt["dst"], pkt.get("sport", 0), pkt.get("dport", 0), pkt["proto"]) & ((1 << lg) - 1)
+    return buckets[slot % n]
 INGRESS = ("AntreaPolicyIngressRule", "IngressRule", "IngressDefaultRule", "IngressMetric")
 
 
@@ -138,7 +168,8 @@ def classifier_lookup(flows: List[dict], pkt: dict, st: dict, allow_conj=True):
 class Pipeline:
     """The two policy stages over a flow dump (list of flow-text lines)."""
 
-    def __init__(self, flow_lines: List[str], tiers: Optional[Dict[int, int]] = None):
+    def __init__(self, flow_lines: List[str], tiers: Optional[Dict[int, int]] = None,
+                 group_lines: Optional[List[str]] = None, pods: Optional[Dict[int, int]] = None):
         self.tables: Dict[str, List[dict]] = defaultdict(list)
         for line in flow_lines:
             f = parse_flow(line)
@@ -146,6 +177,59 @@ class Pipeline:
             f["_by"] = 0
             self.tables[f["table"]].append(f)
         self.tiers = tiers or {}
+        self.groups = {g["id"]: g for g in (parse_group(l) for l in (group_lines or []))}
+        self.pods = pods or {}  # Pod IP -> ofport (L3Forwarding of DNATed traffic)
+
+    def service_stage(self, pkt: dict):
+        """AntreaProxy tables in front of the policy stages (pipeline.go:2373-2592): ServiceLB flow ->
+        select group bucket -> EndpointDNAT ct(nat) -> L3Forwarding. Returns (packet as the policy
+        tables see it, lb flags, lb result dict)."""
+        if pkt["proto"] not in (6, 17, 132) or not self.tables.get("ServiceLB"):
+            return pkt, 0, None
+        st = {"regs": {4: EP_TO_SELECT}, "ct_label": 0, "conj_id": 0}
+        f, _ = classifier_lookup(self.tables["ServiceLB"], pkt, st, allow_conj=False)
+        if f is None:
+            return pkt, 0, None
+        p = dict(pkt)
+        p.setdefault("ct_dst", pkt["dst"])  # ct_nw_dst: the pre-NAT (Service) address
+        flags, gid = LB_HIT, None
+        for a in f["actions"]:
+            if a[0] == "set_reg":
+                _, r, v, m = a
+                m = 0xFFFFFFFF if m is None else m
+                st["regs"][r] = (st["regs"].get(r, 0) & ~m) | (v & m)
+            elif a[0] == "group":
+                gid = a[1]
+        if 7 in st["regs"]:
+            p["svc_group"] = st["regs"][7]
+        res = {"group_id": gid, "endpoint_ip": 0, "endpoint_port": 0, "out_port": 0}
+        g = self.groups.get(gid)
+        if g is None or not g["buckets"]:
+            return p, flags | LB_NO_ENDPOINT, res
+        b = select_bucket(g["buckets"], pkt)
+        for a in b["actions"]:
+            if a[0] == "set_reg":
+                _, r, v, m = a
+                m = 0xFFFFFFFF if m is None else m
+                st["regs"][r] = (st["regs"].get(r, 0) & ~m) | (v & m)
+        if st["regs"].get(0, 0) & SVC_NO_EP:  # serviceNoEndpointFlow: packet-in, rejected
+            return p, flags | LB_NO_ENDPOINT, res
+        if st["regs"].get(4, 0) & REMOTE_EP:
+            flags |= LB_REMOTE
+        ep_ip, ep_port = st["regs"].get(3, 0), st["regs"].get(4, 0) & 0xFFFF
+        res.update(endpoint_ip=ep_ip, endpoint_port=ep_port)
+        d, _ = classifier_lookup(self.tables.get("EndpointDNAT", []), pkt, st, allow_conj=False)
+        if d is not None:
+            for a in d["actions"]:
+                if a[0] == "ct_commit" and len(a) > 3 and a[3] is not None:
+                    p["dst"], p["dport"] = a[3]
+                    flags |= LB_DNAT
+        if ep_ip in self.pods:
+            p["out_port"], p["dest"] = self.pods[ep_ip], DEST_POD
+        else:
+            p["out_port"], p["dest"] = 0, DEST_TUNNEL if flags & LB_REMOTE else DEST_GATEWAY
+        res["out_port"] = p["out_port"]
+        return p, flags, res
 
     def _stage(self, tables, pkt, st):
         t1, t2, t3, metric = tables
@@ -209,8 +293,14 @@ class Pipeline:
             tindex = 0
         return action, conj, tindex, flags, mf
 
-    def classify(self, pkt: dict):
-        """Returns ((e_act, e_conj, e_table, e_tier, e_flags), (i_act, ...))."""
+    def classify(self, pkt: dict, lb: Optional[list] = None):
+        """Returns ((e_act, e_conj, e_table, e_tier, e_flags), (i_act, ...)). `lb`: optional list that
+        receives (flags, result dict) of the Service stage."""
+        pkt, lbf, lbr = self.service_stage(pkt)
+        if lb is not None:
+            lb.append((lbf, lbr))
+        if lbf & LB_NO_ENDPOINT:
+            return (ACT_REJECT, 0, TABLE_ENDPOINT_DNAT, 0, 0), (ACT_NONE, 0, 0, 0, 0)
         st = {"regs": {}, "ct_label": 0, "conj_id": 0}
         ct = pkt.get("ct_state", CT_NEW | CT_TRK)
         e = self._stage(EGRESS, pkt, st)

@@ -29,19 +29,34 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
 using namespace gpc;
 
 extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_t* oblob, const void* ohdr,
-                            const uint32_t* dead, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
-                            unsigned long long* counters) {
+                            const uint32_t* dead, const uint32_t* svc, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
+                            uint32_t* lb_out, unsigned long long* counters) {
   View im{{blob, static_cast<const ImageHdr*>(hdr), dead}, {oblob, static_cast<const ImageHdr*>(ohdr), nullptr},
           oblob ? 2u : 1u};
   for (size_t i = 0; i < n; i++) {
+    const uint32_t src = pk->src[i];
+    uint32_t dst = pk->dst[i], dport = pk->dport[i];
+    const uint32_t sport = pk->sport[i], proto = pk->proto[i];
+    uint32_t out_port = pk->out_port[i], svc_group = pk->svc_group ? pk->svc_group[i] : 0u;
+    uint32_t dest = pk->dest ? pk->dest[i] : 0u;
+    const uint32_t ct_src = pk->ct_src ? pk->ct_src[i] : src, ct_dst = pk->ct_dst ? pk->ct_dst[i] : dst;
+    uint32_t lb[4] = {0, 0, 0, 0};
+    uint32_t lbf = svc ? lb_stage(svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb) : 0u;
+    if (lb_out)
+      for (int k = 0; k < 4; k++) lb_out[4 * i + k] = lb[k];
+    if (lbf & GPC_LB_NO_ENDPOINT) {
+      uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);
+      w[0] = 0;
+      w[1] = pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0);
+      w[2] = w[3] = 0;
+      continue;
+    }
     Pkt p;
-    const uint32_t src = pk->src[i], dst = pk->dst[i];
-    make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
-             pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, pk->ct_src ? pk->ct_src[i] : src,
-             pk->ct_dst ? pk->ct_dst[i] : dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+    make_pkt(p, src, dst, sport, dport, proto, out_port, pk->in_port ? pk->in_port[i] : 0u, svc_group,
+             pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
     g_lines.clear();
     g_line_site.clear();
-    PacketOut o = classify_packet(im, p, pk->dest ? pk->dest[i] : 0u);
+    PacketOut o = classify_packet(im, p, dest);
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     std::sort(g_lines.begin(), g_lines.end());

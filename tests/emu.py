@@ -27,15 +27,16 @@ def load():
     _lib = C.CDLL(LIB)
     _lib.gpc_emu_stats_arr = (C.c_ulonglong * 8).in_dll(_lib, "gpc_emu_stats")
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
-    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                  C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p]
+    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
     return _lib
 
 
-def classify(clf: "gpc.Classifier", cols, counters=None):
+def classify(clf: "gpc.Classifier", cols, counters=None, lb=None):
     """Emulated verdicts (n, 2) of the image last committed by `clf` (commit may fail with EDEV
     on a host without GPU: the host image is built before the upload). `counters`: optional
-    uint64 array of n_slots x 3 {packets, bytes, sessions} accumulated like the kernel does."""
+    uint64 array of n_slots x 3 {packets, bytes, sessions} accumulated like the kernel does.
+    `lb`: optional gpc.LB_DTYPE array of n entries receiving the Service stage results."""
     blob, nw, hdr, _ = clf.debug_image()
     oblob, ohdr, dead, _ = clf.debug_epoch()
     soa, keep, n = gpc.pkt_soa_host(cols)
@@ -44,7 +45,12 @@ def classify(clf: "gpc.Classifier", cols, counters=None):
     if counters is not None:
         assert counters.dtype == np.uint64 and counters.flags.c_contiguous
         cptr = counters.ctypes.data
-    load().emu_classify(blob, hdr, oblob, ohdr, dead, C.byref(soa), n, out.ctypes.data, cptr)
+    svc = clf.debug_service_image()
+    lptr = None
+    if lb is not None:
+        assert lb.dtype == gpc.LB_DTYPE and len(lb) >= n
+        lptr = lb.ctypes.data
+    load().emu_classify(blob, hdr, oblob, ohdr, dead, svc, C.byref(soa), n, out.ctypes.data, lptr, cptr)
     return out.reshape(n, 2)
 
 

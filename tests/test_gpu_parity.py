@@ -138,3 +138,29 @@ def test_gpu_delta_epochs(name):
     assert c.image_stats()["n_overlay_rules"] == 0
     again = c.classify_host(cols)
     _cmp(again, want, cols)
+
+
+@pytest.mark.parametrize("name", ["C1", "C4"])
+def test_gpu_service_stage(name):
+    """AntreaProxy stage on the device: verdicts and per-packet LB results equal the host emulation of
+    the same epoch (small: C1 + 60 Services; full: C4 = C3 + 10k Services x 10 Endpoints); the small
+    case also against the oracle."""
+    from tests.test_service import _oracle, _svc_workload
+    wl = _svc_workload("C1", 61) if name == "C1" else workload.config4()
+    n = 3000 if name == "C1" else 200_000
+    cols = workload.gen_packets(wl, n, seed=61)
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    workload.install_services(c, wl)
+    c.commit()
+    got, lb = c.classify_host(cols, lb=True)
+    want_lb = np.zeros(n, dtype=gpc.LB_DTYPE)
+    want = emu.classify(c, cols, lb=want_lb)
+    _cmp(got, want, cols)
+    assert (lb == want_lb).all()
+    assert ((lb["flags"] & gpc.LB_HIT) != 0).mean() > 0.3
+    if name == "C1":
+        o, olb = _oracle(wl, c, cols, n)
+        _cmp(got, o, cols)
+        assert (lb == olb).all()

@@ -1,0 +1,151 @@
+"""AntreaProxy stage: ServiceLB / EndpointDNAT flows and Endpoint groups.
+
+Flow and group text is pinned by the reference's own golden strings (client_test.go, transcribed in
+tests/golden/service_flows.json). Classification: the product's Service image + kernel body (host
+emulation) against the oracle, which executes OVS semantics over the same realized flow / group text
+(ServiceLB lookup, select-group bucket, EndpointDNAT ct(nat), L3Forwarding by the Pod map) in front
+of the policy stages compiled by the oracle compiler. The select-group bucket hash is OVS-internal
+(not in the reference): the bucket choice is parity unpinned and both sides use the restatement in
+core.hpp lb_hash / ovs_cls.select_bucket."""
+import copy
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from oracle import compiler as oc
+from oracle import ovs_cls
+from tests import emu
+from tests.test_emu_parity import _cmp
+from tests.util import load_golden
+
+GOLD = load_golden("service_flows.json")
+
+
+@pytest.mark.parametrize("case", GOLD["groups"], ids=[c["name"] for c in GOLD["groups"]])
+def test_group_text_golden(case):
+    c = gpc.Classifier()
+    c.install_service_group(case["group_id"], case["endpoints"], case["with_session_affinity"])
+    assert c.dump_groups() == [case["expected"]]
+    c.uninstall_service_group(case["group_id"])
+    assert c.dump_groups() == []
+
+
+@pytest.mark.parametrize("case", GOLD["endpoint_flows"], ids=[c["name"] for c in GOLD["endpoint_flows"]])
+def test_endpoint_flows_golden(case):
+    c = gpc.Classifier()
+    c.install_endpoint_flows(case["protocol"], case["endpoints"])
+    assert sorted(c.dump_flows()) == sorted(case["expected"])
+    c.uninstall_endpoint_flows(case["protocol"], case["endpoints"])
+    assert c.dump_flows() == []
+
+
+@pytest.mark.parametrize("case", GOLD["service_flows"], ids=[c["name"] for c in GOLD["service_flows"]])
+def test_service_flows_golden(case):
+    c = gpc.Classifier()
+    c.install_service_flows(case["config"])
+    assert c.dump_flows() == case["expected"]
+    cfg = case["config"]
+    c.uninstall_service_flows(cfg["ip"], cfg["port"], cfg["protocol"])
+    assert c.dump_flows() == []
+
+
+@pytest.mark.parametrize("extra", [{"affinity_timeout": 100}, {"is_nodeport": True, "is_external": True},
+                                   {"is_dsr": True, "is_external": True}, {"is_nested": True},
+                                   {"is_external": True, "traffic_policy_local": True}])
+def test_unsupported_service_configs_fail_loudly(extra):
+    c = gpc.Classifier()
+    cfg = dict(GOLD["service_flows"][0]["config"], **extra)
+    with pytest.raises(gpc.GpcError):
+        c.install_service_flows(cfg)
+
+
+def _svc_workload(name, seed):
+    wl = workload.config1(seed=seed) if name == "C1" else workload.config3(seed=seed, n_policies_per_dir=6,
+                                                                              rules_per_policy=8)
+    return workload.add_services(wl, 60, 4, seed=seed, noep_frac=0.1, local_policy_frac=0.2)
+
+
+def _oracle(wl, clf, cols, n):
+    """Oracle: NP flows from the oracle compiler, Service flows / groups as realized by the product
+    (pinned against the reference goldens above)."""
+    fnp = oc.FeatureNetworkPolicy()
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    svc_flows = [f for f in clf.dump_flows() if "table=ServiceLB" in f or "table=EndpointDNAT" in f]
+    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in wl.rules}
+    pipe = ovs_cls.Pipeline(fnp.dump_flows() + svc_flows, tiers, clf.dump_groups(), wl.pods)
+    out = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
+    lb = np.zeros(n, dtype=gpc.LB_DTYPE)
+    for i in range(n):
+        rec = []
+        e, g = pipe.classify({k: int(v[i]) for k, v in cols.items()}, lb=rec)
+        for j, v in enumerate((e, g)):
+            out[i, j] = (v[1], v[0], v[2], v[3], v[4])
+        flags, r = rec[0]
+        if flags:
+            lb[i] = (r["endpoint_ip"], r["endpoint_port"], flags, 0, r["group_id"], r["out_port"])
+    return out, lb
+
+
+def _product(wl):
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    workload.install_services(c, wl)
+    emu.commit_host(c)
+    return c
+
+
+@pytest.mark.parametrize("name,seed", [("C1", 51), ("C3s", 52)])
+def test_service_stage_vs_oracle(name, seed):
+    wl = _svc_workload(name, seed)
+    n = 2500
+    cols = workload.gen_packets(wl, n, seed=seed)
+    c = _product(wl)
+    lb = np.zeros(n, dtype=gpc.LB_DTYPE)
+    got = emu.classify(c, cols, lb=lb)
+    want, want_lb = _oracle(wl, c, cols, n)
+    _cmp(got, want, cols)
+    bad = np.nonzero(lb != want_lb)[0]
+    assert len(bad) == 0, (bad[:5], lb[bad[:3]], want_lb[bad[:3]])
+    hits = (lb["flags"] & gpc.LB_HIT) != 0
+    assert hits.mean() > 0.3 and (lb["flags"] & gpc.LB_NO_ENDPOINT).any() and (lb["flags"] & gpc.LB_DNAT).any()
+    assert (got[:, 0]["table"] == gpc.VTABLE_ENDPOINT_DNAT).any()
+    # the policy stage saw the Endpoint: reg7 rules aside, DNATed packets carry the Endpoint address
+    assert (lb["endpoint_ip"][hits & ((lb["flags"] & gpc.LB_NO_ENDPOINT) == 0)] != 0).all()
+
+
+def test_service_churn_commits():
+    wl = _svc_workload("C1", 53)
+    n = 1500
+    cols = workload.gen_packets(wl, n, seed=53)
+    c = _product(wl)
+    # remove a third of the Services and half of one group's Endpoints, then re-check
+    for cfg in wl.services[::3]:
+        c.uninstall_service_flows(cfg["ip"], cfg["port"], cfg["protocol"])
+    wl.services = [s for i, s in enumerate(wl.services) if i % 3]
+    gid, eps = next((g, e) for g, e in wl.groups.items() if len(e) >= 2)
+    wl.groups[gid] = eps[: len(eps) // 2]
+    c.install_service_group(gid, wl.groups[gid])
+    emu.commit_host(c)
+    lb = np.zeros(n, dtype=gpc.LB_DTYPE)
+    got = emu.classify(c, cols, lb=lb)
+    want, want_lb = _oracle(wl, c, cols, n)
+    _cmp(got, want, cols)
+    assert (lb == want_lb).all()
+
+
+def test_reference_golden_service_in_oracle():
+    """The reference's golden ClusterIP flow + group + Endpoint flows, executed by the oracle: the packet
+    to 10.96.0.100:80/tcp is DNATed to one of the two Endpoints with reg7 = 100."""
+    flows = GOLD["service_flows"][0]["expected"] + GOLD["endpoint_flows"][0]["expected"]
+    pipe = ovs_cls.Pipeline(flows, {}, [GOLD["groups"][0]["expected"]], {})
+    import ipaddress
+    pkt = {"src": int(ipaddress.ip_address("10.10.0.5")), "dst": int(ipaddress.ip_address("10.96.0.100")),
+           "proto": 6, "sport": 40000, "dport": 80, "out_port": 0}
+    p, flags, res = pipe.service_stage(pkt)
+    assert flags & ovs_cls.LB_HIT and flags & ovs_cls.LB_DNAT and p["svc_group"] == 100
+    assert p["dst"] in (int(ipaddress.ip_address("10.10.0.100")), int(ipaddress.ip_address("10.10.0.101")))
+    assert p["dport"] == 80 and p["ct_dst"] == pkt["dst"]
+    assert (p["dest"] == ovs_cls.DEST_TUNNEL) == (p["dst"] == int(ipaddress.ip_address("10.10.0.100")))
