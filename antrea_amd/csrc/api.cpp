@@ -49,9 +49,10 @@ struct DevImage {  // one uploaded image (freed when the last epoch using it ret
 };
 
 struct DevEpoch {
-  std::shared_ptr<DevImage> base, ovl;  // base shared by the delta epochs built on it
+  std::shared_ptr<DevImage> base;       // shared by the delta epochs built on it
+  std::shared_ptr<DevImage> pool;       // journal pool of that base (d_hdr unused; append-only)
+  uint32_t jhdr = 0;                    // this epoch's JournalHdr in the pool (0: base only)
   std::shared_ptr<DevImage> svc;        // Service image (d_hdr unused), shared until Services change
-  uint32_t* d_dead = nullptr;           // tombstones over base rule ids (delta epochs)
   uint64_t epoch = 0;
   std::map<hipStream_t, hipEvent_t> last_use;  // last launch on each stream that used this epoch
 };
@@ -65,16 +66,17 @@ struct RetiredEpoch {
   }
   void release(hipStream_t s) {
     for (auto& kv : e.last_use) (void)hipEventDestroy(kv.second);
-    dev_free(e.d_dead, s);
+    (void)s;
     e = DevEpoch();
   }
 };
 
-// Delta commits: rules changed since the last full build are rebuilt into an overlay image and
-// tombstoned in the base. A full rebuild (compaction) happens when the changed set exceeds
-// max(kDeltaMinRules, base rules / kDeltaFraction).
-constexpr size_t kDeltaMinRules = 2048;
-constexpr size_t kDeltaFraction = 32;
+// Delta commits append the changed rules to the journal of the current base (image.hpp Journal).
+// A full rebuild (compaction) happens when the journal holds more than
+// max(kDeltaMinRules, base rules / kDeltaFraction) live rules or its pool would pass its capacity.
+constexpr size_t kDeltaMinRules = 16384;
+constexpr size_t kDeltaFraction = 4;
+constexpr size_t kPoolWords = size_t(256) << 20;  // 1 GiB journal pool per base (HBM is 288 GB)
 
 struct gpc_ctx {
   gpc_config cfg;
@@ -86,10 +88,7 @@ struct gpc_ctx {
   uint64_t svc_gen = ~0ull;              // FeatureService generation the image was built from
   SlotMap slots;
   HostImage last;    // base image of the current epoch: shadow state for re-upload + debug export
-  HostImage ovl;     // overlay of the current epoch (empty blob: none)
-  std::vector<uint32_t> dead;            // tombstone bitmap of the current epoch (host copy)
-  std::set<uint32_t> pending_conj;       // rules changed since the last full build
-  uint8_t pending_hard = 0;              // rule tables whose hard flows changed since then
+  Journal journal;   // delta epochs over `last` (host mirror of the device pool)
   DevEpoch cur;
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
@@ -378,8 +377,8 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   std::lock_guard<std::mutex> d(ctx->data);
   if (!ctx->cur.base) return -GPC_EINVAL;  // nothing committed yet
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.d_dead, ctx->cur.ovl ? ctx->cur.ovl->d_hdr : nullptr,
-               ctx->cur.ovl ? ctx->cur.ovl->d_blob : nullptr, ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr};
+  EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.jhdr ? ctx->cur.pool->d_blob : nullptr, ctx->cur.jhdr,
+               ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr};
   hipStream_t st = (hipStream_t)stream;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count, st);
   if (rc || n == 0) return rc;
@@ -488,9 +487,9 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   std::memset(out, 0, sizeof *out);
   out->epoch = ctx->epoch;
   out->device_bytes = ctx->cur.base ? ctx->cur.base->bytes : 0;
-  out->overlay_bytes = ctx->cur.ovl ? ctx->cur.ovl->bytes : 0;
-  for (int i = 0; i < 6; i++) out->n_overlay_rules += ctx->ovl.n_rules[i];
-  for (uint32_t w : ctx->dead) out->n_tombstones += uint32_t(__builtin_popcount(w));
+  out->overlay_bytes = ctx->journal.active() ? ctx->journal.pool.size() * 4 : 0;
+  out->n_overlay_rules = ctx->journal.n_live;
+  out->n_tombstones = ctx->journal.n_tombstones();
   out->n_full_builds = ctx->n_full;
   out->n_delta_builds = ctx->n_delta;
   for (int i = 0; i < 6; i++) {
@@ -525,16 +524,13 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
   return GPC_OK;
 }
 
-int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** oblob, size_t* on_words, const void** ohdr, const uint32_t** dead,
-                    size_t* dead_words) {
+int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  const bool has = !ctx->ovl.blob.empty();
-  if (oblob) *oblob = has ? ctx->ovl.blob.data() : nullptr;
-  if (on_words) *on_words = ctx->ovl.blob.size();
-  if (ohdr) *ohdr = has ? &ctx->ovl.hdr : nullptr;
-  if (dead) *dead = ctx->dead.empty() ? nullptr : ctx->dead.data();
-  if (dead_words) *dead_words = ctx->dead.size();
+  const bool has = ctx->journal.active();
+  if (pool) *pool = has ? ctx->journal.pool.data() : nullptr;
+  if (pool_words) *pool_words = has ? ctx->journal.pool.size() : 0;
+  if (jhdr) *jhdr = has ? ctx->journal.hdr_off : 0;
   return GPC_OK;
 }
 
@@ -547,41 +543,24 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   FeatureNP::Dirty dirty = ctx->np.take_dirty();
-  ctx->pending_conj.insert(dirty.conj.begin(), dirty.conj.end());
-  ctx->pending_hard |= dirty.hard_tables;
   const bool have_base = !ctx->last.blob.empty();
-  bool full = force_full || !have_base || ctx->last.any_noact || ctx->np.foreign() ||
-              ctx->pending_conj.size() > std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction);
-  HostImage ovl;
+  bool full = force_full || !have_base || ctx->last.any_noact || ctx->np.foreign() || ctx->journal.any_noact ||
+              ctx->journal.n_live > std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction) ||
+              ctx->journal.pool.size() > kPoolWords * 7 / 8;
   int rc = GPC_OK;
   try {
-    if (!full) {
-      rc = build_overlay(ctx->np, ctx->slots, ctx->pending_conj, ctx->pending_hard, &ovl);
-      if (rc) return rc;
-      if (ovl.any_noact) full = true;
+    if (!full && (!dirty.conj.empty() || dirty.hard_tables)) {
+      std::string err;
+      if (ctx->journal.apply(ctx->np, ctx->slots, dirty.conj, dirty.hard_tables, &err) != GPC_OK ||
+          ctx->journal.pool.size() > kPoolWords)
+        full = true;  // a shape the journal does not take (or it is full): rebuild everything
     }
     if (full) {
       HostImage img;
       rc = build_image(ctx->np, ctx->slots, &img);
       if (rc) return rc;
       ctx->last = std::move(img);
-      ctx->ovl = HostImage();
-      ctx->dead.clear();
-      ctx->pending_conj.clear();
-      ctx->pending_hard = 0;
-    } else {
-      std::vector<uint32_t> dead((ctx->last.n_rids + 31) / 32, 0u);
-      for (uint32_t c : ctx->pending_conj) {
-        auto it = ctx->last.conj_rid.find(c);
-        if (it != ctx->last.conj_rid.end()) dead[it->second >> 5] |= 1u << (it->second & 31u);
-      }
-      for (int t = 0; t < 6; t++)
-        if ((ctx->pending_hard >> t) & 1u)
-          for (uint32_t rid : ctx->last.hard_rids[t]) dead[rid >> 5] |= 1u << (rid & 31u);
-      uint32_t n_ovl = 0;
-      for (int t = 0; t < 6; t++) n_ovl += ovl.n_rules[t];
-      ctx->ovl = n_ovl ? std::move(ovl) : HostImage();
-      ctx->dead = std::move(dead);
+      ctx->journal.reset(&ctx->last);
     }
   } catch (...) {
     return -GPC_ENOMEM;
@@ -602,21 +581,26 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   hipStream_t us = ctx->ustream;
   collect_retired(ctx, false);
   DevEpoch ne;
-  if (full) {
+  if (full || !ctx->cur.base) {
     if ((rc = upload_image(ctx->last, us, &ne.base))) return rc;
+    auto pool = std::make_shared<DevImage>();  // journal pool of the new base
+    pool->s = us;
+    pool->bytes = kPoolWords * 4;
+    if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, us))) return -GPC_EDEV;
+    ne.pool = std::move(pool);
+    ctx->journal.uploaded = 0;
   } else {
     ne.base = ctx->cur.base;
-    if (!ne.base && (rc = upload_image(ctx->last, us, &ne.base))) return rc;
-    if (!ctx->ovl.blob.empty() && (rc = upload_image(ctx->ovl, us, &ne.ovl))) return rc;
-    if (!ctx->dead.empty()) {
-      size_t b = ctx->dead.size() * 4;
-      if (hip_ok(dev_alloc((void**)&ne.d_dead, b, us)) ||
-          hip_ok(hipMemcpyAsync(ne.d_dead, ctx->dead.data(), b, hipMemcpyHostToDevice, us))) {
-        RetiredEpoch{std::move(ne)}.release(us);
-        return -GPC_EDEV;
-      }
-    }
+    ne.pool = ctx->cur.pool;
   }
+  Journal& jn = ctx->journal;
+  if (jn.active() && jn.pool.size() > jn.uploaded) {  // append-only: only the new tail travels
+    if (hip_ok(hipMemcpyAsync(ne.pool->d_blob + jn.uploaded, jn.pool.data() + jn.uploaded,
+                              (jn.pool.size() - jn.uploaded) * 4, hipMemcpyHostToDevice, us)))
+      return -GPC_EDEV;
+    jn.uploaded = jn.pool.size();
+  }
+  ne.jhdr = jn.active() ? jn.hdr_off : 0;
   if (!svc_changed) ne.svc = ctx->cur.svc;
   else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, us, &ne.svc))) return rc;
   ne.epoch = ++ctx->epoch;

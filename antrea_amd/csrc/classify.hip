@@ -50,7 +50,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   Pkt p;
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
            pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
-  View im{{ep.blob, ep.hdr, kDelta ? ep.dead : nullptr}, {ep.oblob, ep.ohdr, nullptr}, (kDelta && ep.oblob) ? 2u : 1u};
+  View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
+  if (kDelta) {
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
+    if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
+    im.n_img = 2u;
+  }
   PacketOut o = classify_packet(im, p, dest);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
@@ -72,7 +77,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
                     unsigned long long* counters, int count, hipStream_t stream) {
   if (n == 0) return 0;
   if ((n + kBlock - 1) / kBlock > 0xffffffffull) return -GPC_EINVAL;
-  const bool delta = ep.dead || ep.oblob, svc = ep.svc != nullptr;
+  const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
   if (delta && svc) launch<true, true>(ep, pk, n, out, lb_out, counters, count, stream);
   else if (delta) launch<true, false>(ep, pk, n, out, lb_out, counters, count, stream);
   else if (svc) launch<false, true>(ep, pk, n, out, lb_out, counters, count, stream);

@@ -225,17 +225,70 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 struct Img {
   const uint32_t* blob;
   const ImageHdr* hdr;
-  const uint32_t* dead;  // tombstone bitmap over this image's rule ids (delta epochs), or null
+  const uint32_t* dead;   // tombstones over this image's rule ids (delta epochs), or null: a page table
+  const uint32_t* dpool;  // of journal-pool word offsets, one 256-word (8192-bit) bitmap page each
 };
-GPC_HD bool rule_dead(const Img& im, uint32_t rid) { return im.dead && ((im.dead[rid >> 5] >> (rid & 31u)) & 1u); }
+constexpr uint32_t kDeadPageWords = 256, kDeadPageShift = 13;
+GPC_HD bool rule_dead(const Img& im, uint32_t rid) {
+  if (!im.dead) return false;
+  const uint32_t pg = im.dead[rid >> kDeadPageShift];
+  return pg && ((im.dpool[pg + ((rid >> 5) & (kDeadPageWords - 1u))] >> (rid & 31u)) & 1u);
+}
 
-// One published epoch: the base image and, after delta commits, an overlay image holding the
-// current version of every rule changed since the base was built (the base copies are
-// tombstoned). Table verdict = the OVS decision over the union of both rule sets.
+// One published epoch: the base image and, after delta commits, the journal (ovl.blob = journal
+// pool, jhdr = this epoch's JournalHdr word offset in it) holding the current version of every
+// rule changed since the base was built (the base copies are tombstoned). Table verdict = the OVS
+// decision over the union of both rule sets.
 struct View {
   Img base, ovl;
   uint32_t n_img;  // 1 or 2
+  uint32_t jhdr;
 };
+
+// ------------------------------------------------------------------------------ journal
+// Append-only delta store (journal.cpp). Every commit appends, never rewrites, so launches of
+// older epochs keep reading consistent data while a new epoch is written:
+//   rule records   same format as the base image (no point-hash segments), rid = journal id;
+//   entries        8 words {next head word, key value, meta, record offset, prefilter x, y, lo, hi}
+//                  chained per hash bucket (newest first); meta = table | clause << 3 | axis << 5 |
+//                  band << 9 | orid << 11;
+//   head pages     64 head words each, copied on write; a head word = entry offset / 8 | chain
+//                  length (saturating) << 24, 0 = empty;
+//   JournalHdr     per epoch: the page table, both tombstone bitmaps (base rids, journal rids) and
+//                  per table the bucket kinds (axis, band) per driver clause, the always chains and
+//                  the hard pseudo-rule list (rank order).
+struct JournalTable {
+  uint8_t n_kinds[2], pad[2];
+  uint8_t kinds[2][8];     // axis | band << 4
+  uint32_t always[2];      // head word of the clause's always chain
+  uint32_t hard_off, n_hard;
+};
+struct JournalHdr {
+  uint32_t lg;             // 2^lg buckets
+  uint32_t pt_off;         // page table: 2^(lg-8) words, word offset of each head page (0: empty)
+  uint32_t bdead_off;      // base tombstones: page table (0: none), see rule_dead
+  uint32_t odead_off;      // journal tombstones: page table (0: none)
+  JournalTable t[6];
+};
+constexpr uint32_t kJEntWords = 8;
+constexpr uint32_t kJPageHeads = 64;
+GPC_HD uint32_t jkey(uint32_t axis, uint32_t band, uint32_t v) {  // bucket key value of a packet
+  if (axis <= AX_CTDST) return v >> ip_band_shift(band);
+  if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
+  return v;
+}
+GPC_HD uint32_t jmeta(uint32_t table, uint32_t clause, uint32_t axis, uint32_t band) {
+  return table | (clause << 3) | (axis << 5) | (band << 9);
+}
+GPC_HD uint32_t jbucket(uint32_t meta, uint32_t key, uint32_t lg) {
+  return mix32(key ^ mix32(meta * 0x9e3779b1u + 0x7f4a7c15u)) >> (32 - lg);
+}
+GPC_HD uint32_t jhead(const uint32_t* pool, const JournalHdr* jh, uint32_t b) {
+  GPC_TOUCH(pool + jh->pt_off + (b / kJPageHeads), 4);
+  const uint32_t page = pool[jh->pt_off + (b / kJPageHeads)];
+  if (page) GPC_TOUCH(pool + page + (b % kJPageHeads), 4);
+  return page ? pool[page + (b % kJPageHeads)] : 0u;
+}
 
 GPC_HD bool hash_contains(const Img& im, uint64_t key) {
   const uint64_t* tab = reinterpret_cast<const uint64_t*>(im.blob + im.hdr->hash_off);
@@ -606,9 +659,101 @@ GPC_HD TableResult finish_part(const View& v, const TablePart& q) {
   return res;
 }
 
+// The journal's decision for one table: hard pseudo-rules in rank order (as eval_part), then the
+// chains of the driver clause with the shorter total chain length, every live entry whose key and
+// prefilter pass verified; the best completion (priority desc, conj id asc) and whether another
+// completed at its level. Unordered: the journal is small and its records are not in rank order.
+GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
+  const uint32_t* pool = v.ovl.blob;
+  const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + v.jhdr);
+  const JournalTable& jt = jh->t[table - 1];
+  const uint32_t* odead = jh->odead_off ? pool + jh->odead_off : nullptr;
+  Img im{pool, nullptr, odead, pool};
+  TablePart res;
+  res.h = res.s = res.win = 0;
+  uint32_t hprio = 0, hverdict = RV_MISS, htie = 0;
+  bool hfound = false;
+  for (uint32_t h = 0; h < jt.n_hard; h++) {
+    const uint32_t off = pool[jt.hard_off + h];
+    const uint32_t* rec = pool + off;
+    const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
+    if (rule_dead(im, rid)) continue;
+    if (hfound) {
+      if ((w1 & 0xffffu) != hprio) break;
+      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, 0, p)) htie = kHTie;
+      continue;
+    }
+    if (rule_match(im, table, rec, w2, rid, 3, 0, p)) {
+      hfound = true;
+      hprio = w1 & 0xffffu;
+      hverdict = rec_verdict(w2);
+    }
+  }
+  if (hfound) res.h = hprio | (hverdict << 16) | kHFound | htie;
+  uint32_t cnt[2] = {jt.always[0] >> 24, jt.always[1] >> 24};
+  for (uint32_t k = 0; k < 2; k++)
+    for (uint32_t i = 0; i < jt.n_kinds[k]; i++) {
+      const uint32_t axis = jt.kinds[k][i] & 15u, band = jt.kinds[k][i] >> 4;
+      const uint32_t meta = jmeta(table, k, axis, band);
+      cnt[k] += jhead(pool, jh, jbucket(meta, jkey(axis, band, p.ax[axis]), jh->lg)) >> 24;
+    }
+  if (cnt[0] + cnt[1] == 0) return res;
+  const uint32_t d = (jt.n_kinds[1] || jt.always[1]) && cnt[1] < cnt[0] ? 1u : 0u;
+  uint32_t best = 0, best_prio = 0, best_conj = 0, at_best = 0;
+  for (uint32_t i = 0; i <= jt.n_kinds[d]; i++) {
+    uint32_t meta = 0, key = 0, e;
+    if (i == jt.n_kinds[d]) {
+      e = jt.always[d];
+    } else {
+      const uint32_t axis = jt.kinds[d][i] & 15u, band = jt.kinds[d][i] >> 4;
+      meta = jmeta(table, d, axis, band);
+      key = jkey(axis, band, p.ax[axis]);
+      e = jhead(pool, jh, jbucket(meta, key, jh->lg));
+    }
+    const bool always = i == jt.n_kinds[d];
+    while (e & 0xffffffu) {
+      const uint32_t* en = pool + size_t(e & 0xffffffu) * kJEntWords;
+      GPC_TOUCH(en, 4 * kJEntWords);
+      e = en[0];
+      if (!always && (en[1] != key || (en[2] & 0x7ffu) != meta)) continue;
+      if (rule_dead(im, en[2] >> 11)) continue;
+      Ent f;
+      f.x = en[4];
+      f.y = en[5];
+      f.lo = en[6];
+      f.hi = en[7];
+      if (!entry_pass(p, f)) continue;
+      const uint32_t off = en[3];
+      const uint32_t* rec = pool + off;
+      GPC_TOUCH(rec, 4 * kRecHdrWords);
+      const uint32_t w1 = rec[1], w2 = rec[2];
+      const uint32_t prio = w1 & 0xffffu, conj = rec[0];
+      if (best && prio < best_prio) continue;  // cannot change the decision
+      if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, 0, p)) continue;
+      if (!best || prio > best_prio) {
+        best = off;
+        best_prio = prio;
+        best_conj = conj;
+        at_best = 1;
+      } else if (conj != best_conj) {  // same level (the same rule may be listed under several keys)
+        at_best++;
+        if (conj < best_conj) {
+          best = off;
+          best_conj = conj;
+        }
+      }
+    }
+  }
+  if (best) {
+    res.s = best_prio | kSHave | (at_best > 1 ? kSTie : 0u);
+    res.win = best;
+  }
+  return res;
+}
+
 GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
   TablePart acc = eval_part(v.base, table, p);
-  for (uint32_t s = 1; s < v.n_img; s++) acc = combine_parts(v, acc, eval_part(v.ovl, table, p));
+  if (v.n_img > 1) acc = combine_parts(v, acc, eval_journal(v, table, p));
   return finish_part(v, acc);
 }
 

@@ -701,10 +701,9 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
   return emit(G, np, slots, out);
 }
 
-int build_overlay(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, HostImage* out) {
-  PhaseTimer T_;
-  *out = HostImage();
-  Gather G;
+// Rule-centric gather of the current versions of `conj` (uninstalled ones are skipped) plus every
+// hard flow of the tables in `hard_tables` (bit t-1 = table t).
+static int gather_rules(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t hard_tables, Gather* G) {
   int rc = GPC_OK;
   for (uint32_t c : conj) {
     auto it = np.policies().find(c);
@@ -715,22 +714,255 @@ int build_overlay(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>&
         if (kv.second->flow && !rc) {
           auto act = kv.second->actions.find(c);
           if (act != kv.second->actions.end())
-            rc = G.add_soft(*kv.second->flow, c, act->second.clause_id, act->second.n_clause);
+            rc = G->add_soft(*kv.second->flow, c, act->second.clause_id, act->second.n_clause);
         }
     for (auto& f : cj.action_flows)
-      if (!rc) rc = G.add(f);
+      if (!rc) rc = G->add(f);
     for (auto& f : cj.metric_flows)
-      if (!rc) rc = G.add(f);
+      if (!rc) rc = G->add(f);
   }
   for (auto& kv : np.hard_flows())
-    if (!rc && ((hard_tables >> (kv.second.table - 1)) & 1u)) rc = G.add(kv.second);
+    if (!rc && ((hard_tables >> (kv.second.table - 1)) & 1u)) rc = G->add(kv.second);
+  return rc;
+}
+
+// ------------------------------------------------------------------------------------- journal
+namespace {
+
+void set_bit(std::vector<uint32_t>& bm, uint32_t i, std::set<uint32_t>* dirty_pages) {
+  if (bm.size() <= i / 32) bm.resize(i / 32 + 1, 0u);
+  bm[i / 32] |= 1u << (i % 32);
+  dirty_pages->insert(i >> kDeadPageShift);
+}
+
+// Bucket key values an atom covers in the journal (core.hpp jkey); false = always chain.
+bool journal_keys(const AtomKey& k, std::vector<uint32_t>* out) {
+  out->clear();
+  if (k.axis <= AX_CTDST) {
+    const uint32_t sh = ip_band_shift(k.band);
+    if ((uint64_t(k.hi >> sh) - (k.lo >> sh)) >= kMaxBucketsPerAtom) return false;
+    for (uint64_t t = k.lo >> sh; t <= (k.hi >> sh); t++) out->push_back(uint32_t(t));
+  } else if (k.axis == AX_L4D || k.axis == AX_L4S) {
+    const uint32_t a = jkey(k.axis, 0, k.lo), b = jkey(k.axis, 0, k.hi);
+    for (uint32_t t = a; t <= b; t++) out->push_back(t);
+  } else {
+    for (uint64_t v = k.lo; v <= k.hi; v++) out->push_back(uint32_t(v));
+  }
+  return true;
+}
+
+}  // namespace
+
+void Journal::reset(const HostImage* base, uint32_t lg) {
+  base_ = base;
+  lg_ = lg;
+  pool.assign(16, 0u);  // offset 0 is "none"
+  uploaded = 0;
+  hdr_off = 0;
+  n_versions = n_live = 0;
+  any_noact = false;
+  heads_.assign(size_t(1) << lg_, 0u);
+  pt_.assign((size_t(1) << lg_) / kJPageHeads, 0u);
+  bdead_.clear();
+  odead_.clear();
+  bpt_.clear();
+  opt_.clear();
+  bdirty_.clear();
+  odirty_.clear();
+  live_.clear();
+  for (int t = 0; t < 6; t++) {
+    hard_orids_[t].clear();
+    hard_offs_[t].clear();
+  }
+  std::memset(tables_, 0, sizeof tables_);
+}
+
+uint32_t Journal::n_tombstones() const {
+  uint32_t n = 0;
+  for (uint32_t w : bdead_) n += uint32_t(__builtin_popcount(w));
+  for (uint32_t w : odead_) n += uint32_t(__builtin_popcount(w));
+  return n;
+}
+
+uint32_t Journal::append(const uint32_t* w, size_t n, size_t align) {
+  while (pool.size() % align) pool.push_back(0u);
+  const uint32_t off = uint32_t(pool.size());
+  pool.insert(pool.end(), w, w + n);
+  return off;
+}
+
+int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables,
+                   std::string* err) {
+  // 1. tombstones: every earlier copy of a changed rule (base or journal)
+  for (uint32_t c : conj) {
+    auto it = live_.find(c);
+    if (it != live_.end()) {
+      set_bit(odead_, it->second, &odirty_);
+      live_.erase(it);
+      n_live--;
+    }
+    auto b = base_->conj_rid.find(c);
+    if (b != base_->conj_rid.end()) set_bit(bdead_, b->second, &bdirty_);
+  }
+  for (int t = 0; t < 6; t++) {
+    if (!((hard_tables >> t) & 1u)) continue;
+    for (uint32_t o : hard_orids_[t]) set_bit(odead_, o, &odirty_);
+    hard_orids_[t].clear();
+    hard_offs_[t].clear();
+    for (uint32_t rid : base_->hard_rids[t]) set_bit(bdead_, rid, &bdirty_);
+  }
+  // 2. current versions
+  Gather G;
+  int rc = gather_rules(np, conj, hard_tables, &G);
   if (rc) {
-    out->error = G.error;
+    *err = G.error;
     return rc;
   }
-  T_.lap(0);
-  T_.report("overlay gather");  // (lap 0 = the whole gather)
-  return emit(G, np, slots, out);
+  uint64_t span[AX_N];  // interval prefilter choice: price hulls against the whole axis
+  for (int a = 0; a < AX_N; a++) span[a] = 1ull << 32;
+  std::set<uint32_t> dirty_pages;
+  std::vector<uint32_t> keys;
+  for (int t = 1; t <= 6; t++) {
+    std::vector<RuleB*> rs;
+    for (auto& kv : G.soft[t]) {
+      RuleB& r = kv.second;
+      if (!r.prio_set) continue;
+      bool complete = true;
+      for (int k = 0; k < r.n; k++) complete &= !r.clause[k].empty();
+      if (!complete) continue;
+      auto pit = np.policies().find(r.conj_id);
+      r.tier = pit != np.policies().end() ? uint8_t(std::max(0, std::min(255, pit->second->tier))) : 0;
+      const bool is_deny = r.verdict == RV_DROP || r.verdict == RV_REJECT;
+      r.counted = r.has_act && ((r.verdict == RV_ALLOW && G.counted_allow.count(r.conj_id)) ||
+                                (is_deny && G.counted_deny.count(r.conj_id)));
+      if (!r.has_act) {
+        any_noact = true;
+        *err = "rule without an IPv4 conj_id flow";
+        return -GPC_EINVAL;
+      }
+      rs.push_back(&r);
+    }
+    if ((hard_tables >> (t - 1)) & 1u)
+      for (auto& kv : G.hard[t])
+        if (!kv.second.clause[0].empty()) rs.push_back(&kv.second);
+    std::stable_sort(rs.begin(), rs.end(), [](const RuleB* a, const RuleB* b) {  // hard list in rank order
+      if (a->prio != b->prio) return a->prio > b->prio;
+      if (a->hard != b->hard) return a->hard;
+      if (a->hard) return a->verdict < b->verdict;
+      return a->conj_id < b->conj_id;
+    });
+    for (RuleB* rp : rs) {
+      RuleB& r = *rp;
+      if (n_versions >= (1u << 21)) {
+        *err = "journal rule ids exhausted";
+        return -GPC_ENOMEM;
+      }
+      const uint32_t orid = n_versions++;
+      // record: header, clauses, then this record's out-of-line segment data
+      std::vector<uint32_t> rec(kRecHdrWords, 0u), ext;
+      std::vector<std::pair<uint32_t, uint32_t>> patches;  // (record word, ext offset)
+      uint32_t offs[3] = {0, 0, 0};
+      for (int k = 0; k < r.n; k++) {
+        std::vector<PendingSeg> ps;
+        clause_segments(r.clause[k], &ps);
+        for (auto& sg : ps)
+          if (sg.kind == SK_HASH) sg.kind = SK_PTS;  // no point hash in the journal (sorted points)
+        std::vector<std::pair<uint32_t, uint32_t>> cp;
+        std::vector<uint32_t> cw = encode_clause(ps, &ext, &cp);
+        if (rec.size() > 255) {
+          *err = "rule record too large";
+          return -GPC_EINVAL;
+        }
+        offs[k] = uint32_t(rec.size());
+        for (auto& pt : cp) patches.push_back({uint32_t(rec.size()) + pt.first, pt.second});
+        rec.insert(rec.end(), cw.begin(), cw.end());
+      }
+      while (rec.size() % 16) rec.push_back(0u);
+      const uint32_t ext_at = uint32_t(rec.size());
+      rec.insert(rec.end(), ext.begin(), ext.end());
+      while (pool.size() % 16) pool.push_back(0u);
+      const uint32_t base_off = uint32_t(pool.size());
+      for (auto& pt : patches) rec[pt.first] = base_off + ext_at + pt.second;
+      rec[0] = r.hard ? 0u : r.conj_id;
+      rec[1] = uint32_t(r.prio) | (uint32_t(r.act_prio) << 16);
+      rec[2] = (r.verdict & 7u) | ((r.hard ? 1u : 0u) << 3) | ((r.has_act ? 1u : 0u) << 4) | ((r.counted ? 1u : 0u) << 5) |
+               (uint32_t(r.n & 3) << 6) | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
+      rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0u;
+      rec[4] = uint32_t(r.tier) | (orid << 8);
+      rec[5] = 0u;
+      const uint32_t off = append(rec.data(), rec.size(), 16);
+      if (r.hard) {
+        hard_orids_[t - 1].push_back(orid);
+        hard_offs_[t - 1].push_back(off);
+        continue;
+      }
+      live_[r.conj_id] = orid;
+      n_live++;
+      // driver entries for clauses 0 and 1
+      JournalTable& jt = tables_[t - 1];
+      for (int k = 0; k < 2 && k < r.n; k++) {
+        const std::array<uint32_t, 4> pf = entry_of(r, k, 0u, span);
+        for (auto& a : r.clause[k]) {
+          AtomKey key;
+          const bool keyed = atom_key(a, &key) && journal_keys(key, &keys);
+          if (!keyed) {
+            const uint32_t e[kJEntWords] = {jt.always[k], 0u, (orid << 11), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
+            const uint32_t eo = append(e, kJEntWords, kJEntWords);
+            jt.always[k] = (eo / kJEntWords) | (std::min(255u, (jt.always[k] >> 24) + 1u) << 24);
+            continue;
+          }
+          const uint32_t kind = uint32_t(key.axis) | (uint32_t(key.band) << 4);
+          bool have = false;
+          for (uint32_t i = 0; i < jt.n_kinds[k]; i++) have |= jt.kinds[k][i] == kind;
+          if (!have) {
+            if (jt.n_kinds[k] >= 8) {
+              *err = "too many journal bucket kinds";
+              return -GPC_EINVAL;
+            }
+            jt.kinds[k][jt.n_kinds[k]++] = uint8_t(kind);
+          }
+          const uint32_t meta = jmeta(uint32_t(t), uint32_t(k), key.axis, key.band);
+          for (uint32_t kv : keys) {
+            const uint32_t bkt = jbucket(meta, kv, lg_);
+            const uint32_t e[kJEntWords] = {heads_[bkt], kv, meta | (orid << 11), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
+            const uint32_t eo = append(e, kJEntWords, kJEntWords);
+            if (eo / kJEntWords >= (1u << 24)) {
+              *err = "journal pool exceeds 24-bit entry offsets";
+              return -GPC_ENOMEM;
+            }
+            heads_[bkt] = (eo / kJEntWords) | (std::min(255u, (heads_[bkt] >> 24) + 1u) << 24);
+            dirty_pages.insert(bkt / kJPageHeads);
+          }
+        }
+      }
+    }
+  }
+  // 3. copy-on-write head pages, then this epoch's page table, bitmaps and header
+  for (uint32_t pg : dirty_pages) pt_[pg] = append(&heads_[size_t(pg) * kJPageHeads], kJPageHeads, kJPageHeads);
+  JournalHdr h{};
+  h.lg = lg_;
+  h.pt_off = append(pt_.data(), pt_.size(), 16);
+  // tombstone bitmaps: changed 8192-bit pages copied on write, then this epoch's page tables
+  auto publish = [&](std::vector<uint32_t>& bm, std::vector<uint32_t>& pt, std::set<uint32_t>& dirty, uint32_t n_ids) {
+    if (bm.empty()) return 0u;
+    const size_t n_pages = size_t(n_ids >> kDeadPageShift) + 1;
+    if (pt.size() < n_pages) pt.resize(n_pages, 0u);
+    bm.resize(std::max(bm.size(), n_pages * kDeadPageWords), 0u);
+    for (uint32_t pg : dirty) pt[pg] = append(&bm[size_t(pg) * kDeadPageWords], kDeadPageWords, kDeadPageWords);
+    dirty.clear();
+    return append(pt.data(), pt.size(), 16);
+  };
+  h.bdead_off = publish(bdead_, bpt_, bdirty_, base_->n_rids);
+  h.odead_off = publish(odead_, opt_, odirty_, n_versions);
+  for (int t = 0; t < 6; t++) {
+    h.t[t] = tables_[t];
+    if (!hard_offs_[t].empty()) {
+      h.t[t].hard_off = append(hard_offs_[t].data(), hard_offs_[t].size(), 4);
+      h.t[t].n_hard = uint32_t(hard_offs_[t].size());
+    }
+  }
+  hdr_off = append(reinterpret_cast<const uint32_t*>(&h), sizeof h / 4, 16);
+  return GPC_OK;
 }
 
 namespace {

@@ -42,8 +42,31 @@ class SlotMap {
 };
 
 int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out);
-// Delta image of a subset: the rules of `conj` as currently installed (uninstalled ones are
-// skipped) plus every hard pseudo-rule of the tables in `hard_tables` (bit t-1 = table t).
-int build_overlay(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, HostImage* out);
+// Append-only delta store over one base image (core.hpp "journal"). apply() appends the current
+// versions of the changed rules (records, driver-bucket entries, copied-on-write head pages) and a
+// new epoch header with the cumulative tombstones; nothing published earlier is rewritten, so the
+// device only receives pool[uploaded, size). Cost per commit ~ the changed rules, not the journal.
+class Journal {
+ public:
+  void reset(const HostImage* base, uint32_t lg = 16);
+  int apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, std::string* err);
+  bool active() const { return hdr_off != 0; }
+  uint32_t n_tombstones() const;
+  std::vector<uint32_t> pool;  // host mirror of the device pool
+  size_t uploaded = 0;         // words already on the device
+  uint32_t hdr_off = 0;        // JournalHdr of the latest epoch (0: no journal yet)
+  uint32_t n_versions = 0, n_live = 0;
+  bool any_noact = false;
+
+ private:
+  uint32_t append(const uint32_t* w, size_t n, size_t align);
+  const HostImage* base_ = nullptr;
+  uint32_t lg_ = 16;
+  std::vector<uint32_t> heads_, pt_, bdead_, odead_, bpt_, opt_;
+  std::set<uint32_t> bdirty_, odirty_;  // tombstone pages changed since the last epoch
+  std::unordered_map<uint32_t, uint32_t> live_;  // conj -> journal rule id of its live version
+  std::vector<uint32_t> hard_orids_[6], hard_offs_[6];
+  JournalTable tables_[6];
+};
 
 }  // namespace gpc

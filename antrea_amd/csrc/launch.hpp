@@ -7,13 +7,12 @@
 #include "gpc.h"
 
 namespace gpc {
-// Device pointers of one published epoch (core.hpp View): base image + tombstones, optional overlay.
+// Device pointers of one published epoch (core.hpp View): base image, optional journal.
 struct EpochArgs {
   const ImageHdr* hdr;
   const uint32_t* blob;
-  const uint32_t* dead;   // null: no tombstones
-  const ImageHdr* ohdr;   // null: no overlay
-  const uint32_t* oblob;
+  const uint32_t* pool;   // journal pool (null: base image alone)
+  uint32_t jhdr;          // JournalHdr word offset of this epoch
   const uint32_t* svc;    // null: no Services (AntreaProxy stage skipped)
 };
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,

@@ -143,8 +143,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_dump_flows.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]
     lib.gpc_get_image_stats.argtypes = [vp, C.POINTER(gpc_image_stats)]
     lib.gpc_debug_image.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp), C.POINTER(sz)]
-    lib.gpc_debug_epoch.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp),
-                                    C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
+    lib.gpc_debug_epoch.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(C.c_uint32)]
     lib.gpc_load_flows.argtypes = [vp, C.c_char_p, sz, i32, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
     u8p = C.POINTER(C.c_uint8)
     lib.gpc_install_service_group.argtypes = [vp, C.c_uint32, i32, C.POINTER(gpc_endpoint), sz]
@@ -516,16 +515,13 @@ class Classifier:
         return C.cast(b, C.c_void_p).value, n.value, h.value, hb.value
 
     def debug_epoch(self):
-        """(overlay blob pointer or None, overlay hdr pointer or None, dead bitmap pointer or None,
-        dead words) of the current epoch's host shadow."""
-        ob = C.POINTER(C.c_uint32)()
-        on = C.c_size_t()
-        oh = C.c_void_p()
-        d = C.POINTER(C.c_uint32)()
-        dn = C.c_size_t()
-        _check(self.lib.gpc_debug_epoch(self.h, C.byref(ob), C.byref(on), C.byref(oh), C.byref(d), C.byref(dn)),
-               "gpc_debug_epoch")
-        return C.cast(ob, C.c_void_p).value, oh.value, C.cast(d, C.c_void_p).value, dn.value
+        """(journal pool pointer or None, pool words, JournalHdr offset) of the current epoch's host
+        mirror (None / 0 / 0 when the epoch is the base image alone)."""
+        p = C.POINTER(C.c_uint32)()
+        n = C.c_size_t()
+        h = C.c_uint32()
+        _check(self.lib.gpc_debug_epoch(self.h, C.byref(p), C.byref(n), C.byref(h)), "gpc_debug_epoch")
+        return C.cast(p, C.c_void_p).value, n.value, h.value
 
     def image_stats(self) -> dict:
         st = gpc_image_stats()

@@ -279,7 +279,7 @@ def main():
                 "pmc_kb_raw": pmc or None,
                 "bytes_per_packet_alg": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
                 "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
-    cpu = None if args.no_cpu_baseline else _cpu_baseline(wl, args.cpu_seconds)
+    cpu = None if (args.no_cpu_baseline or world > 1) else _cpu_baseline(wl, args.cpu_seconds)  # rank 0, N=1 only
     st = clf.image_stats()
     res = {
         "metric": "Mpps classified (5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW",

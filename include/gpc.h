@@ -264,9 +264,9 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint64_t bytes_entries;        /* driver-index entries (16 B each) incl. always lists        */
   uint64_t bytes_hash;           /* image-wide point hash                                      */
   /* delta epochs (gpc_commit): rules changed since the last full build live in an overlay image */
-  uint64_t overlay_bytes;        /* device bytes of the current overlay (0: none)               */
-  uint32_t n_overlay_rules;      /* rules + hard pseudo-rules in the overlay                   */
-  uint32_t n_tombstones;         /* base rules superseded or removed                           */
+  uint64_t overlay_bytes;        /* journal pool bytes in use (0: base image alone)              */
+  uint32_t n_overlay_rules;      /* live rules in the journal                                  */
+  uint32_t n_tombstones;         /* superseded or removed rule copies (base + journal)         */
   uint64_t n_full_builds, n_delta_builds;
 } gpc_image_stats;
 
@@ -332,10 +332,10 @@ int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed);
 
 /* ---------------------------------------------------------------------------- data path */
 /* Publish the realized flow table to the device atomically (the bundle commit,
- * ofctrl_bridge.go:468-539). Rules whose flows changed since the last full build are rebuilt
- * into a small overlay image and their base copies tombstoned (a delta epoch: cost proportional
- * to the changed rules); when the changed set exceeds max(2048, base rules / 32) the whole image
- * is rebuilt. Launches already queued keep the epoch they were launched with. */
+ * ofctrl_bridge.go:468-539). The rules whose flows changed in this commit are appended to an
+ * append-only journal over the base image and their older copies tombstoned (a delta epoch: cost
+ * proportional to the changed rules); past max(16384, base rules / 4) live journal rules the whole
+ * image is rebuilt. Launches already queued keep the epoch they were launched with. */
 int gpc_commit(gpc_ctx* ctx);
 /* Same, but always rebuilds the whole image (compaction: empties the overlay). */
 int gpc_compact(gpc_ctx* ctx);
@@ -371,9 +371,9 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out);
 int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes);
 /* The host copy of the committed Service image (NULL / 0 when no Services). */
 int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words);
-/* The overlay image and tombstone bitmap of the current epoch (NULL / 0 when absent). */
-int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** overlay_blob, size_t* overlay_words, const void** overlay_hdr,
-                    const uint32_t** dead, size_t* dead_words);
+/* Host mirror of the journal pool and the current epoch's journal header offset (NULL / 0 when
+ * the epoch is the base image alone). */
+int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
 const char* gpc_strerror(int err);
 int gpc_abi_version(void);
 

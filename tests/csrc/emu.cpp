@@ -28,11 +28,15 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
 
 using namespace gpc;
 
-extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_t* oblob, const void* ohdr,
-                            const uint32_t* dead, const uint32_t* svc, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
-                            uint32_t* lb_out, unsigned long long* counters) {
-  View im{{blob, static_cast<const ImageHdr*>(hdr), dead}, {oblob, static_cast<const ImageHdr*>(ohdr), nullptr},
-          oblob ? 2u : 1u};
+extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_t* pool, uint32_t jhdr,
+                            const uint32_t* svc, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, uint32_t* lb_out,
+                            unsigned long long* counters) {
+  View im{{blob, static_cast<const ImageHdr*>(hdr), nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr};
+  if (pool) {
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + jhdr);
+    if (jh->bdead_off) im.base.dead = pool + jh->bdead_off;
+    im.n_img = 2u;
+  }
   for (size_t i = 0; i < n; i++) {
     const uint32_t src = pk->src[i];
     uint32_t dst = pk->dst[i], dport = pk->dport[i];

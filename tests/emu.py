@@ -27,7 +27,7 @@ def load():
     _lib = C.CDLL(LIB)
     _lib.gpc_emu_stats_arr = (C.c_ulonglong * 8).in_dll(_lib, "gpc_emu_stats")
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
-    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+    _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                   C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
     return _lib
 
@@ -38,7 +38,7 @@ def classify(clf: "gpc.Classifier", cols, counters=None, lb=None):
     uint64 array of n_slots x 3 {packets, bytes, sessions} accumulated like the kernel does.
     `lb`: optional gpc.LB_DTYPE array of n entries receiving the Service stage results."""
     blob, nw, hdr, _ = clf.debug_image()
-    oblob, ohdr, dead, _ = clf.debug_epoch()
+    pool, _, jhdr = clf.debug_epoch()
     soa, keep, n = gpc.pkt_soa_host(cols)
     out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
     cptr = None
@@ -50,7 +50,7 @@ def classify(clf: "gpc.Classifier", cols, counters=None, lb=None):
     if lb is not None:
         assert lb.dtype == gpc.LB_DTYPE and len(lb) >= n
         lptr = lb.ctypes.data
-    load().emu_classify(blob, hdr, oblob, ohdr, dead, svc, C.byref(soa), n, out.ctypes.data, lptr, cptr)
+    load().emu_classify(blob, hdr, pool, jhdr, svc, C.byref(soa), n, out.ctypes.data, lptr, cptr)
     return out.reshape(n, 2)
 
 
