@@ -77,6 +77,7 @@ struct RetiredEpoch {
 constexpr size_t kDeltaMinRules = 16384;
 constexpr size_t kDeltaFraction = 4;
 constexpr size_t kPoolWords = size_t(256) << 20;  // 1 GiB journal pool per base (HBM is 288 GB)
+constexpr size_t kMinUploadBytes = size_t(1) << 20;
 
 struct gpc_ctx {
   gpc_config cfg;
@@ -92,6 +93,8 @@ struct gpc_ctx {
   DevEpoch cur;
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
+  void* stage = nullptr;                 // pinned staging buffer of journal uploads
+  size_t stage_bytes = 0;
   unsigned long long* d_counters = nullptr;
   size_t counter_cap = 0;  // slots
   std::vector<uint32_t> released_slots;
@@ -182,6 +185,7 @@ void gpc_destroy(gpc_ctx* ctx) {
       (void)hipStreamSynchronize(ctx->ustream);
       (void)hipStreamDestroy(ctx->ustream);
     }
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
   }
   delete ctx;
 }
@@ -594,9 +598,23 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     ne.pool = ctx->cur.pool;
   }
   Journal& jn = ctx->journal;
-  if (jn.active() && jn.pool.size() > jn.uploaded) {  // append-only: only the new tail travels
-    if (hip_ok(hipMemcpyAsync(ne.pool->d_blob + jn.uploaded, jn.pool.data() + jn.uploaded,
-                              (jn.pool.size() - jn.uploaded) * 4, hipMemcpyHostToDevice, us)))
+  if (jn.active() && jn.pool.size() > jn.uploaded) {
+    // Append-only: only the new tail travels, through a pinned buffer and padded to at least
+    // kMinUploadBytes (the padding lands in not-yet-used pool space) so the runtime takes the DMA
+    // path; a small copy may otherwise run as a blit kernel queued behind in-flight classification.
+    const size_t tail = (jn.pool.size() - jn.uploaded) * 4;
+    const size_t room = ne.pool->bytes - jn.uploaded * 4;
+    const size_t bytes = std::min(std::max(tail, kMinUploadBytes), room);
+    if (ctx->stage_bytes < bytes) {
+      if (ctx->stage) (void)hipHostFree(ctx->stage);
+      ctx->stage = nullptr;
+      ctx->stage_bytes = 0;
+      const size_t cap = std::max(bytes, size_t(4) << 20);
+      if (hip_ok(hipHostMalloc(&ctx->stage, cap, hipHostMallocDefault))) return -GPC_EDEV;
+      ctx->stage_bytes = cap;
+    }
+    std::memcpy(ctx->stage, jn.pool.data() + jn.uploaded, tail);
+    if (hip_ok(hipMemcpyAsync(ne.pool->d_blob + jn.uploaded, ctx->stage, bytes, hipMemcpyHostToDevice, us)))
       return -GPC_EDEV;
     jn.uploaded = jn.pool.size();
   }

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
     if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
     im.n_img = 2u;
   }
-  PacketOut o = classify_packet(im, p, dest);
+  PacketOut o = classify_packet<kDelta>(im, p, dest);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
     count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&counters[w], v); });

@@ -630,7 +630,7 @@ GPC_HD TablePart combine_parts(const View& v, const TablePart& a, TablePart b) {
   return r;
 }
 
-GPC_HD TableResult finish_part(const View& v, const TablePart& q) {
+GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_blob, const TablePart& q) {
   TableResult res;
   res.verdict = RV_MISS;
   res.tie = (q.h & kHTie) ? 1 : 0;
@@ -640,7 +640,7 @@ GPC_HD TableResult finish_part(const View& v, const TablePart& q) {
   res.slot = 0;
   const bool hf = (q.h & kHFound) != 0, have = (q.s & kSHave) != 0;
   if (have && !(q.s & kSNoAct)) {
-    const uint32_t* rec = ((q.s & kSImg) ? v.ovl.blob : v.base.blob) + q.win;
+    const uint32_t* rec = ((q.s & kSImg) ? ovl_blob : base_blob) + q.win;
     const uint32_t w2 = rec[2];
     if (!(hf && (q.h & 0xffffu) > (rec[1] >> 16))) {  // the soft winner's action flow beats the hard match
       res.verdict = uint8_t(rec_verdict(w2));
@@ -751,10 +751,12 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
   return res;
 }
 
+// kJournal = false: the base image alone (the journal code is not instantiated).
+template <bool kJournal>
 GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
   TablePart acc = eval_part(v.base, table, p);
-  if (v.n_img > 1) acc = combine_parts(v, acc, eval_journal(v, table, p));
-  return finish_part(v, acc);
+  if (kJournal && v.n_img > 1) acc = combine_parts(v, acc, eval_journal(v, table, p));
+  return finish_part(v.base.blob, kJournal ? v.ovl.blob : nullptr, acc);
 }
 
 // ------------------------------------------------------------------------------ Service image
@@ -858,6 +860,7 @@ struct PacketOut {
   int ecounted, gcounted;
 };
 
+template <bool kJournal = true>
 GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
   PacketOut o;
   o.e.conj = o.g.conj = 0;
@@ -867,7 +870,7 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
   uint32_t flags = 0, conj = 0, tier = 0;
   uint32_t t = 1;
   while (true) {
-    const TableResult r = eval_table(im, t, p);
+    const TableResult r = eval_table<kJournal>(im, t, p);
     const uint32_t i = t <= 3 ? t - 1 : t - 4;  // position inside the stage
     if (r.tie) flags |= 2;
     uint32_t act = 0, slot = 0;
