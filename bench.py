@@ -201,6 +201,7 @@ def main():
     lat, th = [], None
     if churn:
         import threading
+        sys.setswitchinterval(2e-4)  # the control thread must not wait 5 ms for the GIL behind launches
         stop = threading.Event()
         th = threading.Thread(target=_churn_loop, args=(clf, wl, args.churn_rate, args.max_batch, stop, lat,
                                                         1234 + rank), daemon=True)

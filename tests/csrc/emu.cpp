@@ -14,6 +14,8 @@ static std::vector<uintptr_t> g_lines;
 static std::map<uintptr_t, int> g_line_site;
 extern "C" {
 unsigned long long gpc_emu_site_lines[2048];
+// per packet (first 1M): record verifications and entries scanned (SIMT divergence studies)
+unsigned gpc_emu_pkt_verif[1 << 20], gpc_emu_pkt_scan[1 << 20];
 }
 extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
   uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -60,12 +62,17 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
              pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
     g_lines.clear();
     g_line_site.clear();
+    const unsigned long long v0 = ::gpc_emu_stats[3], s0 = ::gpc_emu_stats[4];
     PacketOut o = classify_packet(im, p, dest);
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;
+    if (i < (1u << 20)) {
+      gpc_emu_pkt_verif[i] = unsigned(::gpc_emu_stats[3] - v0);
+      gpc_emu_pkt_scan[i] = unsigned(::gpc_emu_stats[4] - s0);
+    }
     for (auto& kv : g_line_site) gpc_emu_site_lines[kv.second & 2047]++;                                                              // packets
     uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);
     w[0] = o.e.conj;
