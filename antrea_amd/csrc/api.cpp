@@ -4,7 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -16,6 +20,7 @@
 #include "gpc.h"
 #include "image.hpp"
 #include "launch.hpp"
+#include "oplog.hpp"
 #include "service.hpp"
 
 using namespace gpc;
@@ -79,6 +84,28 @@ constexpr size_t kDeltaFraction = 4;
 constexpr size_t kPoolWords = size_t(256) << 20;  // 1 GiB journal pool per base (HBM is 288 GB)
 constexpr size_t kMinUploadBytes = size_t(1) << 20;
 
+// Background compaction: a shadow compiler replays the control-plane log on its own thread; asked
+// to compact, it builds a full image of its state at a commit boundary, catches up on the log by
+// appending the rules changed meanwhile to a fresh journal (from its own state, no lock on the
+// live compiler), uploads both and hands them over. The next gpc_commit installs them after
+// appending the rules changed since the handover commit (from the live compiler) -- so the
+// synchronous full rebuild is only a fallback when the journal outgrows its hard limit first.
+struct Compactor {
+  std::thread th;
+  std::mutex mu;  // everything below
+  std::condition_variable cv;
+  std::vector<Op> log;       // operations the shadow has not replayed yet
+  bool enabled = true, stop = false, busy = false;
+  uint64_t want_commit = 0;  // compact once the shadow reaches this commit (0: not requested)
+  bool ready = false;        // a result is waiting to be installed
+  int rc = 0;
+  std::unique_ptr<HostImage> base;
+  std::unique_ptr<Journal> journal;
+  std::shared_ptr<DevImage> dbase, dpool;
+  size_t uploaded = 0;
+  uint64_t at_commit = 0;
+};
+
 struct gpc_ctx {
   gpc_config cfg;
   std::mutex ctl;    // control plane (conjMatchFlowLock + replayMutex role)
@@ -99,9 +126,22 @@ struct gpc_ctx {
   size_t counter_cap = 0;  // slots
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
-  uint64_t epoch = 0, n_full = 0, n_delta = 0;
+  uint64_t epoch = 0, n_full = 0, n_delta = 0, n_bg = 0;
+  uint64_t commit_no = 0;                // commits so far (COMMIT markers in the log)
+  bool comp_pending = false;             // a background compaction was requested, not installed yet
+  std::vector<std::pair<uint64_t, FeatureNP::Dirty>> dirty_hist;  // per commit since the request
+  Compactor comp;
   explicit gpc_ctx(const gpc_config& c) : cfg(c), np(c), svc(c) {}
 };
+
+static void log_op(gpc_ctx* ctx, Op&& op) {
+  {
+    std::lock_guard<std::mutex> g(ctx->comp.mu);
+    if (!ctx->comp.enabled) return;
+    ctx->comp.log.push_back(std::move(op));
+  }
+  ctx->comp.cv.notify_one();
+}
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : -GPC_EDEV; }
 
@@ -144,6 +184,117 @@ static void collect_retired(gpc_ctx* ctx, bool wait) {
 
 static int commit_impl(gpc_ctx* ctx, bool force_full);
 
+static void compactor_main(gpc_ctx* ctx) {
+  Compactor& C = ctx->comp;
+  FeatureNP shadow(ctx->cfg);
+  uint64_t shadow_commit = 0;
+  bool at_marker = true;
+  hipStream_t bs = nullptr;
+  const bool dev_ok = hipSetDevice(ctx->cfg.device) == hipSuccess &&
+                      hipStreamCreateWithFlags(&bs, hipStreamNonBlocking) == hipSuccess;
+  if (!dev_ok) (void)hipGetLastError();
+  auto grab = [&](std::vector<Op>* out, bool wait) {  // false: stop requested
+    std::unique_lock<std::mutex> lk(C.mu);
+    if (wait)
+      C.cv.wait_for(lk, std::chrono::milliseconds(50), [&] { return C.stop || !C.log.empty() || C.want_commit; });
+    if (C.stop) return false;
+    out->swap(C.log);
+    return true;
+  };
+  auto replay = [&](std::vector<Op>& ops) {
+    for (auto& op : ops) {
+      try {
+        (void)op.apply(shadow);
+      } catch (...) {
+      }
+      at_marker = op.kind == Op::COMMIT;
+      if (at_marker) shadow_commit = op.commit_no;
+    }
+    size_t n = ops.size();
+    ops.clear();
+    return n;
+  };
+  std::vector<Op> ops;
+  while (grab(&ops, true)) {
+    replay(ops);
+    uint64_t want;
+    {
+      std::lock_guard<std::mutex> g(C.mu);
+      want = C.want_commit;
+      if (want && at_marker && shadow_commit >= want) {
+        C.want_commit = 0;
+        C.busy = true;
+      } else {
+        continue;
+      }
+    }
+    // full image of the shadow's state, then catch up through a fresh journal
+    auto base = std::make_unique<HostImage>();
+    auto jn = std::make_unique<Journal>();
+    int rc = GPC_OK;
+    try {
+      (void)shadow.take_dirty();
+      rc = build_image(shadow, ctx->slots, base.get());
+      jn->reset(base.get());
+      for (int round = 0; rc == GPC_OK && round < 4; round++) {
+        size_t n = 0;
+        do {
+          if (!grab(&ops, n > 0 || !at_marker)) {
+            rc = -GPC_EINVAL;
+            break;
+          }
+          n += replay(ops);
+        } while (!at_marker);
+        if (rc) break;
+        FeatureNP::Dirty d = shadow.take_dirty();
+        std::string err;
+        if ((!d.conj.empty() || d.hard_tables) && jn->apply(shadow, ctx->slots, d.conj, d.hard_tables, &err) != GPC_OK)
+          rc = -GPC_EINVAL;
+        if (n < 256) break;
+      }
+    } catch (...) {
+      rc = -GPC_ENOMEM;
+    }
+    if (const char* d = std::getenv("GPC_TEST_COMPACT_DELAY_MS"))  // tests: widen the handover race window
+      std::this_thread::sleep_for(std::chrono::milliseconds(std::atoi(d)));
+    std::shared_ptr<DevImage> dbase, dpool;
+    size_t up = 0;
+    if (rc == GPC_OK && dev_ok) {
+      auto pool = std::make_shared<DevImage>();
+      pool->s = bs;
+      pool->bytes = kPoolWords * 4;
+      if (upload_image(*base, bs, &dbase) || hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, bs)) ||
+          (jn->active() && hip_ok(hipMemcpyAsync(pool->d_blob, jn->pool.data(), jn->pool.size() * 4,
+                                                 hipMemcpyHostToDevice, bs))) ||
+          hip_ok(hipStreamSynchronize(bs))) {
+        dbase.reset();
+      } else {
+        dpool = std::move(pool);
+        up = jn->active() ? jn->pool.size() : 0;
+      }
+    }
+    std::lock_guard<std::mutex> g(C.mu);
+    C.busy = false;
+    C.ready = true;
+    C.rc = rc;
+    C.base = std::move(base);
+    C.journal = std::move(jn);
+    C.dbase = std::move(dbase);
+    C.dpool = std::move(dpool);
+    C.uploaded = up;
+    C.at_commit = shadow_commit;
+  }
+  {
+    std::lock_guard<std::mutex> g(C.mu);  // results not installed are dropped with the context
+    C.dbase.reset();
+    C.dpool.reset();
+  }
+  if (bs) {
+    (void)hipStreamSynchronize(bs);
+    (void)hipStreamDestroy(bs);
+  }
+}
+
 extern "C" {
 
 int gpc_abi_version(void) { return GPC_ABI_VERSION; }
@@ -167,6 +318,8 @@ int gpc_create(const gpc_config* cfg, gpc_ctx** out) {
   if (!cfg->ipv4_enabled && !cfg->ipv6_enabled) return -GPC_EINVAL;
   try {
     *out = new gpc_ctx(*cfg);
+    if (cfg->compact_after >= 0) (*out)->comp.th = std::thread(compactor_main, *out);
+    else (*out)->comp.enabled = false;
   } catch (...) {
     return -GPC_ENOMEM;
   }
@@ -175,6 +328,12 @@ int gpc_create(const gpc_config* cfg, gpc_ctx** out) {
 
 void gpc_destroy(gpc_ctx* ctx) {
   if (!ctx) return;
+  {
+    std::lock_guard<std::mutex> g(ctx->comp.mu);
+    ctx->comp.stop = true;
+  }
+  ctx->comp.cv.notify_all();
+  if (ctx->comp.th.joinable()) ctx->comp.th.join();
   if (ctx->cur.base || ctx->d_counters || !ctx->retired.empty()) {
     (void)hipSetDevice(ctx->cfg.device);
     (void)hipDeviceSynchronize();
@@ -193,14 +352,23 @@ void gpc_destroy(gpc_ctx* ctx) {
 int gpc_initialize(gpc_ctx* ctx) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  return ctx->np.initialize();
+  int rc = ctx->np.initialize();
+  Op op;
+  op.kind = Op::INIT;
+  log_op(ctx, std::move(op));
+  return rc;
 }
 
 int gpc_install_rule(gpc_ctx* ctx, const gpc_rule* rule) {
   if (!ctx || !rule) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   try {
-    return ctx->np.install_rule(*rule);
+    int rc = ctx->np.install_rule(*rule);
+    Op op;
+    op.kind = Op::INSTALL;
+    op.rules.emplace_back(*rule);
+    log_op(ctx, std::move(op));
+    return rc;
   } catch (...) {
     return -GPC_ENOMEM;
   }
@@ -210,7 +378,13 @@ int gpc_batch_install(gpc_ctx* ctx, const gpc_rule* rules, size_t n) {
   if (!ctx || (!rules && n)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   try {
-    return ctx->np.batch_install(rules, n);
+    int rc = ctx->np.batch_install(rules, n);
+    Op op;
+    op.kind = Op::BATCH;
+    op.rules.reserve(n);
+    for (size_t i = 0; i < n; i++) op.rules.emplace_back(rules[i]);
+    log_op(ctx, std::move(op));
+    return rc;
   } catch (...) {
     return -GPC_ENOMEM;
   }
@@ -221,6 +395,10 @@ int gpc_uninstall_rule(gpc_ctx* ctx, uint32_t rule_id, uint16_t* stale, size_t c
   std::lock_guard<std::mutex> g(ctx->ctl);
   std::vector<uint16_t> st;
   int rc = ctx->np.uninstall_rule(rule_id, &st);
+  Op op;
+  op.kind = Op::UNINSTALL;
+  op.id = rule_id;
+  log_op(ctx, std::move(op));
   if (rc) return rc;
   ctx->slots.release(rule_id, &ctx->released_slots);
   if (n_stale) *n_stale = st.size();
@@ -234,20 +412,47 @@ int gpc_add_rule_addrs(gpc_ctx* ctx, uint32_t rule_id, int32_t addr_type, const 
                        const uint16_t* prio, int32_t enable_logging, int32_t is_mcnp) {
   if (!ctx || (!addrs && n)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  return ctx->np.add_rule_addrs(rule_id, addr_type, addrs, n, prio, enable_logging != 0, is_mcnp != 0);
+  int rc = ctx->np.add_rule_addrs(rule_id, addr_type, addrs, n, prio, enable_logging != 0, is_mcnp != 0);
+  Op op;
+  op.kind = Op::ADD;
+  op.id = rule_id;
+  op.addr_type = addr_type;
+  op.addrs.assign(addrs, addrs + n);
+  op.has_prio = prio != nullptr;
+  op.prio = prio ? *prio : 0;
+  op.logging = enable_logging != 0;
+  op.mcnp = is_mcnp != 0;
+  log_op(ctx, std::move(op));
+  return rc;
 }
 
 int gpc_del_rule_addrs(gpc_ctx* ctx, uint32_t rule_id, int32_t addr_type, const gpc_addr* addrs, size_t n,
                        const uint16_t* prio) {
   if (!ctx || (!addrs && n)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  return ctx->np.del_rule_addrs(rule_id, addr_type, addrs, n, prio);
+  int rc = ctx->np.del_rule_addrs(rule_id, addr_type, addrs, n, prio);
+  Op op;
+  op.kind = Op::DEL;
+  op.id = rule_id;
+  op.addr_type = addr_type;
+  op.addrs.assign(addrs, addrs + n);
+  op.has_prio = prio != nullptr;
+  op.prio = prio ? *prio : 0;
+  log_op(ctx, std::move(op));
+  return rc;
 }
 
 int gpc_reassign_priorities(gpc_ctx* ctx, const uint16_t* from, const uint16_t* to, size_t n, uint8_t table) {
   if (!ctx || ((!from || !to) && n)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  return ctx->np.reassign_priorities(from, to, n, table);
+  int rc = ctx->np.reassign_priorities(from, to, n, table);
+  Op op;
+  op.kind = Op::REASSIGN;
+  op.from.assign(from, from + n);
+  op.to.assign(to, to + n);
+  op.table = table;
+  log_op(ctx, std::move(op));
+  return rc;
 }
 
 int gpc_load_flows(gpc_ctx* ctx, const char* text, size_t len, int32_t replace, size_t* n_loaded, size_t* n_skipped,
@@ -279,6 +484,11 @@ int gpc_load_flows(gpc_ctx* ctx, const char* text, size_t len, int32_t replace, 
   std::lock_guard<std::mutex> g(ctx->ctl);
   try {
     int rc = ctx->np.load_flows(flows, replace != 0);
+    {  // loaded flows always commit as full rebuilds: the shadow compiler is not needed any more
+      std::lock_guard<std::mutex> c(ctx->comp.mu);
+      ctx->comp.enabled = false;
+      ctx->comp.log.clear();
+    }
     if (rc) return rc;
   } catch (...) {
     return -GPC_ENOMEM;
@@ -496,6 +706,7 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   out->n_tombstones = ctx->journal.n_tombstones();
   out->n_full_builds = ctx->n_full;
   out->n_delta_builds = ctx->n_delta;
+  out->n_background_builds = ctx->n_bg;
   for (int i = 0; i < 6; i++) {
     out->n_rules[i] = ctx->last.n_rules[i];
     out->n_hard[i] = ctx->last.n_hard[i];
@@ -547,6 +758,45 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   FeatureNP::Dirty dirty = ctx->np.take_dirty();
+  const uint64_t commit_no = ++ctx->commit_no;
+  {
+    Op m;
+    m.kind = Op::COMMIT;
+    m.commit_no = commit_no;
+    log_op(ctx, std::move(m));
+  }
+  // a background compaction result: install it, then append what changed after its commit
+  bool installed = false;
+  std::shared_ptr<DevImage> bg_base, bg_pool;
+  size_t bg_uploaded = 0;
+  {
+    std::unique_lock<std::mutex> lk(ctx->comp.mu);
+    if (ctx->comp.ready) {
+      ctx->comp.ready = false;
+      ctx->comp_pending = false;
+      if (ctx->comp.rc == GPC_OK && !force_full && !ctx->np.foreign()) {
+        ctx->last = std::move(*ctx->comp.base);
+        ctx->journal = std::move(*ctx->comp.journal);
+        ctx->journal.set_base(&ctx->last);
+        bg_base = std::move(ctx->comp.dbase);
+        bg_pool = std::move(ctx->comp.dpool);
+        bg_uploaded = ctx->comp.uploaded;
+        for (auto& h : ctx->dirty_hist)
+          if (h.first > ctx->comp.at_commit) {
+            dirty.conj.insert(h.second.conj.begin(), h.second.conj.end());
+            dirty.hard_tables |= h.second.hard_tables;
+          }
+        installed = true;
+        ctx->n_bg++;
+      }
+      ctx->comp.base.reset();
+      ctx->comp.journal.reset();
+      ctx->comp.dbase.reset();
+      ctx->comp.dpool.reset();
+      ctx->dirty_hist.clear();
+    }
+  }
+  if (ctx->comp_pending) ctx->dirty_hist.push_back({commit_no, dirty});
   const bool have_base = !ctx->last.blob.empty();
   bool full = force_full || !have_base || ctx->last.any_noact || ctx->np.foreign() || ctx->journal.any_noact ||
               ctx->journal.n_live > std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction) ||
@@ -565,9 +815,24 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       if (rc) return rc;
       ctx->last = std::move(img);
       ctx->journal.reset(&ctx->last);
+      installed = false;
     }
   } catch (...) {
     return -GPC_ENOMEM;
+  }
+  // ask the compactor for a new base once the journal is large; commits continue meanwhile
+  const int32_t ca = ctx->cfg.compact_after;
+  const size_t soft = ca > 0 ? size_t(ca) : std::max<size_t>(2048, ctx->last.conj_rid.size() / 32);
+  if (!full && ca >= 0 && !ctx->comp_pending && ctx->journal.n_live > soft) {
+    {
+      std::lock_guard<std::mutex> c(ctx->comp.mu);
+      if (ctx->comp.enabled && !ctx->comp.busy && !ctx->comp.ready) {
+        ctx->comp.want_commit = commit_no;
+        ctx->comp_pending = true;
+        ctx->dirty_hist.clear();
+      }
+    }
+    ctx->comp.cv.notify_one();
   }
   const bool svc_changed = ctx->svc.generation() != ctx->svc_gen;
   if (svc_changed) {
@@ -585,7 +850,13 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   hipStream_t us = ctx->ustream;
   collect_retired(ctx, false);
   DevEpoch ne;
-  if (full || !ctx->cur.base) {
+  if (installed && bg_base && bg_pool) {  // uploaded by the compactor
+    bg_base->s = us;
+    bg_pool->s = us;
+    ne.base = std::move(bg_base);
+    ne.pool = std::move(bg_pool);
+    ctx->journal.uploaded = bg_uploaded;
+  } else if (full || installed || !ctx->cur.base) {
     if ((rc = upload_image(ctx->last, us, &ne.base))) return rc;
     auto pool = std::make_shared<DevImage>();  // journal pool of the new base
     pool->s = us;

@@ -20,6 +20,7 @@
 namespace gpc {
 
 uint32_t SlotMap::get(uint32_t conj) {
+  std::lock_guard<std::mutex> g(mu_);
   auto it = slot_.find(conj);
   if (it != slot_.end()) return it->second;
   uint32_t s;
@@ -36,6 +37,7 @@ uint32_t SlotMap::get(uint32_t conj) {
 }
 
 void SlotMap::release(uint32_t conj, std::vector<uint32_t>* freed) {
+  std::lock_guard<std::mutex> g(mu_);
   auto it = slot_.find(conj);
   if (it == slot_.end()) return;
   free_.push_back(it->second);

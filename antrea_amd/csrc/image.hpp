@@ -2,6 +2,7 @@
 #pragma once
 
 #include <map>
+#include <mutex>
 #include <set>
 #include <unordered_map>
 #include <string>
@@ -28,14 +29,22 @@ struct HostImage {
 
 // Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
 // rank that applies the same control-plane calls, so slots line up for the RCCL all-reduce).
+// Thread-safe: the background compactor assigns slots too.
 class SlotMap {
  public:
   uint32_t get(uint32_t conj);
   void release(uint32_t conj, std::vector<uint32_t>* freed);
-  uint32_t size() const { return uint32_t(slot_conj_.size()); }
-  const std::vector<uint32_t>& slot_conj() const { return slot_conj_; }
+  uint32_t size() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return uint32_t(slot_conj_.size());
+  }
+  std::vector<uint32_t> slot_conj() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return slot_conj_;
+  }
 
  private:
+  mutable std::mutex mu_;
   std::map<uint32_t, uint32_t> slot_;
   std::vector<uint32_t> slot_conj_;
   std::vector<uint32_t> free_;
@@ -49,6 +58,7 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out);
 class Journal {
  public:
   void reset(const HostImage* base, uint32_t lg = 16);
+  void set_base(const HostImage* base) { base_ = base; }  // the base image object moved
   int apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, std::string* err);
   bool active() const { return hdr_off != 0; }
   uint32_t n_tombstones() const;

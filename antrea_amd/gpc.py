@@ -39,7 +39,7 @@ VTABLE_ENDPOINT_DNAT = 4
 class gpc_config(C.Structure):
     _fields_ = [("ipv4_enabled", C.c_int32), ("ipv6_enabled", C.c_int32), ("enable_antrea_policy", C.c_int32),
                 ("enable_deny_tracking", C.c_int32), ("cookie", C.c_uint64), ("device", C.c_int32),
-                ("reserved", C.c_int32 * 7)]
+                ("compact_after", C.c_int32), ("reserved", C.c_int32 * 6)]
 
 
 class gpc_addr(C.Structure):
@@ -87,7 +87,7 @@ class gpc_image_stats(C.Structure):
                 ("bytes_records", C.c_uint64), ("bytes_ext", C.c_uint64), ("bytes_bucket_offsets", C.c_uint64),
                 ("bytes_entries", C.c_uint64), ("bytes_hash", C.c_uint64), ("overlay_bytes", C.c_uint64),
                 ("n_overlay_rules", C.c_uint32), ("n_tombstones", C.c_uint32), ("n_full_builds", C.c_uint64),
-                ("n_delta_builds", C.c_uint64)]
+                ("n_delta_builds", C.c_uint64), ("n_background_builds", C.c_uint64)]
 
 
 class gpc_endpoint(C.Structure):
@@ -323,11 +323,12 @@ class Classifier:
     """One gpc context (one GPU)."""
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
-                 cookie=0x1020000000000, device=0):
+                 cookie=0x1020000000000, device=0, compact_after=0):
         self.lib = load()
         cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
                          enable_antrea_policy=int(enable_antrea_policy),
-                         enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device)
+                         enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device,
+                         compact_after=int(compact_after))
         h = C.c_void_p()
         _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
         self.h = h
@@ -532,4 +533,4 @@ class Classifier:
                           "entries": st.bytes_entries, "hash": st.bytes_hash},
                 "overlay_bytes": st.overlay_bytes, "n_overlay_rules": st.n_overlay_rules,
                 "n_tombstones": st.n_tombstones, "n_full_builds": st.n_full_builds,
-                "n_delta_builds": st.n_delta_builds}
+                "n_delta_builds": st.n_delta_builds, "n_background_builds": st.n_background_builds}

@@ -120,7 +120,9 @@ typedef struct gpc_config {
   int32_t enable_deny_tracking;
   uint64_t cookie;               /* cookie printed in flow dumps (round<<48 | category<<40)     */
   int32_t device;                /* HIP device ordinal used by this context                    */
-  int32_t reserved[7];
+  int32_t compact_after;         /* live journal rules that start a background compaction
+                                    (0: max(2048, rules / 32); < 0: never in the background)   */
+  int32_t reserved[6];
 } gpc_config;
 
 typedef struct gpc_addr {        /* 24 bytes */
@@ -268,6 +270,7 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint32_t n_overlay_rules;      /* live rules in the journal                                  */
   uint32_t n_tombstones;         /* superseded or removed rule copies (base + journal)         */
   uint64_t n_full_builds, n_delta_builds;
+  uint64_t n_background_builds;  /* full rebuilds done by the background compactor and installed */
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */

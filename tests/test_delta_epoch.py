@@ -1,9 +1,10 @@
-"""Delta epochs: gpc_commit rebuilds only the rules whose flows changed into an
-overlay image and tombstones their base copies. Two product classifiers run the same churn in lock
-step, one publishing delta epochs (gpc_commit) and one rebuilding the whole image every time
-(gpc_compact); the CPU emulation of the kernel body must give identical verdicts and per-rule
-counters for both after every step. The oracle side of the same churn is covered by
-test_churn.py, which also publishes through gpc_commit (delta epochs)."""
+"""Delta epochs: gpc_commit appends the rules whose flows changed to the journal over
+the base image and tombstones their older copies; a background compactor (shadow compiler)
+rebuilds the base. Two product classifiers run the same churn in lock step, one publishing delta
+epochs (gpc_commit) and one rebuilding the whole image every time (gpc_compact); the CPU emulation
+of the kernel body must give identical verdicts and per-rule counters for both after every step.
+The oracle side of the same churn is covered by test_churn.py, which also publishes through
+gpc_commit (delta epochs)."""
 import copy
 
 import numpy as np
@@ -138,3 +139,41 @@ def test_delta_no_change_commit():
     st = a.image_stats()
     assert st["n_full_builds"] == 1 and st["n_delta_builds"] == 1
     assert st["n_overlay_rules"] == 0 and st["n_tombstones"] == 0
+
+
+@pytest.mark.parametrize("delay_ms", [0, 150])
+def test_background_compaction(delay_ms, monkeypatch):
+    """A low compaction threshold makes the shadow compiler rebuild the base in the background while
+    churn continues; after every commit (some of them installing a background result) the verdicts
+    and counters equal a full rebuild of the live state. delay_ms holds the finished result back so
+    that commits land between the compactor's snapshot and the install (the catch-up path)."""
+    import time
+    monkeypatch.setenv("GPC_TEST_COMPACT_DELAY_MS", str(delay_ms))
+    wl = workload.config3(seed=25, n_policies_per_dir=8, rules_per_policy=20)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=25)
+    rng = np.random.default_rng(25)
+    a, b = gpc.Classifier(compact_after=6), gpc.Classifier(compact_after=-1)
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    by_id = {r["flow_id"]: r for r in rules if r.get("from")}
+    ids = sorted(by_id)
+    for step in range(60):
+        rid = int(rng.choice(ids))
+        r = by_id[rid]
+        addrs = [_ip(int(cols["src"][i])) for i in rng.choice(N_PKTS, size=2, replace=False)]
+        for c in (a, b):
+            c.add_policy_rule_address(rid, "src", addrs, r.get("priority"))
+        r["from"].extend(addrs)
+        if step % 7 == 3 and len(r["from"]) > 2:
+            for c in (a, b):
+                c.delete_policy_rule_address(rid, "src", [r["from"][0]], r.get("priority"))
+            del r["from"][0]
+        if step % 10 == 9:
+            time.sleep(0.3 if not delay_ms else 0.05)  # let the compactor work; the next commit installs
+        _compare(a, b, cols, "step %d" % step)
+    st = a.image_stats()
+    assert st["n_background_builds"] >= 1, st
+    assert st["n_full_builds"] == 1, st  # only the initial build ran in the foreground
