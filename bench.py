@@ -236,7 +236,8 @@ def main():
                                     "max": round(float(op_ms.max()), 3) if len(op_ms) else None},
                   "commit_ms": {"p50": pct(commit_ms, 50), "p99": pct(commit_ms, 99)},
                   "overlay_rules_end": st["n_overlay_rules"], "tombstones_end": st["n_tombstones"],
-                  "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"]}
+                  "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"],
+                  "background_builds": st["n_background_builds"]}
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
