@@ -860,7 +860,9 @@ struct PacketOut {
   int ecounted, gcounted;
 };
 
-template <bool kJournal = true>
+// kStage: 0 = both stages; 1 = egress only; 2 = ingress only (the caller has checked that the
+// egress verdict lets the packet reach the ingress tables).
+template <bool kJournal = true, int kStage = 0>
 GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
   PacketOut o;
   o.e.conj = o.g.conj = 0;
@@ -868,7 +870,7 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
   o.eslot = o.gslot = 0;
   o.ecounted = o.gcounted = 0;
   uint32_t flags = 0, conj = 0, tier = 0;
-  uint32_t t = 1;
+  uint32_t t = kStage == 2 ? 4u : 1u;
   while (true) {
     const TableResult r = eval_table<kJournal>(im, t, p);
     const uint32_t i = t <= 3 ? t - 1 : t - 4;  // position inside the stage
@@ -904,6 +906,7 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
     o.e = v;
     o.eslot = slot;
     o.ecounted = counted;
+    if (kStage == 1) break;
     if (act == RV_DROP || act == RV_REJECT || act == RV_ISO_DROP) break;  // ingress never reached (NONE)
     if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
       o.g.packed = RV_BYPASS;
