@@ -858,17 +858,20 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     ctx->journal.uploaded = bg_uploaded;
   } else if (full || installed || !ctx->cur.base) {
     if ((rc = upload_image(ctx->last, us, &ne.base))) return rc;
-    auto pool = std::make_shared<DevImage>();  // journal pool of the new base
-    pool->s = us;
-    pool->bytes = kPoolWords * 4;
-    if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, us))) return -GPC_EDEV;
-    ne.pool = std::move(pool);
-    ctx->journal.uploaded = 0;
+    ctx->journal.uploaded = 0;  // the journal pool of the new base is allocated on first use
   } else {
     ne.base = ctx->cur.base;
     ne.pool = ctx->cur.pool;
   }
   Journal& jn = ctx->journal;
+  if (jn.active() && !ne.pool) {
+    auto pool = std::make_shared<DevImage>();
+    pool->s = us;
+    pool->bytes = kPoolWords * 4;
+    if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, us))) return -GPC_EDEV;
+    ne.pool = std::move(pool);
+    jn.uploaded = 0;
+  }
   if (jn.active() && jn.pool.size() > jn.uploaded) {
     // Append-only: only the new tail travels, through a pinned buffer and padded to at least
     // kMinUploadBytes (the padding lands in not-yet-used pool space) so the runtime takes the DMA

@@ -84,7 +84,7 @@ constexpr int kIdxPerClause = 5;  // sub-indexes (axis, band) per driver clause 
 // are rejected without reading the record.
 //   x  = record offset / 16 << 8 | interval axis << 4 | Bloom axis          (15 = none)
 //   y  = Bloom bits: 0-19 one IP / exact-axis clause on the Bloom axis, 20-31 the service clause
-//        (protocol class x 4096-port block of tp_dst)
+//        (protocol class x tp_dst for single ports, protocol class x 4096-port block for ranges)
 //   lo, hi = hull of the most selective non-driver clause on the interval axis
 // Both tests are necessary conditions of the clauses, so skipping never changes a verdict.
 struct alignas(16) Ent {
@@ -171,13 +171,16 @@ GPC_HD uint32_t proto_class(uint32_t proto) {
   }
 }
 // Bands of the IP axes, by prefix length L: 0 = L 4..12 keyed by the top 12 bits (direct),
-// 1 = L 13..16 by the top 16 (direct), 2 = L 17..24 by a hash of the top 20, 3 = L 25..32 by a
-// hash of the top 28. An atom is listed under every key its prefix covers (at most 2^8, 2^3, 2^3,
-// 2^3 keys); longer prefixes than the key share their key's bucket and are checked on
-// verification. Exact axes (in_port, reg1, reg7, tun) band 0 = low `bits` bits of the value;
-// L4 axes band 0 = proto class x port/8.
-constexpr uint32_t kIpBands = 4;
-GPC_HD uint32_t ip_band_shift(uint32_t band) { return band == 0 ? 20u : band == 1 ? 16u : band == 2 ? 12u : 4u; }
+// 1 = L 13..16 by the top 16 (direct), 2 = L 17..24 by a hash of the top 20, 3 = L 25..31 by a
+// hash of the top 28, 4 = host addresses (L 32) by a hash of the address. An atom is listed under
+// every key its prefix covers (at most 2^8, 2^3, 2^3, 2^3, 1 keys); longer prefixes than the key
+// share their key's bucket and are checked on verification. Host addresses get their own exact
+// band so AddressGroup / Pod members do not share /28 buckets. Exact axes (in_port, reg1, reg7,
+// tun) band 0 = low `bits` bits of the value; L4 axes band 0 = proto class x port/8.
+constexpr uint32_t kIpBands = 5;
+GPC_HD uint32_t ip_band_shift(uint32_t band) {
+  return band == 0 ? 20u : band == 1 ? 16u : band == 2 ? 12u : band == 3 ? 4u : 0u;
+}
 GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t bits, uint32_t v) {
   if (axis <= AX_CTDST) {
     const uint32_t key = v >> ip_band_shift(band);
@@ -201,8 +204,11 @@ constexpr uint32_t kFiltL4All = 0xfff00000u;
 GPC_HD uint32_t filt_ip_bit(uint32_t axis, uint32_t band, uint32_t key) {
   return 1u << uint32_t((uint64_t(mix32(key ^ (axis << 24) ^ (band << 28))) * kFiltIpBits) >> 32);
 }
-GPC_HD uint32_t filt_l4_bit(uint32_t pclass, uint32_t block) {
+GPC_HD uint32_t filt_l4_bit(uint32_t pclass, uint32_t block) {  // a port range: its 4096-port blocks
   return 1u << (kFiltL4Shift + uint32_t((uint64_t(mix32(((pclass << 4) | block) + 0x3c6ef372u)) * kFiltL4Bits) >> 32));
+}
+GPC_HD uint32_t filt_l4x_bit(uint32_t pclass, uint32_t port) {  // a single port (most Services)
+  return 1u << (kFiltL4Shift + uint32_t((uint64_t(mix32(((pclass << 16) | port) ^ 0xa54ff53au)) * kFiltL4Bits) >> 32));
 }
 GPC_HD uint32_t filt_pkt_axis(uint32_t axis, uint32_t v) {
   if (axis <= 3u)
@@ -251,7 +257,7 @@ struct View {
 //   rule records   same format as the base image (no point-hash segments), rid = journal id;
 //   entries        8 words {next head word, key value, meta, record offset, prefilter x, y, lo, hi}
 //                  chained per hash bucket (newest first); meta = table | clause << 3 | axis << 5 |
-//                  band << 9 | orid << 11;
+//                  band << 9 | orid << 12;
 //   head pages     64 head words each, copied on write; a head word = entry offset / 8 | chain
 //                  length (saturating) << 24, 0 = empty;
 //   JournalHdr     per epoch: the page table, both tombstone bitmaps (base rids, journal rids) and
@@ -271,6 +277,7 @@ struct JournalHdr {
   JournalTable t[6];
 };
 constexpr uint32_t kJEntWords = 8;
+constexpr uint32_t kJOridShift = 12, kJMetaMask = (1u << kJOridShift) - 1u;  // meta: 12 bits, orid: 20
 constexpr uint32_t kJPageHeads = 64;
 GPC_HD uint32_t jkey(uint32_t axis, uint32_t band, uint32_t v) {  // bucket key value of a packet
   if (axis <= AX_CTDST) return v >> ip_band_shift(band);
@@ -715,8 +722,8 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
       const uint32_t* en = pool + size_t(e & 0xffffffu) * kJEntWords;
       GPC_TOUCH(en, 4 * kJEntWords);
       e = en[0];
-      if (!always && (en[1] != key || (en[2] & 0x7ffu) != meta)) continue;
-      if (rule_dead(im, en[2] >> 11)) continue;
+      if (!always && (en[1] != key || (en[2] & kJMetaMask) != meta)) continue;
+      if (rule_dead(im, en[2] >> kJOridShift)) continue;
       Ent f;
       f.x = en[4];
       f.y = en[5];
@@ -955,7 +962,8 @@ GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_
   p.ax[AX_CTST] = ct_state;
 #pragma unroll
   for (uint32_t a = 0; a < 8; a++) p.fm[a] = filt_pkt_axis(a, p.ax[a]);
-  p.l4m = filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12);
+  p.l4m = filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12) |
+          filt_l4x_bit(proto_class(proto), p.ax[AX_L4D] & 0xffffu);
 }
 
 }  // namespace gpc

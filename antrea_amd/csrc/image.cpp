@@ -308,7 +308,7 @@ bool atom_key(const Atom& a, AtomKey* k) {
   k->hi = k->lo | ~cov;
   if (pt->axis <= AX_CTDST) {
     if (L < 4) return false;  // /0../3: always list
-    k->band = L <= 12 ? 0 : L <= 16 ? 1 : L <= 24 ? 2 : 3;
+    k->band = L <= 12 ? 0 : L <= 16 ? 1 : L <= 24 ? 2 : L <= 31 ? 3 : 4;
   } else if (pt->axis == AX_L4D || pt->axis == AX_L4S) {
     k->band = 0;
     if ((k->lo >> 16) != (k->hi >> 16)) return false;
@@ -407,6 +407,10 @@ bool filt_clause_l4(const std::vector<Atom>& atoms, uint32_t* bits) {
     uint32_t pm = l4->mask & 0xffffu;
     uint32_t lo = l4->val & pm & 0xffffu, hi = lo | (~pm & 0xffffu);
     if (!is_prefix(l4->mask)) lo = 0, hi = 0xffffu;
+    if (lo == hi) {
+      m |= filt_l4x_bit(pc, lo);
+      continue;
+    }
     for (uint32_t blk = lo >> 12; blk <= (hi >> 12); blk++) m |= filt_l4_bit(pc, blk);
   }
   *bits = m;
@@ -855,7 +859,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     });
     for (RuleB* rp : rs) {
       RuleB& r = *rp;
-      if (n_versions >= (1u << 21)) {
+      if (n_versions >= (1u << (32 - kJOridShift))) {
         *err = "journal rule ids exhausted";
         return -GPC_ENOMEM;
       }
@@ -908,7 +912,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
           AtomKey key;
           const bool keyed = atom_key(a, &key) && journal_keys(key, &keys);
           if (!keyed) {
-            const uint32_t e[kJEntWords] = {jt.always[k], 0u, (orid << 11), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
+            const uint32_t e[kJEntWords] = {jt.always[k], 0u, (orid << kJOridShift), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
             const uint32_t eo = append(e, kJEntWords, kJEntWords);
             jt.always[k] = (eo / kJEntWords) | (std::min(255u, (jt.always[k] >> 24) + 1u) << 24);
             continue;
@@ -926,7 +930,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
           const uint32_t meta = jmeta(uint32_t(t), uint32_t(k), key.axis, key.band);
           for (uint32_t kv : keys) {
             const uint32_t bkt = jbucket(meta, kv, lg_);
-            const uint32_t e[kJEntWords] = {heads_[bkt], kv, meta | (orid << 11), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
+            const uint32_t e[kJEntWords] = {heads_[bkt], kv, meta | (orid << kJOridShift), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
             const uint32_t eo = append(e, kJEntWords, kJEntWords);
             if (eo / kJEntWords >= (1u << 24)) {
               *err = "journal pool exceeds 24-bit entry offsets";
@@ -1111,6 +1115,24 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
           }
           sub[{key.axis, key.band}].push_back({key, ent});
         }
+      }
+      // Host addresses get the exact band only where they dominate the axis (Pod / AddressGroup
+      // members); a few /32 among CIDRs ride in band 3 (/28 keys) and save the packet a lookup.
+      for (uint8_t ax = 0; ax <= AX_CTDST; ax++) {
+        auto h = sub.find({ax, uint8_t(4)});
+        if (h == sub.end()) continue;
+        size_t on_axis = 0;
+        for (uint8_t b = 0; b < kIpBands; b++) {
+          auto it = sub.find({ax, b});
+          if (it != sub.end()) on_axis += it->second.size();
+        }
+        if (h->second.size() * 4 >= on_axis) continue;
+        auto& b3 = sub[{ax, uint8_t(3)}];
+        for (auto& e : h->second) {
+          e.first.band = 3;
+          b3.push_back(e);
+        }
+        sub.erase(h);
       }
       std::vector<std::pair<size_t, std::pair<uint8_t, uint8_t>>> order;
       for (auto& kv : sub) order.push_back({kv.second.size(), kv.first});
