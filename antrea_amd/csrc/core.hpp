@@ -61,7 +61,9 @@ enum Axis : uint8_t {
 //   SK_IVAL  2n words, sorted disjoint [lo,hi]     SK_XIVAL  1 word: offset of the 2n words
 //   SK_PTS   n words, sorted points                SK_XPTS   1 word: offset of the n words
 //   SK_BOX   7n words (val[3], mask[3], axes|nt)   SK_XBOX   1 word: offset of the 7n words
-//   SK_HASH  no data: points live in the image-wide point hash, key (table, clause, axis, rid, v)
+//   SK_HASH  no data: the clause's values on `axis` live in the image-wide point hash, key
+//            (record offset, axis, v) -- clauses that are large sets of exact values (AddressGroup
+//            members, Pod ofports); driver entries probe it during the candidate scan
 //   SK_ALWAYS
 enum SegKind : uint8_t { SK_ALWAYS = 0, SK_IVAL = 1, SK_PTS = 2, SK_HASH = 3, SK_BOX = 4, SK_XIVAL = 5, SK_XPTS = 6, SK_XBOX = 7 };
 enum RuleKind : uint8_t { RK_SOFT = 0, RK_HARD = 1 };
@@ -83,6 +85,9 @@ constexpr int kIdxPerClause = 5;  // sub-indexes (axis, band) per driver clause 
 // Driver-index entry (16 B): a prefilter of the rule's NON-driver clauses, so that most candidates
 // are rejected without reading the record.
 //   x  = record offset / 16 << 8 | interval axis << 4 | Bloom axis          (15 = none)
+//        Bloom axis 8 + a (a < 7): "probe" entry -- the non-driver clause on axis a is an SK_HASH
+//        point set, so the scan probes the point hash for (record, a, packet value) and the
+//        Bloom bits are those of axis a
 //   y  = Bloom bits: 0-19 one IP / exact-axis clause on the Bloom axis, 20-31 the service clause
 //        (protocol class x tp_dst for single ports, protocol class x 4096-port block for ranges)
 //   lo, hi = hull of the most selective non-driver clause on the interval axis
@@ -109,7 +114,7 @@ struct TableHdr {
 
 struct ImageHdr {
   TableHdr t[6];        // AP egress, egress, egress default, AP ingress, ingress, ingress default
-  uint32_t hash_off;    // point hash: 2^hash_log2 buckets x 8 uint64 keys
+  uint32_t hash_off;    // point hash: 2^hash_log2 buckets x kHashSlots uint64 keys (16 B)
   uint32_t hash_log2;
   uint32_t n_slots;
   uint32_t reserved;
@@ -189,10 +194,12 @@ GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t bits, uint32_t 
   if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
   return v & ((1u << bits) - 1u);
 }
-GPC_HD uint64_t point_key(uint32_t table, uint32_t clause, uint32_t axis, uint32_t rid, uint32_t v) {
-  uint32_t hi = (table << 29) | (clause << 27) | (axis << 23) | (rid & 0x7fffffu);
-  return (uint64_t(hi) << 32) | v;
+// Point-hash key of value v on `axis` of the record at word offset `off` (16-word aligned, < 2^28):
+// (off / 16) << 4 | axis in the high word. ~0 (empty slot) is never a key.
+GPC_HD uint64_t point_key(uint32_t off, uint32_t axis, uint32_t v) {
+  return (uint64_t(((off >> 4) << 4) | axis) << 32) | v;
 }
+constexpr uint32_t kHashSlots = 2;  // 16-B buckets, two choices: one 16-B load per choice
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
 GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0x9e3779b97f4a7c15ull) >> 32) & mask; }
 
@@ -297,20 +304,16 @@ GPC_HD uint32_t jhead(const uint32_t* pool, const JournalHdr* jh, uint32_t b) {
   return page ? pool[page + (b % kJPageHeads)] : 0u;
 }
 
+// Both buckets are loaded before either is compared (two independent 16-B loads).
 GPC_HD bool hash_contains(const Img& im, uint64_t key) {
   const uint64_t* tab = reinterpret_cast<const uint64_t*>(im.blob + im.hdr->hash_off);
-  uint32_t mask = (1u << im.hdr->hash_log2) - 1;
-  const uint64_t* b = tab + size_t(hash_b1(key, mask)) * 8;
-  GPC_TOUCH(b, 64);
-  bool hit = false;
-#pragma unroll
-  for (int i = 0; i < 8; i++) hit |= b[i] == key;
-  if (hit) return true;
-  b = tab + size_t(hash_b2(key, mask)) * 8;
-  GPC_TOUCH(b, 64);
-#pragma unroll
-  for (int i = 0; i < 8; i++) hit |= b[i] == key;
-  return hit;
+  const uint32_t mask = (1u << im.hdr->hash_log2) - 1;
+  const uint64_t* b1 = tab + size_t(hash_b1(key, mask)) * kHashSlots;
+  const uint64_t* b2 = tab + size_t(hash_b2(key, mask)) * kHashSlots;
+  GPC_TOUCH(b1, 16);
+  GPC_TOUCH(b2, 16);
+  const uint64_t k0 = b1[0], k1 = b1[1], k2 = b2[0], k3 = b2[1];
+  return (k0 == key) | (k1 == key) | (k2 == key) | (k3 == key);
 }
 
 GPC_HD bool ival_hit(const uint32_t* iv, uint32_t n, uint32_t v) {
@@ -362,8 +365,8 @@ GPC_HD bool box_hit(const uint32_t* bx, uint32_t n, const Pkt& p) {
   return false;
 }
 
-// One clause of the record at `rec` (OR of its segments).
-GPC_HD bool clause_match(const Img& im, uint32_t table, uint32_t k, uint32_t rid, const uint32_t* c, const Pkt& p) {
+// One clause of the record at word offset `roff` (OR of its segments).
+GPC_HD bool clause_match(const Img& im, uint32_t roff, const uint32_t* c, const Pkt& p) {
   GPC_TOUCH(c, 4);
   const uint32_t nseg = c[0];
   const uint32_t* w = c + 1;
@@ -376,7 +379,7 @@ GPC_HD bool clause_match(const Img& im, uint32_t table, uint32_t k, uint32_t rid
       case SK_ALWAYS: return true;
       case SK_IVAL: hit = ival_hit(w, n, p.ax[axis]); w += 2 * n; break;
       case SK_PTS: hit = pts_hit(w, n, p.ax[axis]); w += n; break;
-      case SK_HASH: hit = hash_contains(im, point_key(table, k, axis, rid, p.ax[axis])); break;
+      case SK_HASH: hit = hash_contains(im, point_key(roff, axis, p.ax[axis])); break;
       case SK_BOX: hit = box_hit(w, n, p); w += kBoxWords * n; break;
       case SK_XIVAL: GPC_TOUCH(w, 4); hit = ival_hit(im.blob + *w, n, p.ax[axis]); w++; break;
       case SK_XPTS: GPC_TOUCH(w, 4); hit = pts_hit(im.blob + *w, n, p.ax[axis]); w++; break;
@@ -391,15 +394,15 @@ GPC_HD bool clause_match(const Img& im, uint32_t table, uint32_t k, uint32_t rid
 // All clauses of a record; clause `last` (the driver, already a likely hit) is checked last
 // (last >= n_clauses: natural order). One clause_match call site keeps the code small.
 // `skip`: clauses already decided (the entry's exact interval test).
-GPC_HD bool rule_match(const Img& im, uint32_t table, const uint32_t* rec, uint32_t w2, uint32_t rid, uint32_t last,
-                       uint32_t skip, const Pkt& p) {
+GPC_HD bool rule_match(const Img& im, const uint32_t* rec, uint32_t w2, uint32_t last, uint32_t skip, const Pkt& p) {
+  const uint32_t roff = uint32_t(rec - im.blob);
   const uint32_t ncl = rec_nclauses(w2);
   const uint32_t first = last < ncl ? last + 1 : 0;
   for (uint32_t j = 0; j < ncl; j++) {
     uint32_t k = first + j;
     if (k >= ncl) k -= ncl;
     if ((skip >> k) & 1u) continue;
-    if (!clause_match(im, table, k, rid, rec + rec_off(w2, k), p)) return false;
+    if (!clause_match(im, roff, rec + rec_off(w2, k), p)) return false;
   }
   return true;
 }
@@ -439,10 +442,10 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     if (rule_dead(im, rid)) continue;
     if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
       if ((w1 & 0xffffu) != hprio) break;
-      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, 0, p)) htie = kHTie;
+      if (rec_verdict(w2) != hverdict && rule_match(im, rec, w2, 3, 0, p)) htie = kHTie;
       continue;
     }
-    if (rule_match(im, table, rec, w2, rid, 3, 0, p)) {
+    if (rule_match(im, rec, w2, 3, 0, p)) {
       rH = off;
       hprio = w1 & 0xffffu;
       hverdict = rec_verdict(w2);
@@ -535,11 +538,31 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
         GPC_STAT(4, j < total ? 1 : 0);
         ev[u] = E[idx];
       }
+      bool ps[kScanUnroll];
+      bool probe = false;
 #pragma unroll
       for (int u = 0; u < kScanUnroll; u++) {
-        const Ent& e = ev[u];
-        const uint32_t off = ent_off(e.x);
-        const bool pass = (off > after) & (off < rH) & entry_pass(p, e);
+        const uint32_t off = ent_off(ev[u].x);
+        ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u]);
+        probe |= ps[u] & ((ev[u].x & 15u) - 8u < 7u);
+      }
+      // Probe entries that passed: exact membership of the packet in the non-driver point-set
+      // clause (point hash, both choices loaded before the compare), one entry slot at a time
+      // and only when a lane of the wave needs it.
+      if (GPC_WAVE_ANY(probe)) {
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; u++) {
+          const uint32_t pax = (ev[u].x & 15u) - 8u;
+          const bool need = ps[u] & (pax < 7u);
+          if (GPC_WAVE_ANY(need)) {
+            if (need) ps[u] = hash_contains(im, point_key(ent_off(ev[u].x), pax, p.ax[pax]));
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; u++) {
+        const uint32_t off = ent_off(ev[u].x);
+        const bool pass = ps[u];
         const uint32_t v = pass ? off : 0xffffffffu;
         const bool fresh = (v != 0xffffffffu) & (v != c0) & (v != c1);
         more |= fresh & (c1 != 0xffffffffu);  // a third distinct survivor: one of them is dropped
@@ -570,7 +593,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       if (w2 != 0xffffffffu) continue;
 #endif
       const uint32_t rid = rec[4] >> 8;
-      if (rule_dead(im, rid) || !rule_match(im, table, rec, w2, rid, d, (rec[5] >> (3 * d)) & 7u, p)) {
+      if (rule_dead(im, rid) || !rule_match(im, rec, w2, d, (rec[5] >> (3 * d)) & 7u, p)) {
         GPC_STAT(5, 1);
         continue;
       }
@@ -687,10 +710,10 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
     if (rule_dead(im, rid)) continue;
     if (hfound) {
       if ((w1 & 0xffffu) != hprio) break;
-      if (rec_verdict(w2) != hverdict && rule_match(im, table, rec, w2, rid, 3, 0, p)) htie = kHTie;
+      if (rec_verdict(w2) != hverdict && rule_match(im, rec, w2, 3, 0, p)) htie = kHTie;
       continue;
     }
-    if (rule_match(im, table, rec, w2, rid, 3, 0, p)) {
+    if (rule_match(im, rec, w2, 3, 0, p)) {
       hfound = true;
       hprio = w1 & 0xffffu;
       hverdict = rec_verdict(w2);
@@ -736,7 +759,7 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
       const uint32_t w1 = rec[1], w2 = rec[2];
       const uint32_t prio = w1 & 0xffffu, conj = rec[0];
       if (best && prio < best_prio) continue;  // cannot change the decision
-      if (!rule_match(im, table, rec, w2, rec[4] >> 8, d, 0, p)) continue;
+      if (!rule_match(im, rec, w2, d, 0, p)) continue;
       if (!best || prio > best_prio) {
         best = off;
         best_prio = prio;
@@ -931,12 +954,16 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
 constexpr uint32_t kCounterWords = 3;
 constexpr uint32_t kCounterBytes = kCounterWords * 8;
 
+GPC_HD uint32_t count_session(const VerdictOut& v, uint32_t ct_state) {
+  return ((v.packed & 0xffu) != RV_ALLOW || (ct_state & GPC_CT_NEW)) ? 1u : 0u;
+}
+
 template <typename Add>
 GPC_HD void count_stage(const VerdictOut& v, uint32_t slot, uint32_t len, uint32_t ct_state, Add add) {
   const uint32_t base = kCounterWords * slot;
   add(base, 1ull);
   add(base + 1, (unsigned long long)len);
-  if ((v.packed & 0xffu) != RV_ALLOW || (ct_state & GPC_CT_NEW)) add(base + 2, 1ull);
+  if (count_session(v, ct_state)) add(base + 2, 1ull);
 }
 
 template <typename Add>

@@ -170,7 +170,7 @@ uint8_t action_verdict(const Flow& f, bool* ok) {  // conj_id flows and hard flo
 }
 
 // Segment builder ------------------------------------------------------------------------------
-constexpr uint32_t kHashMinPoints = 64;   // > 64 points: image-wide point hash
+constexpr uint32_t kHashMinPoints = 24;   // > 24 exact values on one axis: image-wide point hash
 constexpr uint32_t kInlinePoints = 16;    // <= 16 points inline in the record
 constexpr uint32_t kInlineIvals = 6;      // <= 6 intervals inline
 constexpr uint32_t kInlineBoxes = 2;
@@ -181,12 +181,42 @@ struct PendingSeg {
   uint32_t n = 0;
 };
 
+// A clause that is a large set of exact values on one axis (AddressGroup members as /32s, Pod
+// ofports): its values go to the point hash (SK_HASH) and driver entries of the rule's other
+// clauses probe it (core.hpp Ent). Axes 0-6 only (the probe marker is Bloom axis 8 + axis).
+bool hash_clause(const std::vector<Atom>& atoms, uint8_t* axis, std::vector<uint32_t>* pts) {
+  if (atoms.size() <= kHashMinPoints) return false;
+  const uint8_t ax = atoms[0].t.empty() ? 0xff : atoms[0].t[0].axis;
+  if (ax > AX_REG7) return false;
+  std::vector<uint32_t> v;
+  v.reserve(atoms.size());
+  for (auto& a : atoms) {
+    if (a.t.size() != 1 || a.t[0].axis != ax || a.t[0].mask != 0xffffffffu) return false;
+    v.push_back(a.t[0].val);
+  }
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  if (v.size() <= kHashMinPoints) return false;
+  *axis = ax;
+  if (pts) *pts = std::move(v);
+  return true;
+}
+
 void clause_segments(const std::vector<Atom>& atoms, std::vector<PendingSeg>* out) {
   for (auto& a : atoms)
     if (a.t.empty()) {
       out->push_back(PendingSeg());  // SK_ALWAYS
       return;
     }
+  {
+    PendingSeg hs;
+    if (hash_clause(atoms, &hs.axis, &hs.data)) {
+      hs.kind = SK_HASH;
+      hs.n = uint32_t(hs.data.size());
+      out->push_back(std::move(hs));
+      return;
+    }
+  }
   std::map<uint8_t, std::vector<std::pair<uint32_t, uint32_t>>> by_axis;
   PendingSeg boxes;
   boxes.kind = SK_BOX;
@@ -223,7 +253,7 @@ void clause_segments(const std::vector<Atom>& atoms, std::vector<PendingSeg>* ou
     ps.axis = kv.first;
     ps.n = uint32_t(merged.size());
     if (points) {
-      ps.kind = merged.size() > kHashMinPoints ? SK_HASH : SK_PTS;
+      ps.kind = SK_PTS;
       for (auto& x : merged) ps.data.push_back(x.first);
     } else {
       ps.kind = SK_IVAL;
@@ -493,11 +523,30 @@ IvalChoice choose_interval(const RuleB& r, int d, const uint64_t* span) {
   return ch;
 }
 
-// Clauses a passing entry of driver d has already decided (record word 5, core.hpp).
+// The non-driver clause driver-d entries probe in the point hash (the largest hash clause), or -1.
+int probe_clause(const RuleB& r, int d, uint8_t* axis) {
+  int best = -1;
+  size_t most = 0;
+  for (int c = 0; c < r.n; c++) {
+    uint8_t ax;
+    uint32_t fax, fbits;
+    if (c == d || r.clause[c].size() <= most || !hash_clause(r.clause[c], &ax, nullptr)) continue;
+    if (!filt_clause_ip(r.clause[c], &fax, &fbits) || fax != ax) continue;
+    best = c;
+    most = r.clause[c].size();
+    *axis = ax;
+  }
+  return best;
+}
+
+// Clauses a passing entry of driver d has already decided (record word 5, core.hpp): the exact
+// interval test, and the probed point-set clause.
 uint32_t skip_mask(const RuleB& r, int d, const uint64_t* span) {
   if (d >= r.n) return 0;
   IvalChoice ch = choose_interval(r, d, span);
-  return ch.exact ? (1u << ch.clause) : 0u;
+  uint8_t pax;
+  const int pc = probe_clause(r, d, &pax);
+  return (ch.exact ? (1u << ch.clause) : 0u) | (pc >= 0 ? (1u << pc) : 0u);
 }
 
 // Driver entry (core.hpp Ent) of rule r for driver clause d at record offset `off`; `span` = value
@@ -505,8 +554,15 @@ uint32_t skip_mask(const RuleB& r, int d, const uint64_t* span) {
 std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint64_t* span) {
   uint32_t axis = kFiltNoAxis, ipbits = 0, l4bits = kFiltL4All;
   bool have_ip = false, have_l4 = false;
+  uint8_t pax;
+  const int pc = probe_clause(r, d, &pax);
+  if (pc >= 0) {
+    filt_clause_ip(r.clause[pc], &axis, &ipbits);
+    axis = 8u + pax;  // probe entry; the Bloom bits are the probed clause's
+    have_ip = true;
+  }
   for (int c = 0; c < r.n; c++) {
-    if (c == d) continue;
+    if (c == d || c == pc) continue;
     uint32_t ax, b;
     if (!have_l4 && filt_clause_l4(r.clause[c], &b)) {
       l4bits = b;
@@ -521,22 +577,25 @@ std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint
   return {((off >> 4) << 8) | (ch.axis << 4) | axis, ipbits | l4bits, ch.lo, ch.hi};
 }
 
+// Point hash (core.hpp hash_contains): 2-choice cuckoo hash of kHashSlots-slot 16-B buckets,
+// sized to <= 70 % load (random-walk insertion; a failed build retries with twice the buckets).
 bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vector<uint64_t>* tab) {
+  constexpr uint32_t S = kHashSlots;
   uint32_t lg = 0;
-  while ((8ull << lg) * 3 / 4 < keys.size() + 1) lg++;
+  while (double(S << lg) * 0.7 < double(keys.size() + 1)) lg++;
   for (int attempt = 0; attempt < 8; attempt++, lg++) {
     uint32_t nb = 1u << lg, mask = nb - 1;
-    tab->assign(size_t(nb) * 8, ~0ull);
+    tab->assign(size_t(nb) * S, ~0ull);
     std::mt19937 rng(1234 + attempt);
     bool ok = true;
     for (uint64_t k : keys) {
       uint64_t cur = k;
       bool placed = false;
-      for (int kick = 0; kick < 500 && !placed; kick++) {
+      for (int kick = 0; kick < 1000 && !placed; kick++) {
         uint32_t bs[2] = {hash_b1(cur, mask), hash_b2(cur, mask)};
         for (uint32_t b : bs) {
-          uint64_t* slot = tab->data() + size_t(b) * 8;
-          for (int i = 0; i < 8; i++)
+          uint64_t* slot = tab->data() + size_t(b) * S;
+          for (uint32_t i = 0; i < S; i++)
             if (slot[i] == ~0ull || slot[i] == cur) {
               slot[i] = cur;
               placed = true;
@@ -546,8 +605,8 @@ bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vect
         }
         if (!placed) {
           uint32_t b = bs[rng() & 1];
-          int i = int(rng() & 7);
-          std::swap(cur, (*tab)[size_t(b) * 8 + i]);
+          uint32_t i = rng() % S;
+          std::swap(cur, (*tab)[size_t(b) * S + i]);
         }
       }
       if (!placed) {
@@ -1043,12 +1102,12 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
       // encode clauses, smallest first in the record
       std::vector<std::vector<uint32_t>> cw(r.n);
       std::vector<std::vector<std::pair<uint32_t, uint32_t>>> cp(r.n);
+      std::vector<PendingSeg> hsegs;  // point-hash segments: keys need the record offset
       for (int k = 0; k < r.n; k++) {
         std::vector<PendingSeg> ps;
         clause_segments(r.clause[k], &ps);
         for (auto& sg : ps)
-          if (sg.kind == SK_HASH)
-            for (uint32_t v : sg.data) hash_keys.push_back(point_key(uint32_t(t), uint32_t(k), sg.axis, rid, v));
+          if (sg.kind == SK_HASH) hsegs.push_back(sg);
         cw[k] = encode_clause(ps, &ext, &cp[k]);
       }
       std::vector<int> order(r.n);
@@ -1080,6 +1139,8 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
         return -GPC_ENOMEM;
       }
       rec_off[rank] = base;
+      for (auto& sg : hsegs)
+        for (uint32_t v : sg.data) hash_keys.push_back(point_key(base, sg.axis, v));
       B.w.insert(B.w.end(), rec.begin(), rec.end());
       if (r.hard) {
         hard_offs.push_back(base);

@@ -74,3 +74,26 @@ def test_emu_vs_c_oracle_full_c3(full_c3):
     got = emu.classify(clf, cols)
     bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
     assert len(bad) == 0, (len(bad), got[bad[0]], want[bad[0]])
+
+
+def test_emu_vs_c_oracle_full_c2():
+    """Full-size C2 (1k rules over AddressGroups of 50-1000 Pod IPs): the group clauses are point
+    sets in the image's point hash and the driver entries probe them during the candidate scan;
+    verdicts equal the C oracle's."""
+    from antrea_amd import gpc
+    from tests import emu
+    wl = workload.config2()
+    clf = gpc.Classifier()
+    clf.initialize()
+    clf.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in wl.rules}
+    pipe = CPipeline(clf.dump_flows(), tiers)
+    emu.commit_host(clf)
+    assert clf.image_stats()["bytes"]["hash"] > 1 << 20  # the group clauses did go to the point hash
+    n = 20000
+    cols = workload.gen_packets(wl, n, seed=78)
+    want = pipe.classify(cols, threads=8)
+    got = emu.classify(clf, cols)
+    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+    assert len(bad) == 0, (len(bad), got[bad[0]], want[bad[0]])
+    assert (got["action"] == ACT["ALLOW"]).sum() > n // 50
