@@ -58,6 +58,8 @@ struct DevEpoch {
   std::shared_ptr<DevImage> pool;       // journal pool of that base (d_hdr unused; append-only)
   uint32_t jhdr = 0;                    // this epoch's JournalHdr in the pool (0: base only)
   std::shared_ptr<DevImage> svc;        // Service image (d_hdr unused), shared until Services change
+  std::shared_ptr<DevImage> v6;         // IPv6 image (ipv6_enabled), shared until rules change
+  uint32_t v6_lpm = 0;                  // its ImageHdr.v6_lpm
   uint64_t epoch = 0;
   std::map<hipStream_t, hipEvent_t> last_use;  // last launch on each stream that used this epoch
 };
@@ -116,6 +118,7 @@ struct gpc_ctx {
   uint64_t svc_gen = ~0ull;              // FeatureService generation the image was built from
   SlotMap slots;
   HostImage last;    // base image of the current epoch: shadow state for re-upload + debug export
+  HostImage last6;   // IPv6 image (ipv6_enabled): rebuilt in full by every commit that changes rules
   Journal journal;   // delta epochs over `last` (host mirror of the device pool)
   DevEpoch cur;
   std::vector<RetiredEpoch> retired;
@@ -605,6 +608,65 @@ int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict
   return gpc_classify_host_lb(ctx, pk, n, out, nullptr, count);
 }
 
+int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
+  if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
+  if (n && (!pk->src6 || !pk->dst6 || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
+  for (const void* c : {(const void*)pk->src6, (const void*)pk->dst6, (const void*)pk->ct_src6, (const void*)pk->ct_dst6})
+    if (reinterpret_cast<uintptr_t>(c) % 16) return -GPC_EINVAL;  // one 128-bit load per address
+  std::lock_guard<std::mutex> d(ctx->data);
+  if (!ctx->cur.v6) return -GPC_EINVAL;  // IPv6 disabled or nothing committed yet
+  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm};
+  hipStream_t st = (hipStream_t)stream;
+  int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, st);
+  if (rc || n == 0) return rc;
+  hipEvent_t& ev = ctx->cur.last_use[st];
+  if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
+  return hip_ok(hipEventRecord(ev, st));
+}
+
+int gpc_classify6_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count) {
+  if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
+  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  if (n == 0) return GPC_OK;
+  gpc_pkt_soa d{};
+  std::vector<void*> allocs;
+  int rc = GPC_OK;
+  auto up = [&](const void* h, size_t elem, const void** dst) {
+    if (!h || rc) return;
+    void* p = nullptr;
+    if (hip_ok(hipMalloc(&p, n * elem)) || hip_ok(hipMemcpy(p, h, n * elem, hipMemcpyHostToDevice))) {
+      rc = -GPC_EDEV;
+      if (p) (void)hipFree(p);
+      return;
+    }
+    allocs.push_back(p);
+    *dst = p;
+  };
+  up(pk->src6, 16, (const void**)&d.src6);
+  up(pk->dst6, 16, (const void**)&d.dst6);
+  up(pk->ct_src6, 16, (const void**)&d.ct_src6);
+  up(pk->ct_dst6, 16, (const void**)&d.ct_dst6);
+  up(pk->sport, 2, (const void**)&d.sport);
+  up(pk->dport, 2, (const void**)&d.dport);
+  up(pk->proto, 1, (const void**)&d.proto);
+  up(pk->out_port, 4, (const void**)&d.out_port);
+  up(pk->in_port, 4, (const void**)&d.in_port);
+  up(pk->svc_group, 4, (const void**)&d.svc_group);
+  up(pk->tun_id, 4, (const void**)&d.tun_id);
+  up(pk->ct_state, 1, (const void**)&d.ct_state);
+  up(pk->dest, 1, (const void**)&d.dest);
+  up(pk->len, 2, (const void**)&d.len);
+  void* dout = nullptr;
+  if (!rc && hip_ok(hipMalloc(&dout, n * 2 * sizeof(gpc_verdict)))) rc = -GPC_EDEV;
+  if (!rc) rc = gpc_classify6(ctx, &d, n, (gpc_verdict*)dout, count, nullptr);
+  if (!rc && hip_ok(hipDeviceSynchronize())) rc = -GPC_EDEV;
+  if (!rc && hip_ok(hipMemcpy(out, dout, n * 2 * sizeof(gpc_verdict), hipMemcpyDeviceToHost))) rc = -GPC_EDEV;
+  if (dout) (void)hipFree(dout);
+  for (void* p : allocs) (void)hipFree(p);
+  return rc;
+}
+
 int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
                          int32_t count) {
   if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
@@ -731,6 +793,17 @@ int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const 
   return GPC_OK;
 }
 
+int gpc_debug_image6(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  const bool has = !ctx->last6.blob.empty();
+  if (blob) *blob = has ? ctx->last6.blob.data() : nullptr;
+  if (n_words) *n_words = ctx->last6.blob.size();
+  if (hdr) *hdr = has ? &ctx->last6.hdr : nullptr;
+  if (hdr_bytes) *hdr_bytes = sizeof(ImageHdr);
+  return GPC_OK;
+}
+
 int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
@@ -834,6 +907,23 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     }
     ctx->comp.cv.notify_one();
   }
+  const bool v6_changed = ctx->cfg.ipv6_enabled &&
+                          (full || installed || !dirty.conj.empty() || dirty.hard_tables || ctx->last6.blob.empty());
+  if (v6_changed) {  // an IPv6 rule set the image cannot take leaves IPv6 unpublished, not IPv4
+    HostImage img6;
+    int r6;
+    try {
+      r6 = build_image6(ctx->np, ctx->slots, &img6);
+    } catch (...) {
+      r6 = -GPC_ENOMEM;
+    }
+    if (r6) {
+      std::string e = img6.error.empty() ? "IPv6 image build failed" : img6.error;
+      img6 = HostImage();
+      img6.error = e;
+    }
+    ctx->last6 = std::move(img6);
+  }
   const bool svc_changed = ctx->svc.generation() != ctx->svc_gen;
   if (svc_changed) {
     std::string err;
@@ -893,6 +983,13 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     jn.uploaded = jn.pool.size();
   }
   ne.jhdr = jn.active() ? jn.hdr_off : 0;
+  if (!v6_changed) {
+    ne.v6 = ctx->cur.v6;
+    ne.v6_lpm = ctx->cur.v6_lpm;
+  } else if (!ctx->last6.blob.empty()) {
+    if ((rc = upload_image(ctx->last6, us, &ne.v6))) return rc;
+    ne.v6_lpm = ctx->last6.hdr.v6_lpm;
+  }
   if (!svc_changed) ne.svc = ctx->cur.svc;
   else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, us, &ne.svc))) return rc;
   ne.epoch = ++ctx->epoch;

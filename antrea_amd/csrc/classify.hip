@@ -27,20 +27,38 @@ constexpr int kBlock = GPC_BLOCK;
 // stage, measured 8 % faster on C3 than one launch walking both stages (kStage = 0; lanes leave the
 // egress stage at different times). With Services one launch (0) does both stages: a second
 // launch would have to repeat the Service lookup, which costs more than the split saves (C4).
-template <bool kDelta, bool kSvc, int kStage>
+// IPv6 address column (16 network-order bytes per packet, 16-B aligned) -> the address's code in
+// the IPv6 image (core.hpp v6_code): one coalesced 128-bit load, byte swaps, longest-prefix match.
+__device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_t* col, uint64_t i) {
+  const uint4 v = reinterpret_cast<const uint4*>(col)[i];
+  const uint32_t a[4] = {__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z), __builtin_bswap32(v.w)};
+  return v6_code(ep.blob, ep.v6_lpm, a);
+}
+
+// kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
+template <bool kDelta, bool kSvc, int kStage, bool kV6 = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count) {
   uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= n) return;
-  const uint32_t src = pk.src[i];
-  uint32_t dst = pk.dst[i], dport = pk.dport[i];
+  uint32_t src, dst, ct_src, ct_dst;
+  if (kV6) {
+    src = v6_code_at(ep, pk.src6, i);
+    dst = v6_code_at(ep, pk.dst6, i);
+    ct_src = pk.ct_src6 ? v6_code_at(ep, pk.ct_src6, i) : src;
+    ct_dst = pk.ct_dst6 ? v6_code_at(ep, pk.ct_dst6, i) : dst;
+  } else {
+    src = pk.src[i];
+    dst = pk.dst[i];
+    ct_src = pk.ct_src ? pk.ct_src[i] : src;
+    ct_dst = pk.ct_dst ? pk.ct_dst[i] : dst;  // pre-NAT destination
+  }
+  uint32_t dport = pk.dport[i];
   const uint32_t sport = pk.sport[i], proto = pk.proto[i];
   uint32_t out_port = pk.out_port[i];
   uint32_t svc_group = pk.svc_group ? pk.svc_group[i] : 0u;
   uint32_t dest = pk.dest ? pk.dest[i] : 0u;
-  const uint32_t ct_src = pk.ct_src ? pk.ct_src[i] : src;
-  const uint32_t ct_dst = pk.ct_dst ? pk.ct_dst[i] : dst;  // pre-NAT destination
   if (kSvc) {  // both launches derive the same Endpoint (the selection is a pure function of the packet)
     uint32_t lb[4];
     const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
@@ -94,6 +112,18 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
                      reinterpret_cast<uint4*>(out), lb_out, counters, count);
   hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
                      reinterpret_cast<uint4*>(out), lb_out, counters, count);
+}
+
+int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
+                     unsigned long long* counters, int count, hipStream_t stream) {
+  if (n == 0) return 0;
+  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 0xffffffffull) return -GPC_EINVAL;
+  hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count);
+  hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count);
+  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,

@@ -117,7 +117,7 @@ struct ImageHdr {
   uint32_t hash_off;    // point hash: 2^hash_log2 buckets x kHashSlots uint64 keys (16 B)
   uint32_t hash_log2;
   uint32_t n_slots;
-  uint32_t reserved;
+  uint32_t v6_lpm;      // IPv6 image: word offset of its V6Lpm block (0 in IPv4 images)
 };
 
 struct Pkt {
@@ -234,6 +234,61 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 #define GPC_STAT(i, v) ((void)0)
 #define GPC_TOUCH(p, n) ((void)0)
 #endif
+
+// ------------------------------------------------------------------------------ IPv6 interning
+// An IPv6 image is an ordinary image over 32-bit *codes* of the IPv6 address axes. Every IPv6
+// prefix of the rule set (ipv6_src / ipv6_dst / ct_ipv6_* matches) is a node of the prefix tree
+// (prefixes are nested or disjoint); node codes are 32-bit prefixes: the children of a node with
+// code c/l get c.i/(l + w), w = ceil(log2(m + 1)) bits for m children (i = 1..m; 0 = "in the
+// node, in none of its children"), or ceil(log2 m) with i = 0..m-1 when the children tile the
+// node. Then "a in P" <=> "code(a) in code(P)", where code(a) = code of the deepest prefix holding
+// a (its longest matching prefix) padded with zeros, so the flows keep their prefix shape and the
+// whole IPv4 machinery (bands, Bloom bits, intervals) applies unchanged. code(a) is found on the
+// device by a longest-prefix match: one hash probe per distinct prefix length, longest first.
+constexpr uint32_t kV6MaxLens = 64;
+struct V6Lpm {
+  uint32_t hash_off, hash_log2, n_lens, reserved;
+  uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), descending
+};
+// hash slot (8 words): masked address (4 words, most significant first), len | kV6Valid, code, 2 pad;
+// bucket = 2 slots (one 64-B line), two choices
+constexpr uint32_t kV6SlotWords = 8, kV6BucketSlots = 2, kV6Valid = 0x100u;
+GPC_HD void v6_mask(const uint32_t* a, uint32_t len, uint32_t* m) {
+  for (int w = 0; w < 4; w++) {
+    const int bits = int(len) - 32 * w;
+    m[w] = bits >= 32 ? a[w] : bits <= 0 ? 0u : (a[w] & ~((1u << (32 - bits)) - 1u));
+  }
+}
+GPC_HD uint64_t v6_hkey(const uint32_t* m, uint32_t len) {
+  const uint64_t h = mix64(((uint64_t(m[0]) << 32) | m[1]) ^ (uint64_t(len + 1) * 0x9e3779b97f4a7c15ull));
+  return mix64(h ^ ((uint64_t(m[2]) << 32) | m[3]));
+}
+// code(a) for the address words a[0..3] (a[0] = most significant).
+GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a) {
+  const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
+  const uint32_t mask = (1u << L->hash_log2) - 1u;
+  for (uint32_t i = 0; i < L->n_lens; i++) {
+    const uint32_t len = L->lens[i];
+    uint32_t m[4];
+    v6_mask(a, len, m);
+    const uint64_t hk = v6_hkey(m, len);
+    const uint32_t* b1 = blob + L->hash_off + size_t(hash_b1(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
+    const uint32_t* b2 = blob + L->hash_off + size_t(hash_b2(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
+    GPC_TOUCH(b1, 64);
+    GPC_TOUCH(b2, 64);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t* w = (c < 2 ? b1 : b2) + (c & 1) * kV6SlotWords;
+      if (w[4] == (len | kV6Valid) && w[0] == m[0] && w[1] == m[1] && w[2] == m[2] && w[3] == m[3]) return w[5];
+    }
+  }
+  return 0u;
+}
+// 16 network-order bytes -> 4 host words, most significant first.
+GPC_HD void v6_words(const uint8_t* p, uint32_t* a) {
+  for (int w = 0; w < 4; w++)
+    a[w] = (uint32_t(p[4 * w]) << 24) | (uint32_t(p[4 * w + 1]) << 16) | (uint32_t(p[4 * w + 2]) << 8) | p[4 * w + 3];
+}
 
 struct Img {
   const uint32_t* blob;
@@ -410,6 +465,7 @@ GPC_HD bool rule_match(const Img& im, const uint32_t* rec, uint32_t w2, uint32_t
 GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
   const uint32_t bax = e.x & 15u, iax = (e.x >> 4) & 15u;
   const bool l4 = (e.y & p.l4m) != 0u;
+  // Bloom axis < 8: IP / exact-axis bits; 8..14 (probe entry): second service Bloom; 15: none
   const bool bl = (bax == kFiltNoAxis) | ((e.y & p.fm[bax & 7u]) != 0u);
   const uint32_t v = p.ax[iax < AX_N ? iax : 0];
   const bool iv = (iax == kFiltNoAxis) | ((e.lo <= v) & (v <= e.hi));

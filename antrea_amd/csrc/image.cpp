@@ -15,7 +15,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <queue>
 #include <set>
+#include <tuple>
 
 namespace gpc {
 
@@ -78,13 +80,175 @@ inline int leading_ones(uint32_t m) {
   return n;
 }
 
-// Flow match -> atom over the IPv4 packet axes. Returns 0 ok, 1 never matches IPv4, -1 unsupported.
-int atom_of(const Match& m, Atom* a) {
+// IPv6 interning (core.hpp "IPv6 interning"): the prefix tree of every IPv6 prefix the realized
+// flows match on, each node's 32-bit code prefix, and the device LPM table that maps an address to
+// the code of its deepest prefix.
+using u128 = unsigned __int128;
+inline u128 v6_value(const IPAddr& a) {
+  u128 v = 0;
+  for (int i = 0; i < 16; i++) v = (v << 8) | a.b[i];
+  return v;
+}
+inline u128 v6_prefix_mask(int len) { return len <= 0 ? u128(0) : len >= 128 ? ~u128(0) : ~((u128(1) << (128 - len)) - 1); }
+
+class V6Codes {
+ public:
+  struct Node {
+    u128 v;
+    int len;
+    uint32_t code = 0;
+    int clen = 0;
+    std::vector<int> kids;
+  };
+  std::vector<Node> nodes;  // nodes[0] = ::/0
+  int max_clen = 0;
+
+  int build(const FeatureNP& np, std::string* err) {
+    std::vector<std::pair<u128, int>> pf;
+    auto take = [&](const IPMatch& f) {
+      if (!f.set || f.addr.fam != 6) return;
+      const int len = f.plen < 0 ? 128 : f.plen;
+      if (len > 0) pf.push_back({v6_value(f.addr) & v6_prefix_mask(len), len});
+    };
+    for (auto& kv : np.installed()) {
+      const Flow& f = kv.second;
+      if (f.table < TB_AP_EGRESS || f.table > TB_INGRESS_DEFAULT) continue;
+      take(f.m.nw_src);
+      take(f.m.nw_dst);
+      take(f.m.ct_nw_src);
+      take(f.m.ct_nw_dst);
+    }
+    std::sort(pf.begin(), pf.end());  // parents (shorter, same start) before children
+    pf.erase(std::unique(pf.begin(), pf.end()), pf.end());
+    nodes.assign(1, Node{0, 0});
+    index_.clear();
+    std::vector<int> st{0};
+    for (auto& p : pf) {
+      while (st.size() > 1) {
+        const Node& t = nodes[st.back()];
+        if (p.second > t.len && (p.first & v6_prefix_mask(t.len)) == t.v) break;
+        st.pop_back();
+      }
+      const int id = int(nodes.size());
+      nodes.push_back(Node{p.first, p.second});
+      nodes[st.back()].kids.push_back(id);
+      st.push_back(id);
+      index_[{p.first, p.second}] = id;
+    }
+    // Codes. The children of a node (plus a "none of them" leaf unless they tile the node) get a
+    // prefix-free code built like a minimax Huffman tree: merge the two leaves / subtrees needing
+    // the fewest bits below them, repeatedly (optimal for the deepest code). Codes need not keep
+    // address order -- only containment along tree paths matters -- but the "none" leaf must be
+    // the all-zero path: addresses in no child keep the node's code padded with zeros.
+    const size_t nn = nodes.size();
+    std::vector<int> req(nn, 0);
+    for (size_t n = nn; n-- > 0;) {
+      std::vector<MergeNode> mt;
+      req[n] = merge_children(n, req, &mt);
+    }
+    if (req[0] > 32) {
+      *err = "IPv6 prefix set needs more than 32 code bits";
+      return -GPC_EINVAL;
+    }
+    for (size_t n = 0; n < nn; n++) {
+      const Node& N = nodes[n];
+      if (N.kids.empty()) continue;
+      std::vector<MergeNode> mt;
+      merge_children(n, req, &mt);
+      std::vector<std::tuple<int, uint32_t, int>> st{{int(mt.size()) - 1, 0u, 0}};  // (merge node, path, depth)
+      while (!st.empty()) {
+        auto [m, path, depth] = st.back();
+        st.pop_back();
+        const MergeNode& M = mt[size_t(m)];
+        if (M.leaf == kInternal) {
+          int zero = M.a, one = M.b;
+          if (mt[size_t(one)].has_none) std::swap(zero, one);
+          st.push_back({zero, path << 1, depth + 1});
+          st.push_back({one, (path << 1) | 1u, depth + 1});
+        } else if (M.leaf != kNone) {
+          Node& K = nodes[size_t(M.leaf)];
+          K.clen = N.clen + depth;
+          K.code = N.code | (depth ? path << (32 - K.clen) : 0u);
+          max_clen = std::max(max_clen, K.clen);
+        }
+      }
+    }
+    return GPC_OK;
+  }
+  static constexpr int kInternal = -1, kNone = -2;
+  struct MergeNode {
+    int leaf;      // child node id, kNone, or kInternal
+    int a, b;      // merged subtrees (internal)
+    bool has_none;
+  };
+  // Minimax merge of node n's children (+ the none leaf); returns the bits the node needs below
+  // its own code; *mt ends with the merge tree's root.
+  int merge_children(size_t n, const std::vector<int>& req, std::vector<MergeNode>* mt) const {
+    const Node& N = nodes[n];
+    if (N.kids.empty()) return 0;
+    bool tiles = false;
+    if (N.len > 0) {
+      u128 sum = 0;
+      for (int k : N.kids) sum += u128(1) << (128 - nodes[size_t(k)].len);
+      tiles = sum == (u128(1) << (128 - N.len));
+    }
+    using E = std::tuple<int, int, int>;  // (bits needed, sequence, merge node)
+    std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+    int seq = 0;
+    for (int k : N.kids) {
+      mt->push_back({k, 0, 0, false});
+      pq.push({req[size_t(k)], seq++, int(mt->size()) - 1});
+    }
+    if (!tiles) {
+      mt->push_back({kNone, 0, 0, true});
+      pq.push({0, seq++, int(mt->size()) - 1});
+    }
+    while (pq.size() > 1) {
+      E x = pq.top();
+      pq.pop();
+      E y = pq.top();
+      pq.pop();
+      const int a = std::get<2>(x), b = std::get<2>(y);
+      mt->push_back({kInternal, a, b, (*mt)[size_t(a)].has_none || (*mt)[size_t(b)].has_none});
+      pq.push({std::max(std::get<0>(x), std::get<0>(y)) + 1, seq++, int(mt->size()) - 1});
+    }
+    return std::get<0>(pq.top());
+  }
+
+  // code prefix of the flow prefix (a, len): false if unknown (not collected)
+  bool term(const IPAddr& a, int len, uint32_t* val, uint32_t* mask) const {
+    if (len <= 0) {
+      *val = *mask = 0;
+      return true;
+    }
+    auto it = index_.find({v6_value(a) & v6_prefix_mask(len), len});
+    if (it == index_.end()) return false;
+    const Node& N = nodes[it->second];
+    // a leaf prefix (no prefix below it): every address in it has exactly the code N.code, so
+    // the term is an exact value (host addresses stay points: exact band, point hash)
+    *mask = N.kids.empty() ? 0xffffffffu : prefix_mask(N.clen);
+    *val = N.code & *mask;
+    return true;
+  }
+
+ private:
+  std::map<std::pair<u128, int>, int> index_;
+};
+
+// Flow match -> atom over the packet axes of a `fam` image (IPv6: addresses as V6Codes codes).
+// Returns 0 ok, 1 never matches a packet of that family, -1 unsupported.
+int atom_of(const Match& m, Atom* a, int fam = 4, const V6Codes* codes = nullptr) {
   a->t.clear();
-  if (m.has_dl && m.dl_type != kEthIP) return 1;
+  if (m.has_dl && m.dl_type != (fam == 4 ? kEthIP : kEthIPv6)) return 1;
   auto ip = [&](const IPMatch& f, uint8_t axis) -> int {
     if (!f.set) return 0;
-    if (f.addr.fam != 4) return 1;
+    if (f.addr.fam != fam) return 1;
+    if (fam == 6) {
+      uint32_t v, mk;
+      if (!codes || !codes->term(f.addr, f.plen < 0 ? 128 : f.plen, &v, &mk)) return -1;
+      if (mk) a->t.push_back({axis, v, mk});
+      return 0;
+    }
     int plen = f.plen < 0 ? 32 : f.plen;
     uint32_t mk = prefix_mask(plen);
     if (mk) a->t.push_back({axis, f.addr.v4() & mk, mk});
@@ -556,9 +720,9 @@ std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint
   bool have_ip = false, have_l4 = false;
   uint8_t pax;
   const int pc = probe_clause(r, d, &pax);
-  if (pc >= 0) {
+  if (pc >= 0) {  // probe entry: the Bloom bits are the probed clause's (probe_clause checked them)
     filt_clause_ip(r.clause[pc], &axis, &ipbits);
-    axis = 8u + pax;  // probe entry; the Bloom bits are the probed clause's
+    axis = 8u + pax;
     have_ip = true;
   }
   for (int c = 0; c < r.n; c++) {
@@ -644,6 +808,8 @@ struct PhaseTimer {
 
 // Flow -> rule gathering (step 1 of an image build).
 struct Gather {
+  int fam = 4;                      // image family: 4, or 6 (addresses through `codes`)
+  const V6Codes* codes = nullptr;
   std::map<uint32_t, RuleB> soft[7];
   std::map<std::pair<int, int>, RuleB> hard[7];  // key (-priority, verdict)
   std::set<uint32_t> counted_allow, counted_deny;
@@ -651,12 +817,13 @@ struct Gather {
   std::string error;
   // only_conj != 0: take only that conjunction's actions of a soft flow (delta builds gather per rule).
   int add(const Flow& f, uint32_t only_conj = 0);
+  uint16_t eth() const { return fam == 4 ? kEthIP : kEthIPv6; }
   // One conjunction(id, k/n) action of soft flow f (delta builds: the action comes from the
   // context's action map, not from a scan of the flow's possibly long action list).
   int add_soft(const Flow& f, uint32_t id, uint32_t k, uint32_t n) {
     n_flows++;
     Atom a;
-    int ar = atom_of(f.m, &a);
+    int ar = atom_of(f.m, &a, fam, codes);
     if (ar < 0) {
       error = "unsupported match: " + f.str();
       return -GPC_EINVAL;
@@ -686,7 +853,7 @@ int Gather::add(const Flow& f, uint32_t only_conj) {
   n_flows++;
   if (f.table == TB_EGRESS_METRIC || f.table == TB_INGRESS_METRIC) {
     const Match& m = f.m;
-    if (m.has_ct_label && m.has_ct_state && (m.ct_mask & 1) && (m.ct_data & 1) && (!m.has_dl || m.dl_type == kEthIP)) {
+    if (m.has_ct_label && m.has_ct_state && (m.ct_mask & 1) && (m.ct_data & 1) && (!m.has_dl || m.dl_type == eth())) {
       uint32_t id = f.table == TB_INGRESS_METRIC ? uint32_t(m.label_v & 0xffffffffu) : uint32_t(m.label_v >> 32);
       counted_allow.insert(id);
     } else if ((m.reg_present & (1u << 3)) && (m.reg_present & 1) && (m.reg_v[0] & 0x400)) {
@@ -698,7 +865,7 @@ int Gather::add(const Flow& f, uint32_t only_conj) {
   if (f.m.has_conj) {  // conj action flow
     Match rest = f.m;
     rest.has_conj = false;
-    bool fam_ok = !rest.has_dl || rest.dl_type == kEthIP;
+    bool fam_ok = !rest.has_dl || rest.dl_type == eth();
     rest.has_dl = false;
     if (rest.str(0) != "priority=0") {
       error = "unsupported conj_id flow: " + f.str();
@@ -720,7 +887,7 @@ int Gather::add(const Flow& f, uint32_t only_conj) {
     return GPC_OK;
   }
   Atom a;
-  int ar = atom_of(f.m, &a);
+  int ar = atom_of(f.m, &a, fam, codes);
   if (ar < 0) {
     error = "unsupported match: " + f.str();
     return -GPC_EINVAL;
@@ -764,6 +931,92 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     }
   }
   return emit(G, np, slots, out);
+}
+
+// IPv6 image: the same build over the IPv6 half of the flows (addresses interned as codes), plus
+// the LPM table the kernel maps packet addresses through (appended to the blob, hdr.v6_lpm).
+int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out) {
+  *out = HostImage();
+  V6Codes codes;
+  int rc = codes.build(np, &out->error);
+  if (rc) return rc;
+  Gather G;
+  G.fam = 6;
+  G.codes = &codes;
+  for (auto& kv : np.installed()) {
+    if ((rc = G.add(kv.second))) {
+      out->error = G.error;
+      return rc;
+    }
+  }
+  if ((rc = emit(G, np, slots, out))) return rc;
+  // LPM: one slot per tree node (root excluded: a miss means code 0)
+  std::vector<uint32_t> lens;
+  for (size_t n = 1; n < codes.nodes.size(); n++) lens.push_back(uint32_t(codes.nodes[n].len));
+  std::sort(lens.rbegin(), lens.rend());
+  lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
+  if (lens.size() > kV6MaxLens) {
+    out->error = "too many distinct IPv6 prefix lengths";
+    return -GPC_EINVAL;
+  }
+  const size_t nk = codes.nodes.size() - 1;
+  const uint32_t S = kV6BucketSlots, W = kV6SlotWords;
+  uint32_t lg = 0;
+  while (double(S << lg) * 0.7 < double(nk + 1)) lg++;
+  std::vector<uint32_t> tab;
+  bool ok = false;
+  for (int attempt = 0; attempt < 8 && !ok; attempt++, lg++) {
+    const uint32_t nb = 1u << lg, mask = nb - 1;
+    tab.assign(size_t(nb) * S * W, 0u);
+    std::mt19937 rng(4321 + attempt);
+    ok = true;
+    for (size_t n = 1; n < codes.nodes.size() && ok; n++) {
+      const auto& N = codes.nodes[n];
+      uint32_t cur[8] = {uint32_t(N.v >> 96), uint32_t(N.v >> 64), uint32_t(N.v >> 32), uint32_t(N.v),
+                         uint32_t(N.len) | kV6Valid, N.code, 0u, 0u};
+      bool placed = false;
+      for (int kick = 0; kick < 1000 && !placed; kick++) {
+        const uint64_t hk = v6_hkey(cur, cur[4] & 0xffu);
+        const uint32_t bs[2] = {hash_b1(hk, mask), hash_b2(hk, mask)};
+        for (uint32_t b : bs) {
+          for (uint32_t i = 0; i < S && !placed; i++) {
+            uint32_t* sl = tab.data() + (size_t(b) * S + i) * W;
+            if (!(sl[4] & kV6Valid)) {
+              std::memcpy(sl, cur, sizeof cur);
+              placed = true;
+            }
+          }
+          if (placed) break;
+        }
+        if (!placed) {
+          uint32_t* sl = tab.data() + (size_t(bs[rng() & 1]) * S + rng() % S) * W;
+          for (uint32_t w = 0; w < W; w++) std::swap(cur[w], sl[w]);
+        }
+      }
+      ok = placed;
+    }
+  }
+  if (!ok) {
+    out->error = "IPv6 LPM table construction failed";
+    return -GPC_ENOMEM;
+  }
+  auto& b = out->blob;
+  while (b.size() % 16) b.push_back(0u);
+  const uint32_t lpm = uint32_t(b.size());
+  V6Lpm L{};
+  L.hash_log2 = lg - 1;  // the loop advanced lg past the successful attempt
+  L.n_lens = uint32_t(lens.size());
+  for (size_t i = 0; i < lens.size(); i++) L.lens[i] = lens[i];
+  const size_t lw = (sizeof(V6Lpm) / 4 + 15) / 16 * 16;
+  L.hash_off = lpm + uint32_t(lw);
+  b.resize(b.size() + lw, 0u);
+  std::memcpy(b.data() + lpm, &L, sizeof L);
+  b.insert(b.end(), tab.begin(), tab.end());
+  out->hdr.v6_lpm = lpm;
+  out->bytes_hash += 4ull * tab.size();
+  out->v6_code_bits = uint32_t(codes.max_clen);
+  out->v6_prefixes = uint32_t(nk);
+  return GPC_OK;
 }
 
 // Rule-centric gather of the current versions of `conj` (uninstalled ones are skipped) plus every

@@ -25,6 +25,7 @@ struct HostImage {
   std::unordered_map<uint32_t, uint32_t> conj_rid;  // soft rules
   std::vector<uint32_t> hard_rids[6];                // hard pseudo-rules per table
   bool any_noact = false;  // a soft rule without an IPv4 conj_id flow (delta combine needs none)
+  uint32_t v6_code_bits = 0, v6_prefixes = 0;  // IPv6 image: deepest code, interned prefixes
 };
 
 // Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
@@ -51,6 +52,8 @@ class SlotMap {
 };
 
 int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out);
+// The IPv6 image (core.hpp "IPv6 interning"): full build, no journal.
+int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out);
 // Append-only delta store over one base image (core.hpp "journal"). apply() appends the current
 // versions of the changed rules (records, driver-bucket entries, copied-on-write head pages) and a
 // new epoch header with the cumulative tombstones; nothing published earlier is rewritten, so the

@@ -14,7 +14,11 @@ struct EpochArgs {
   const uint32_t* pool;   // journal pool (null: base image alone)
   uint32_t jhdr;          // JournalHdr word offset of this epoch
   const uint32_t* svc;    // null: no Services (AntreaProxy stage skipped)
+  uint32_t v6_lpm;        // IPv6 image: word offset of its V6Lpm block (host copy of ImageHdr.v6_lpm)
 };
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, hipStream_t stream);
+// IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).
+int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
+                     unsigned long long* counters, int count, hipStream_t stream);
 }

@@ -67,7 +67,8 @@ class gpc_rule(C.Structure):
 
 class gpc_pkt_soa(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("src", "dst", "sport", "dport", "proto", "out_port", "in_port", "svc_group",
-                                          "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "len")]
+                                          "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "len",
+                                          "src6", "dst6", "ct_src6", "ct_dst6")]
 
 
 class gpc_policy_info(C.Structure):
@@ -109,7 +110,7 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_install_service_group", "gpc_uninstall_service_group", "gpc_install_endpoint_flows",
            "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
-           "gpc_abi_version"]
+           "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6"]
 
 _lib = None
 
@@ -158,6 +159,9 @@ def load(path: str = LIB_PATH):
     lib.gpc_classify_lb.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32, vp]
     lib.gpc_classify_host_lb.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32]
     lib.gpc_debug_service_image.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
+    lib.gpc_classify6.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32, vp]
+    lib.gpc_classify6_host.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32]
+    lib.gpc_debug_image6.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp), C.POINTER(sz)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -287,7 +291,9 @@ class RuleBuf:
 
 PKT_COLUMNS = {"src": np.uint32, "dst": np.uint32, "sport": np.uint16, "dport": np.uint16, "proto": np.uint8,
                "out_port": np.uint32, "in_port": np.uint32, "svc_group": np.uint32, "tun_id": np.uint32,
-               "ct_src": np.uint32, "ct_dst": np.uint32, "ct_state": np.uint8, "dest": np.uint8, "len": np.uint16}
+               "ct_src": np.uint32, "ct_dst": np.uint32, "ct_state": np.uint8, "dest": np.uint8, "len": np.uint16,
+               # IPv6 batches: (n, 16) uint8, network byte order
+               "src6": np.uint8, "dst6": np.uint8, "ct_src6": np.uint8, "ct_dst6": np.uint8}
 
 
 def pkt_soa_host(cols: Dict[str, np.ndarray]):
@@ -482,6 +488,25 @@ class Classifier:
         _check(self.lib.gpc_classify_host_lb(self.h, C.byref(soa), n, out.ctypes.data,
                                              lbo.ctypes.data if lb else None, int(count)), "gpc_classify_host")
         return (out.reshape(n, 2), lbo) if lb else out.reshape(n, 2)
+
+    def classify6_host(self, cols: Dict[str, np.ndarray], count=False):
+        """IPv6 verdicts (n, 2): cols carries src6 / dst6 as (n, 16) uint8 (network order)."""
+        soa, keep, n = pkt_soa_host(cols)
+        out = np.zeros(2 * n, dtype=VERDICT_DTYPE)
+        _check(self.lib.gpc_classify6_host(self.h, C.byref(soa), n, out.ctypes.data, int(count)), "gpc_classify6_host")
+        return out.reshape(n, 2)
+
+    def classify6_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0):
+        _check(self.lib.gpc_classify6(self.h, C.byref(soa), n, out_ptr, int(count), stream or None), "gpc_classify6")
+
+    def debug_image6(self):
+        """(blob pointer, n_words, hdr pointer) of the committed IPv6 image (None when absent)."""
+        b = C.POINTER(C.c_uint32)()
+        n = C.c_size_t()
+        h = C.c_void_p()
+        hb = C.c_size_t()
+        _check(self.lib.gpc_debug_image6(self.h, C.byref(b), C.byref(n), C.byref(h), C.byref(hb)), "gpc_debug_image6")
+        return (C.cast(b, C.c_void_p).value if n.value else None), n.value, h.value
 
     def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, lb_ptr: int = 0):
         _check(self.lib.gpc_classify_lb(self.h, C.byref(soa), n, out_ptr, lb_ptr or None, int(count), stream or None),

@@ -378,3 +378,77 @@ def gen_packets_torch(wl: Workload, n: int, seed=PKT_SEED, device="cuda"):
     u32 = lambda t: (t & 0xFFFFFFFF).to(torch.int64).to(torch.uint32) if hasattr(torch, "uint32") else t.to(torch.int32)
     return {"src": u32(src), "dst": u32(dst), "sport": sport.to(torch.int16), "dport": dport.to(torch.int16),
             "proto": proto.to(torch.uint8), "out_port": u32(out_port), "len": length.to(torch.int16)}
+
+
+# ------------------------------------------------------------------------------------- IPv6
+# IPv6 (and dual-stack) variants: every IPv4 address / CIDR of a workload embedded in fd00:10::/96
+# (a.b.c.d -> fd00:10::a.b.c.d, /L -> /(96 + L)). The rule structure, priorities and conj ids are
+# unchanged, so IPv6 packets mapped the same way must get exactly the IPv4 verdicts (metamorphic
+# parity of the IPv6 image against the IPv4 one, itself pinned by the oracles).
+V6_EMBED = int(ipaddress.IPv6Address("fd00:10::"))
+_V6_PREFIX12 = np.frombuffer(V6_EMBED.to_bytes(16, "big")[:12], dtype=np.uint8)
+
+
+def _v6_addr(a):
+    if isinstance(a, str):
+        if "." not in a:
+            return a
+        if "/" in a:
+            return _v6_addr({"ipnet": a})["ipnet"]
+        return str(ipaddress.IPv6Address(V6_EMBED | int(ipaddress.ip_address(a))))
+    (k, v), = a.items()
+    if k in ("ip", "ctip"):
+        return {k: str(ipaddress.IPv6Address(V6_EMBED | int(ipaddress.ip_address(v))))}
+    if k in ("ipnet", "ctipnet"):
+        n = ipaddress.ip_network(v, strict=False)
+        return {k: "%s/%d" % (ipaddress.IPv6Address(V6_EMBED | int(n.network_address)), 96 + n.prefixlen)}
+    return a
+
+
+def to_ipv6(wl: Workload, dual=False) -> Workload:
+    """The workload with its addresses in IPv6 (dual=True: both families in every peer list)."""
+    import copy
+    out = Workload(wl.name + ("dual" if dual else "v6"))
+    out.local_ips, out.local_ports, out.meta = wl.local_ips, wl.local_ports, wl.meta
+    for r in wl.rules:
+        r6 = copy.deepcopy(r)
+        for side in ("from", "to"):
+            if r.get(side) is not None:
+                mapped = [_v6_addr(a) for a in r[side]]
+                r6[side] = (list(r[side]) + [m for m, a in zip(mapped, r[side]) if m != a]) if dual else mapped
+        out.rules.append(r6)
+    return out
+
+
+def v6_bytes(v4: np.ndarray) -> np.ndarray:
+    """(n,) IPv4 addresses -> (n, 16) uint8 network-order IPv6 addresses in fd00:10::/96."""
+    v4 = np.asarray(v4, dtype=np.uint32)
+    tail = v4.astype(">u4").view(np.uint8).reshape(-1, 4)
+    return np.ascontiguousarray(np.concatenate([np.broadcast_to(_V6_PREFIX12, (len(v4), 12)), tail], axis=1))
+
+
+def packets_to_v6(cols: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """IPv4 packet columns -> the IPv6 batch of the same packets (ICMP -> ICMPv6)."""
+    out = {k: v for k, v in cols.items() if k not in ("src", "dst", "ct_src", "ct_dst")}
+    for k in ("src", "dst", "ct_src", "ct_dst"):
+        if k in cols:
+            out[k + "6"] = v6_bytes(cols[k])
+    out["proto"] = np.where(cols["proto"] == 1, 58, cols["proto"]).astype(np.uint8)
+    return out
+
+
+def packets_to_v6_torch(cols):
+    """Device version of packets_to_v6 (bench): (n, 16) uint8 address columns in fd00:10::/96."""
+    import torch
+    out = {k: v for k, v in cols.items() if k not in ("src", "dst", "ct_src", "ct_dst")}
+    for k in ("src", "dst", "ct_src", "ct_dst"):
+        if k not in cols:
+            continue
+        v = cols[k].to(torch.int64) & 0xFFFFFFFF
+        n = v.shape[0]
+        tail = torch.stack([(v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255], dim=1).to(torch.uint8)
+        head = torch.as_tensor(_V6_PREFIX12.copy(), device=v.device).expand(n, 12)
+        out[k + "6"] = torch.cat([head, tail], dim=1).contiguous()
+    p = cols["proto"]
+    out["proto"] = torch.where(p == 1, torch.full_like(p, 58), p)
+    return out

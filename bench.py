@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def _lbar(wl, clf, n=20000):
+def _lbar(wl, clf, n=20000, family=4):
     """Mean distinct 64-B image lines one packet's evaluation reads (instrumented host emulation of
     the same image, tests/csrc/emu.cpp), i.e. L-bar of SURVEY §8(d)."""
     try:
@@ -38,7 +38,10 @@ def _lbar(wl, clf, n=20000):
         from antrea_amd import workload
         cols = workload.gen_packets(wl, n, seed=12345)
         emu.stats(reset=True)
-        emu.classify(clf, cols)
+        if family == 6:
+            emu.classify6(clf, workload.packets_to_v6(cols))
+        else:
+            emu.classify(clf, cols)
         s = emu.stats()
         return s[6] / max(1, s[7])
     except Exception as e:  # pragma: no cover - g++ missing
@@ -105,7 +108,8 @@ def _pmc_pass(counter, args):
     d = tempfile.mkdtemp(prefix="gpc_pmc_")
     cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "classify_kernel", "-d", d, "-o", "pmc",
            "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline", "--no-traffic", "--config", args.config, "--packets", str(args.packets)]
+           "--no-cpu-baseline", "--no-traffic", "--config", args.config, "--packets", str(args.packets),
+           "--family", str(args.family)]
     if args.no_count:
         cmd.append("--no-count")
     try:
@@ -139,9 +143,13 @@ def main():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
+    ap.add_argument("--family", type=int, default=4, choices=(4, 6),
+                    help="6: the workload's addresses embedded in fd00:10::/96, IPv6 packets (gpc_classify6)")
     args = ap.parse_args()
+    if args.family == 6 and args.config in ("C4", "C5"):
+        ap.error("--family 6: C1-C3 only (no IPv6 AntreaProxy stage / delta epochs)")
     churn = args.config == "C5"
-    if args.config == "C4":  # the C oracle has no AntreaProxy stage: no CPU leg for C4
+    if args.config == "C4" or args.family == 6:  # the C oracle has no AntreaProxy stage / IPv6
         args.no_cpu_baseline = True
     if churn:
         args.no_traffic = True
@@ -176,9 +184,10 @@ def main():
 
     t0 = time.time()
     wl = workload.CONFIGS["C3" if churn else args.config]()
-    clf = gpc.Classifier(device=local)
+    v6 = args.family == 6
+    clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6)
     clf.initialize()
-    clf.batch_install_policy_rule_flows(wl.rules)
+    clf.batch_install_policy_rule_flows(workload.to_ipv6(wl).rules if v6 else wl.rules)
     if getattr(wl, "services", None):
         workload.install_services(clf, wl)
     clf.commit()
@@ -186,13 +195,16 @@ def main():
 
     n = args.packets
     cols = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + rank, device=dev)
+    if v6:
+        cols = workload.packets_to_v6_torch(cols)
+    classify = clf.classify6_device if v6 else clf.classify_device
     out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
     soa = gpc.pkt_soa_device(cols)
     count = not args.no_count
     stream = torch.cuda.Stream(dev) if churn else torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     for _ in range(args.warmup):
-        clf.classify_device(soa, n, out.data_ptr(), count=count, stream=sptr)
+        classify(soa, n, out.data_ptr(), count=count, stream=sptr)
     clf.reset_counters()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -214,7 +226,7 @@ def main():
     t_start = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
-        clf.classify_device(soa, n, out.data_ptr(), count=count, stream=sptr)
+        classify(soa, n, out.data_ptr(), count=count, stream=sptr)
         ends[i].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -269,8 +281,10 @@ def main():
         a, c = np.unique(v[:, j, 4], return_counts=True)
         mix[stage] = {names[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
 
-    lbar = _lbar(wl, clf)
+    lbar = _lbar(wl, clf, family=args.family)
     b_in, b_out = (19 if getattr(wl, "services", None) else 17), 16  # +2 B len for C4
+    if v6:
+        b_in += 24  # 16-B instead of 4-B src / dst
     b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
     pps_kernel = n / (kern_ms / 1e3)
     achieved = pps_kernel * b_alg / 1e9
@@ -291,7 +305,8 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": args.config, "rules": len(wl.rules), "packets_per_gpu": n,
-                   "flows": st["n_flows"], "image_mb": round(st["device_bytes"] / 1e6, 1),
+                   "flows": st["n_flows"],
+                   "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
                    "verdict_mix": mix, "build_s": round(t_build, 1)},
         "kernel_ms": round(kern_ms, 3),  # both stage launches of a step (HIP events on the launch stream)
@@ -304,6 +319,10 @@ def main():
         res["config"]["services"] = len(wl.services)
         res["config"]["endpoints"] = sum(len(e) for e in wl.groups.values())
         res["config"]["to_service_frac"] = wl.svc_frac
+    if v6:
+        res["metric"] = "Mpps classified (IPv6 5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW"
+        res["config"]["family"] = 6
+        res["config"]["v6_embedding"] = "fd00:10::/96"
     if update is not None:
         res["update"] = update
         res["metric"] = "Mpps classified under AddPolicyRuleAddress/DeletePolicyRuleAddress churn @100k rules"

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GPC_ABI_VERSION 1
+#define GPC_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------- error codes */
 #define GPC_OK 0
@@ -186,6 +186,13 @@ typedef struct gpc_pkt_soa {
   const uint8_t* ct_state;       /* (+new+trk) */
   const uint8_t* dest;           /* gpc_dest (POD) */
   const uint16_t* len;           /* bytes for per-rule counters (0) */
+  /* IPv6 batches (gpc_classify6): 16 network-order bytes per packet, 16-byte aligned; src6 and
+   * dst6 required (they replace src / dst), ct_src6 / ct_dst6 optional (default src6 / dst6).
+   * proto is the upper-layer protocol (ICMPv6 = 58). Ignored by gpc_classify. */
+  const uint8_t* src6;           /* ipv6_src */
+  const uint8_t* dst6;           /* ipv6_dst */
+  const uint8_t* ct_src6;        /* ct_ipv6_src */
+  const uint8_t* ct_dst6;        /* ct_ipv6_dst */
 } gpc_pkt_soa;
 
 typedef struct gpc_verdict {     /* 8 bytes; gpc_classify writes 2 per packet: [egress, ingress] */
@@ -353,6 +360,13 @@ int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* o
  * runs the same stage (it just does not write lb_out). */
 int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
                     int32_t count, void* stream);
+/* IPv6 packets (pkts->src6 / dst6 columns) against the IPv6 half of the rule set (the ipv6_* /
+ * tcp6 / udp6 / icmp6 flows and the family-less ones), as OVS classifies an IPv6 packet in the
+ * same tables. Needs gpc_config.ipv6_enabled; every commit that changes rules rebuilds the IPv6
+ * image in full (no delta epochs, no AntreaProxy stage for IPv6). Same verdict / counter layout.
+ * -GPC_EINVAL if the IPv6 prefixes of the rule set need more than 32 code bits (core.hpp). */
+int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
+int gpc_classify6_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
 /* Same with HOST pointers (copies in and out; synchronous). */
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
 int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
@@ -372,6 +386,8 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out);
  * device reset). Pointers stay valid until the next gpc_commit. Used by tests to verify the
  * image independently of the device. */
 int gpc_debug_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes);
+/* The last committed IPv6 image (NULL / 0 when IPv6 is disabled). */
+int gpc_debug_image6(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words, const void** hdr, size_t* hdr_bytes);
 /* The host copy of the committed Service image (NULL / 0 when no Services). */
 int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words);
 /* Host mirror of the journal pool and the current epoch's journal header offset (NULL / 0 when

@@ -82,3 +82,38 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
   }
   return 0;
 }
+
+// IPv6 batch over the IPv6 image (gpc_debug_image6): addresses mapped to codes as the kernel does.
+extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
+                             unsigned long long* counters) {
+  const ImageHdr* h = static_cast<const ImageHdr*>(hdr);
+  View im{{blob, h, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}, 1u, 0u};
+  auto code = [&](const uint8_t* col, size_t i) {
+    uint32_t a[4];
+    v6_words(col + 16 * i, a);
+    return v6_code(blob, h->v6_lpm, a);
+  };
+  for (size_t i = 0; i < n; i++) {
+    g_lines.clear();
+    g_line_site.clear();
+    const uint32_t src = code(pk->src6, i), dst = code(pk->dst6, i);
+    const uint32_t ct_src = pk->ct_src6 ? code(pk->ct_src6, i) : src, ct_dst = pk->ct_dst6 ? code(pk->ct_dst6, i) : dst;
+    const uint32_t dest = pk->dest ? pk->dest[i] : 0u;
+    Pkt p;
+    make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
+             pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst,
+             pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+    PacketOut o = classify_packet<false, 0>(im, p, dest);
+    std::sort(g_lines.begin(), g_lines.end());
+    ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
+    ::gpc_emu_stats[7] += 1;
+    if (counters)
+      count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
+    uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);
+    w[0] = o.e.conj;
+    w[1] = o.e.packed;
+    w[2] = o.g.conj;
+    w[3] = o.g.packed;
+  }
+  return 0;
+}

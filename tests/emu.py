@@ -29,7 +29,23 @@ def load():
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
     _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                   C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
+    _lib.emu_classify6.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p,
+                                   C.c_void_p]
     return _lib
+
+
+def classify6(clf: "gpc.Classifier", cols, counters=None):
+    """Emulated IPv6 verdicts (n, 2) of the IPv6 image last committed by `clf`."""
+    blob, nw, hdr = clf.debug_image6()
+    assert blob, "no IPv6 image (ipv6 disabled, or the IPv6 rule set was rejected)"
+    soa, keep, n = gpc.pkt_soa_host(cols)
+    out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
+    cptr = None
+    if counters is not None:
+        assert counters.dtype == np.uint64 and counters.flags.c_contiguous
+        cptr = counters.ctypes.data
+    load().emu_classify6(blob, hdr, C.byref(soa), n, out.ctypes.data, cptr)
+    return out.reshape(n, 2)
 
 
 def classify(clf: "gpc.Classifier", cols, counters=None, lb=None):

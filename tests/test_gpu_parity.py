@@ -185,3 +185,27 @@ def test_gpu_service_stage(name):
         o, olb = _oracle(wl, c, cols, n)
         _cmp(got, o, cols)
         assert (lb == olb).all()
+
+
+@pytest.mark.parametrize("name", ["C1dual", "C3"])
+def test_gpu_ipv6(name):
+    """gpc_classify6 (IPv6 image, LPM address interning on the device) == host emulation of the
+    same image, verdicts and per-rule counters; C1dual also classifies IPv4 packets through the
+    same dual-stack context. Full C3 in IPv6: 100k rules, 245k nested prefixes."""
+    wl = workload.config1(seed=9) if name == "C1dual" else workload.config3()
+    n = 20000 if name == "C1dual" else 200_000
+    cols = workload.gen_packets(wl, n, seed=9)
+    cols6 = workload.packets_to_v6(cols)
+    c = gpc.Classifier(ipv6=True)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(workload.to_ipv6(wl, dual=name == "C1dual").rules))
+    c.commit()
+    got = c.classify6_host(cols6, count=True)
+    _, slots = c.counters()
+    arr = np.zeros((len(slots), 3), dtype=np.uint64)
+    want = emu.classify6(c, cols6, counters=arr)
+    _cmp(got, want, cols6)
+    exp = {conj: tuple(int(x) for x in arr[i]) for i, conj in enumerate(slots) if conj and arr[i].any()}
+    assert exp and {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)} == exp
+    if name == "C1dual":
+        _cmp(c.classify_host(cols), emu.classify(c, cols), cols)

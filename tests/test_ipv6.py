@@ -1,0 +1,131 @@
+"""IPv6 / dual-stack classification (core.hpp "IPv6 interning", image.cpp build_image6).
+
+CPU tier: the product's IPv6 image evaluated by the host emulation of the kernel body
+  * against the Python oracle (OVS classifier restatement over the oracle-compiled IPv6 flows,
+    IPv6 packets) -- direct parity;
+  * against the product's own IPv4 image on the same workload embedded in fd00:10::/96 --
+    metamorphic parity up to full C3 (100k rules), where the IPv4 side is itself pinned by the C
+    oracle (tests/test_oracle_c.py);
+  * the IPv6 flow dump equals the oracle compiler's.
+The GPU tier (tests/test_gpu_parity.py) checks gpc_classify6 against the same emulation."""
+import copy
+import ipaddress
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from oracle import compiler as oc
+from oracle import ovs_cls
+from tests import emu
+from tests.test_emu_parity import _cmp
+
+
+def _classifier(rules, ipv4=True, ipv6=True):
+    c = gpc.Classifier(ipv4=ipv4, ipv6=ipv6)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    emu.commit_host(c)
+    return c
+
+
+def _oracle6(rules, cols6, n, ipv4=True):
+    fnp = oc.FeatureNetworkPolicy(ipv4=ipv4, ipv6=True)
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in rules}
+    pipe = ovs_cls.Pipeline(fnp.dump_flows(), tiers)
+    out = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
+    for i in range(n):
+        pkt = {k: int(v[i]) for k, v in cols6.items() if v.ndim == 1}
+        for k in ("src6", "dst6"):
+            pkt[k[:-1]] = int.from_bytes(bytes(cols6[k][i]), "big")
+        pkt["eth"] = 0x86DD
+        e, g = pipe.classify(pkt)
+        for j, v in enumerate((e, g)):
+            out[i, j] = (v[1], v[0], v[2], v[3], v[4])
+    return out
+
+
+def _small_c3(seed):
+    return workload.config3(seed=seed, n_policies_per_dir=6, rules_per_policy=8)
+
+
+@pytest.mark.parametrize("name,dual", [("C1", False), ("C1", True), ("C3s", False), ("C3s", True)])
+def test_ipv6_emu_vs_oracle(name, dual):
+    wl = workload.config1(seed=4) if name == "C1" else _small_c3(4)
+    w6 = workload.to_ipv6(wl, dual=dual)
+    n = 300
+    cols6 = workload.packets_to_v6(workload.gen_packets(wl, n, seed=4))
+    want = _oracle6(w6.rules, cols6, n)
+    got = emu.classify6(_classifier(w6.rules), cols6)
+    _cmp(got, want, cols6)
+    assert (got["action"] == 2).sum() > 0 and (got["action"] == 1).sum() > 0
+
+
+@pytest.mark.parametrize("name", ["C1", "C3s", "C2", "C3-10k"])
+def test_ipv6_metamorphic_vs_ipv4(name):
+    """Every address embedded in fd00:10::/96: IPv6 verdicts == IPv4 verdicts, packet by packet."""
+    wl = {"C1": lambda: workload.config1(seed=5), "C3s": lambda: _small_c3(5), "C2": workload.config2,
+          "C3-10k": lambda: workload.config3(n_policies_per_dir=50, rules_per_policy=100)}[name]()
+    n = 20000
+    cols = workload.gen_packets(wl, n, seed=5)
+    want = emu.classify(_classifier(wl.rules, ipv6=False), cols)
+    c6 = _classifier(workload.to_ipv6(wl).rules)
+    got = emu.classify6(c6, workload.packets_to_v6(cols))
+    _cmp(got, want, cols)
+
+
+def test_ipv6_metamorphic_full_c3():
+    """Full C3 (100k rules, 245k nested CIDRs) in IPv6: the prefix tree fits 32-bit codes and the
+    verdicts equal the IPv4 image's."""
+    wl = workload.config3()
+    n = 8000
+    cols = workload.gen_packets(wl, n, seed=6)
+    want = emu.classify(_classifier(wl.rules, ipv6=False), cols)
+    got = emu.classify6(_classifier(workload.to_ipv6(wl).rules), workload.packets_to_v6(cols))
+    _cmp(got, want, cols)
+
+
+def test_dual_stack_both_families():
+    """Peer lists with both families: IPv4 packets through the IPv4 image and IPv6 packets through
+    the IPv6 image of ONE dual-stack context both equal the single-family verdicts."""
+    wl = _small_c3(7)
+    n = 3000
+    cols = workload.gen_packets(wl, n, seed=7)
+    want = emu.classify(_classifier(wl.rules, ipv6=False), cols)
+    c = _classifier(workload.to_ipv6(wl, dual=True).rules)
+    _cmp(emu.classify(c, cols), want, cols)
+    _cmp(emu.classify6(c, workload.packets_to_v6(cols)), want, cols)
+
+
+@pytest.mark.parametrize("dual", [False, True])
+def test_ipv6_flow_dump_matches_oracle_compiler(dual):
+    wl = workload.to_ipv6(_small_c3(8), dual=dual)
+    fnp = oc.FeatureNetworkPolicy(ipv6=True)
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    c = gpc.Classifier(ipv6=True)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    got, want = sorted(c.dump_flows()), sorted(fnp.dump_flows())
+    assert got == want
+    assert any("ipv6_src=fd00:10::" in l for l in got)
+
+
+def test_ipv6_code_overflow_keeps_ipv4():
+    """A prefix chain deeper than 32 code bits: the IPv6 image is not published (gpc_classify6
+    refuses), the IPv4 image of the same commit is."""
+    rules = []
+    base = int(ipaddress.IPv6Address("2001:db8::"))
+    for i, plen in enumerate(range(40, 120)):  # nested chain: each level needs its own bit
+        rules.append({"direction": "In", "table": "IngressRule", "flow_id": i + 1, "policy_type": "K8sNetworkPolicy",
+                      "from": [{"ipnet": "%s/%d" % (ipaddress.IPv6Address(base), plen)}, "10.0.0.%d" % (i % 250 + 1)],
+                      "to": [{"ofport": 3}], "service": None, "policy_name": "p%d" % i})
+    c = _classifier(rules)
+    assert c.debug_image6()[0] is None
+    cols = {"src": np.array([0x0A000001], np.uint32), "dst": np.array([0x0A000002], np.uint32),
+            "sport": np.array([1000], np.uint16), "dport": np.array([80], np.uint16),
+            "proto": np.array([6], np.uint8), "out_port": np.array([3], np.uint32)}
+    v = emu.classify(c, cols)
+    assert v[0, 1]["action"] == 2  # allowed by rule 1 through the IPv4 image
