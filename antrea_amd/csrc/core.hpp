@@ -244,11 +244,12 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 // node. Then "a in P" <=> "code(a) in code(P)", where code(a) = code of the deepest prefix holding
 // a (its longest matching prefix) padded with zeros, so the flows keep their prefix shape and the
 // whole IPv4 machinery (bands, Bloom bits, intervals) applies unchanged. code(a) is found on the
-// device by a longest-prefix match: one hash probe per distinct prefix length, longest first.
+// device by a longest-prefix match: binary search on the distinct prefix lengths (Waldvogel), one
+// hash probe per step -- prefixes and markers, each carrying the code of its best matching prefix.
 constexpr uint32_t kV6MaxLens = 64;
 struct V6Lpm {
   uint32_t hash_off, hash_log2, n_lens, reserved;
-  uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), descending
+  uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
 };
 // hash slot (8 words): masked address (4 words, most significant first), len | kV6Valid, code, 2 pad;
 // bucket = 2 slots (one 64-B line), two choices
@@ -267,8 +268,11 @@ GPC_HD uint64_t v6_hkey(const uint32_t* m, uint32_t len) {
 GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a) {
   const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
   const uint32_t mask = (1u << L->hash_log2) - 1u;
-  for (uint32_t i = 0; i < L->n_lens; i++) {
-    const uint32_t len = L->lens[i];
+  uint32_t best = 0;
+  int lo = 0, hi = int(L->n_lens) - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint32_t len = L->lens[mid];
     uint32_t m[4];
     v6_mask(a, len, m);
     const uint64_t hk = v6_hkey(m, len);
@@ -276,13 +280,19 @@ GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* 
     const uint32_t* b2 = blob + L->hash_off + size_t(hash_b2(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
     GPC_TOUCH(b1, 64);
     GPC_TOUCH(b2, 64);
+    bool hit = false;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t* w = (c < 2 ? b1 : b2) + (c & 1) * kV6SlotWords;
-      if (w[4] == (len | kV6Valid) && w[0] == m[0] && w[1] == m[1] && w[2] == m[2] && w[3] == m[3]) return w[5];
+      if (w[4] == (len | kV6Valid) && w[0] == m[0] && w[1] == m[1] && w[2] == m[2] && w[3] == m[3]) {
+        hit = true;
+        best = w[5];
+      }
     }
+    if (hit) lo = mid + 1;
+    else hi = mid - 1;
   }
-  return 0u;
+  return best;
 }
 // 16 network-order bytes -> 4 host words, most significant first.
 GPC_HD void v6_words(const uint8_t* p, uint32_t* a) {

@@ -96,6 +96,7 @@ class V6Codes {
   struct Node {
     u128 v;
     int len;
+    int parent = -1;
     uint32_t code = 0;
     int clen = 0;
     std::vector<int> kids;
@@ -131,6 +132,7 @@ class V6Codes {
       }
       const int id = int(nodes.size());
       nodes.push_back(Node{p.first, p.second});
+      nodes.back().parent = st.back();
       nodes[st.back()].kids.push_back(id);
       st.push_back(id);
       index_[{p.first, p.second}] = id;
@@ -950,16 +952,48 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     }
   }
   if ((rc = emit(G, np, slots, out))) return rc;
-  // LPM: one slot per tree node (root excluded: a miss means code 0)
+  // LPM by binary search on prefix lengths (Waldvogel et al.): the table holds every tree node
+  // (root excluded: a miss everywhere means code 0) plus, for each node, a marker at every shorter
+  // length its binary search passes through, carrying the best matching prefix's code there.
   std::vector<uint32_t> lens;
   for (size_t n = 1; n < codes.nodes.size(); n++) lens.push_back(uint32_t(codes.nodes[n].len));
-  std::sort(lens.rbegin(), lens.rend());
+  std::sort(lens.begin(), lens.end());
   lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
   if (lens.size() > kV6MaxLens) {
     out->error = "too many distinct IPv6 prefix lengths";
     return -GPC_EINVAL;
   }
-  const size_t nk = codes.nodes.size() - 1;
+  auto pad = [](const V6Codes::Node& N) { return N.kids.empty() || N.clen == 0 ? N.code : N.code & prefix_mask(N.clen); };
+  std::map<std::pair<u128, uint32_t>, uint32_t> lpm_map;  // (value, len) -> code
+  for (size_t n = 1; n < codes.nodes.size(); n++) lpm_map[{codes.nodes[n].v, uint32_t(codes.nodes[n].len)}] = pad(codes.nodes[n]);
+  for (size_t n = 1; n < codes.nodes.size(); n++) {
+    const auto& P = codes.nodes[n];
+    const int t = int(std::lower_bound(lens.begin(), lens.end(), uint32_t(P.len)) - lens.begin());
+    int lo = 0, hi = int(lens.size()) - 1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) / 2;
+      if (mid == t) break;
+      if (mid > t) {
+        hi = mid - 1;
+        continue;
+      }
+      const uint32_t M = lens[size_t(mid)];
+      const std::pair<u128, uint32_t> key{P.v & v6_prefix_mask(int(M)), M};
+      if (!lpm_map.count(key)) {  // marker: code of the deepest ancestor of P no longer than M
+        int a = P.parent;
+        while (a > 0 && codes.nodes[size_t(a)].len > int(M)) a = codes.nodes[size_t(a)].parent;
+        lpm_map[key] = a > 0 ? pad(codes.nodes[size_t(a)]) : 0u;
+      }
+      lo = mid + 1;
+    }
+  }
+  std::vector<std::array<uint32_t, 8>> slots6;
+  for (auto& kv : lpm_map) {
+    const u128 v = kv.first.first;
+    slots6.push_back({uint32_t(v >> 96), uint32_t(v >> 64), uint32_t(v >> 32), uint32_t(v), kv.first.second | kV6Valid,
+                      kv.second, 0u, 0u});
+  }
+  const size_t nk = slots6.size();
   const uint32_t S = kV6BucketSlots, W = kV6SlotWords;
   uint32_t lg = 0;
   while (double(S << lg) * 0.7 < double(nk + 1)) lg++;
@@ -970,10 +1004,9 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out) {
     tab.assign(size_t(nb) * S * W, 0u);
     std::mt19937 rng(4321 + attempt);
     ok = true;
-    for (size_t n = 1; n < codes.nodes.size() && ok; n++) {
-      const auto& N = codes.nodes[n];
-      uint32_t cur[8] = {uint32_t(N.v >> 96), uint32_t(N.v >> 64), uint32_t(N.v >> 32), uint32_t(N.v),
-                         uint32_t(N.len) | kV6Valid, N.code, 0u, 0u};
+    for (size_t n = 0; n < slots6.size() && ok; n++) {
+      uint32_t cur[8];
+      std::memcpy(cur, slots6[n].data(), sizeof cur);
       bool placed = false;
       for (int kick = 0; kick < 1000 && !placed; kick++) {
         const uint64_t hk = v6_hkey(cur, cur[4] & 0xffu);
@@ -1015,7 +1048,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out) {
   out->hdr.v6_lpm = lpm;
   out->bytes_hash += 4ull * tab.size();
   out->v6_code_bits = uint32_t(codes.max_clen);
-  out->v6_prefixes = uint32_t(nk);
+  out->v6_prefixes = uint32_t(codes.nodes.size() - 1);
   return GPC_OK;
 }
 
