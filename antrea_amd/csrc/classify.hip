@@ -27,12 +27,28 @@ constexpr int kBlock = GPC_BLOCK;
 // stage, measured 8 % faster on C3 than one launch walking both stages (kStage = 0; lanes leave the
 // egress stage at different times). With Services one launch (0) does both stages: a second
 // launch would have to repeat the Service lookup, which costs more than the split saves (C4).
-// IPv6 address column (16 network-order bytes per packet, 16-B aligned) -> the address's code in
-// the IPv6 image (core.hpp v6_code): one coalesced 128-bit load, byte swaps, longest-prefix match.
-__device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_t* col, uint64_t i) {
+// IPv6 address columns (16 network-order bytes per packet, 16-B aligned) -> the addresses' codes in
+// the IPv6 image (core.hpp v6_codes): one coalesced 128-bit load per address, byte swaps, then K
+// longest-prefix matches in lock step.
+__device__ __forceinline__ void v6_load(const uint8_t* col, uint64_t i, uint32_t* a) {
   const uint4 v = reinterpret_cast<const uint4*>(col)[i];
-  const uint32_t a[4] = {__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z), __builtin_bswap32(v.w)};
-  return v6_code(ep.blob, ep.v6_lpm, a);
+  a[0] = __builtin_bswap32(v.x);
+  a[1] = __builtin_bswap32(v.y);
+  a[2] = __builtin_bswap32(v.z);
+  a[3] = __builtin_bswap32(v.w);
+}
+__device__ __forceinline__ void v6_code_pair(const EpochArgs& ep, const uint8_t* c0, const uint8_t* c1, uint64_t i,
+                                             uint32_t* code) {
+  uint32_t a[2][4];
+  v6_load(c0, i, a[0]);
+  v6_load(c1, i, a[1]);
+  v6_codes<2>(ep.blob, ep.v6_lpm, a, code);
+}
+__device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_t* col, uint64_t i) {
+  uint32_t a[1][4], c;
+  v6_load(col, i, a[0]);
+  v6_codes<1>(ep.blob, ep.v6_lpm, a, &c);
+  return c;
 }
 
 // kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
@@ -43,11 +59,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
+  uint4 prev = make_uint4(0u, 0u, 0u, 0u);
+  if (kStage == 2) prev = out[i];
   if (kV6) {
-    src = v6_code_at(ep, pk.src6, i);
-    dst = v6_code_at(ep, pk.dst6, i);
-    ct_src = pk.ct_src6 ? v6_code_at(ep, pk.ct_src6, i) : src;
-    ct_dst = pk.ct_dst6 ? v6_code_at(ep, pk.ct_dst6, i) : dst;
+    // The egress launch computes the src / dst codes (both LPMs in lock step) and parks them in the
+    // still empty ingress half of the verdict pair; the ingress launch takes them from there.
+    if (kStage == 2) {
+      src = prev.z;
+      dst = prev.w;
+    } else {
+      uint32_t sd[2];
+      v6_code_pair(ep, pk.src6, pk.dst6, i, sd);
+      src = sd[0];
+      dst = sd[1];
+    }
+    if (pk.ct_src6 && pk.ct_dst6) {
+      uint32_t cd[2];
+      v6_code_pair(ep, pk.ct_src6, pk.ct_dst6, i, cd);
+      ct_src = cd[0];
+      ct_dst = cd[1];
+    } else {
+      ct_src = pk.ct_src6 ? v6_code_at(ep, pk.ct_src6, i) : src;
+      ct_dst = pk.ct_dst6 ? v6_code_at(ep, pk.ct_dst6, i) : dst;
+    }
   } else {
     src = pk.src[i];
     dst = pk.dst[i];
@@ -70,11 +104,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   } else if (kStage != 2 && lb_out) {
     lb_out[i] = make_uint4(0u, 0u, 0u, 0u);
   }
-  uint4 prev = make_uint4(0u, 0u, 0u, 0u);
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
-    prev = out[i];
     const uint32_t ea = prev.y & 0xffu;
-    if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) return;
+    if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
+      if (kV6) out[i] = make_uint4(prev.x, prev.y, 0u, 0u);  // ingress NONE over the parked codes
+      return;
+    }
     if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
       out[i] = make_uint4(prev.x, prev.y, 0u, uint32_t(RV_BYPASS));
       return;
@@ -96,6 +131,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   }
   const VerdictOut e = o.e, g = o.g;
   if (kStage == 2) out[i] = make_uint4(prev.x, prev.y, g.conj, g.packed);
+  else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
   else out[i] = make_uint4(e.conj, e.packed, g.conj, g.packed);  // ingress NONE until the second launch
 }
 

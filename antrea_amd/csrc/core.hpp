@@ -252,7 +252,8 @@ struct V6Lpm {
   uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
 };
 // hash slot (8 words): masked address (4 words, most significant first), len | kV6Valid, code, 2 pad;
-// bucket = 2 slots (one 64-B line), two choices
+// bucket = 2 slots (one 64-B line), two choices (both loaded per probe: measured faster on C3 than
+// 128-B single-line buckets with an overflow flag, whose table is larger)
 constexpr uint32_t kV6SlotWords = 8, kV6BucketSlots = 2, kV6Valid = 0x100u;
 GPC_HD void v6_mask(const uint32_t* a, uint32_t len, uint32_t* m) {
   for (int w = 0; w < 4; w++) {
@@ -264,35 +265,62 @@ GPC_HD uint64_t v6_hkey(const uint32_t* m, uint32_t len) {
   const uint64_t h = mix64(((uint64_t(m[0]) << 32) | m[1]) ^ (uint64_t(len + 1) * 0x9e3779b97f4a7c15ull));
   return mix64(h ^ ((uint64_t(m[2]) << 32) | m[3]));
 }
-// code(a) for the address words a[0..3] (a[0] = most significant).
-GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a) {
+// code(a_k) for K addresses at once (a[k][0..3], [0] = most significant): the K binary searches run
+// in lock step (the step count is the same for every address up to one), so each step issues the
+// 2K bucket loads before any compare -- K independent dependency chains per lane instead of K in a row.
+template <int K>
+GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)[4], uint32_t* code) {
   const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
   const uint32_t mask = (1u << L->hash_log2) - 1u;
-  uint32_t best = 0;
-  int lo = 0, hi = int(L->n_lens) - 1;
-  while (lo <= hi) {
-    const int mid = (lo + hi) >> 1;
-    const uint32_t len = L->lens[mid];
-    uint32_t m[4];
-    v6_mask(a, len, m);
-    const uint64_t hk = v6_hkey(m, len);
-    const uint32_t* b1 = blob + L->hash_off + size_t(hash_b1(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
-    const uint32_t* b2 = blob + L->hash_off + size_t(hash_b2(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
-    GPC_TOUCH(b1, 64);
-    GPC_TOUCH(b2, 64);
-    bool hit = false;
+  int lo[K], hi[K];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t* w = (c < 2 ? b1 : b2) + (c & 1) * kV6SlotWords;
-      if (w[4] == (len | kV6Valid) && w[0] == m[0] && w[1] == m[1] && w[2] == m[2] && w[3] == m[3]) {
-        hit = true;
-        best = w[5];
+  for (int k = 0; k < K; k++) {
+    code[k] = 0;
+    lo[k] = 0;
+    hi[k] = int(L->n_lens) - 1;
+  }
+  while (true) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) any |= lo[k] <= hi[k];
+    if (!any) break;
+    uint32_t len[K], m[K][4];
+    const uint32_t* b[K][2];
+#pragma unroll
+    for (int k = 0; k < K; k++) {  // finished addresses re-probe their last length (result unused)
+      const int mid = lo[k] <= hi[k] ? (lo[k] + hi[k]) >> 1 : 0;
+      len[k] = L->lens[mid];
+      v6_mask(a[k], len[k], m[k]);
+      const uint64_t hk = v6_hkey(m[k], len[k]);
+      b[k][0] = blob + L->hash_off + size_t(hash_b1(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
+      b[k][1] = blob + L->hash_off + size_t(hash_b2(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
+      if (lo[k] <= hi[k]) {
+        GPC_TOUCH(b[k][0], 64);
+        GPC_TOUCH(b[k][1], 64);
       }
     }
-    if (hit) lo = mid + 1;
-    else hi = mid - 1;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      if (lo[k] > hi[k]) continue;
+      const int mid = (lo[k] + hi[k]) >> 1;
+      bool hit = false;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t* w = b[k][c >> 1] + (c & 1) * kV6SlotWords;
+        if (w[4] == (len[k] | kV6Valid) && w[0] == m[k][0] && w[1] == m[k][1] && w[2] == m[k][2] && w[3] == m[k][3]) {
+          hit = true;
+          code[k] = w[5];
+        }
+      }
+      if (hit) lo[k] = mid + 1;
+      else hi[k] = mid - 1;
+    }
   }
-  return best;
+}
+GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a) {
+  uint32_t aa[1][4] = {{a[0], a[1], a[2], a[3]}}, c;
+  v6_codes<1>(blob, lpm_off, aa, &c);
+  return c;
 }
 // 16 network-order bytes -> 4 host words, most significant first.
 GPC_HD void v6_words(const uint8_t* p, uint32_t* a) {

@@ -309,7 +309,7 @@ def main():
                    "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
                    "verdict_mix": mix, "build_s": round(t_build, 1)},
-        "kernel_ms": round(kern_ms, 3),  # both stage launches of a step (HIP events on the launch stream)
+        "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)
         "launches_per_step": 1 if getattr(wl, "services", None) else 2,
         "roofline": roofline,
         "cpu_baseline": cpu,

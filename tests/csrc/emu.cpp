@@ -93,10 +93,18 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pk
     v6_words(col + 16 * i, a);
     return v6_code(blob, h->v6_lpm, a);
   };
+  auto code2 = [&](const uint8_t* c0, const uint8_t* c1, size_t i, uint32_t* c) {  // the kernel's paired LPM
+    uint32_t a[2][4];
+    v6_words(c0 + 16 * i, a[0]);
+    v6_words(c1 + 16 * i, a[1]);
+    v6_codes<2>(blob, h->v6_lpm, a, c);
+  };
   for (size_t i = 0; i < n; i++) {
     g_lines.clear();
     g_line_site.clear();
-    const uint32_t src = code(pk->src6, i), dst = code(pk->dst6, i);
+    uint32_t sd[2];
+    code2(pk->src6, pk->dst6, i, sd);
+    const uint32_t src = sd[0], dst = sd[1];
     const uint32_t ct_src = pk->ct_src6 ? code(pk->ct_src6, i) : src, ct_dst = pk->ct_dst6 ? code(pk->ct_dst6, i) : dst;
     const uint32_t dest = pk->dest ? pk->dest[i] : 0u;
     Pkt p;
