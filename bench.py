@@ -294,6 +294,10 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_per_packet": round(traffic / n, 1) if traffic else None,
+                # measured HBM-side rate (PMC bytes of a step / kernel time): what the DRAM actually
+                # moved, as opposed to `achieved`, which prices every image line the algorithm touches
+                "traffic_gbs": round(traffic / (kern_ms / 1e3) / 1e9, 1) if traffic else None,
+                "traffic_frac": round(traffic / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "pmc_kb_raw": pmc or None,
                 "bytes_per_packet_alg": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
                 "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
