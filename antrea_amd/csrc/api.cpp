@@ -47,6 +47,7 @@ struct DevImage {  // one uploaded image (freed when the last epoch using it ret
   uint32_t* d_blob = nullptr;
   size_t bytes = 0;
   hipStream_t s = nullptr;
+  uint8_t sort_table[2] = {0, 0};       // per policy stage: the table whose scan length orders lanes
   ~DevImage() {
     dev_free(d_hdr, s);
     dev_free(d_blob, s);
@@ -127,6 +128,7 @@ struct gpc_ctx {
   size_t stage_bytes = 0;
   unsigned long long* d_counters = nullptr;
   size_t counter_cap = 0;  // slots
+  uint32_t counter_copies = 1;  // striped copies of the counter array (counter_copies_for)
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
   uint64_t epoch = 0, n_full = 0, n_delta = 0, n_bg = 0;
@@ -148,6 +150,71 @@ static void log_op(gpc_ctx* ctx, Op&& op) {
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : -GPC_EDEV; }
 
+// Per-rule counters are device-scope 64-bit atomics; with few rules (C1: 30 slots) every packet's
+// update lands on a handful of addresses and serializes (64 M packets: 137 ms with counters vs
+// 8.5 ms without). The array is therefore striped over `copies` replicas (block b updates copy
+// b mod copies), sized so the replicas together span >= 64 K slots, and folded into copy 0 before
+// anything reads it (gpc_counters, gpc_metrics). Large rule sets (C3: 89 k slots) keep one copy.
+static uint32_t counter_copies_for(size_t cap) {
+  if (const char* e = std::getenv("GPC_COUNTER_COPIES")) {  // experiments: fixed power of two <= 64
+    uint32_t r = 1;
+    while (r < 64 && r * 2 <= uint32_t(std::atoi(e))) r <<= 1;
+    return r;
+  }
+  uint32_t r = 1;
+  while (r < 64 && cap * r < 65536) r <<= 1;
+  return r;
+}
+static int fold_counters(gpc_ctx* ctx) {  // caller holds ctl; device synchronized on return
+  if (!ctx->d_counters || ctx->counter_copies <= 1) return GPC_OK;
+  if (hip_ok(hipSetDevice(ctx->cfg.device)) || hip_ok(hipDeviceSynchronize())) return -GPC_EDEV;
+  int rc = launch_fold_counters(ctx->d_counters, uint64_t(ctx->counter_cap) * kCounterWords, ctx->counter_copies, nullptr);
+  if (!rc) rc = hip_ok(hipDeviceSynchronize());
+  return rc;
+}
+
+// Lane regrouping (classify.hip sorted_index) pays when a stage's main table has long driver lists:
+// it costs a second round of bucket lookups and a block barrier ahead of the table work, and saves
+// the gap between a wave's longest and average scan. Per stage: the table with the most soft rules,
+// if its entry-weighted mean bucket length (sum len^2 / sum len over the sub-index buckets of the
+// shorter driver clause) reaches kLaneSortMinList. Measured on MI355X: C2 (statistic ~35) 33.4 -> 28.2 ms
+// with it, C3 (statistic ~4: one clause has short lists) 14.6 -> 20.1 ms, so C3 runs without.
+constexpr double kLaneSortMinList = 16.0;
+static void lane_sort_tables(const HostImage& h, uint8_t* sort_table) {
+  for (int st = 0; st < 2; st++) {
+    sort_table[st] = 0;
+    uint32_t best = 0, bt = 0;
+    for (int t = 3 * st; t < 3 * st + 3; t++) {
+      const uint32_t soft = h.hdr.t[t].n_rules - h.hdr.t[t].n_hard;
+      if (soft > best) {
+        best = soft;
+        bt = uint32_t(t + 1);
+      }
+    }
+    if (!bt) continue;
+    const TableHdr& th = h.hdr.t[bt - 1];
+    double mean[2];
+    for (int k = 0; k < 2; k++) {
+      double s1 = th.always_n[k], s2 = double(th.always_n[k]) * th.always_n[k];
+      for (uint32_t i = 0; i < th.n_idx[k]; i++) {
+        const SubIdx& si = th.idx[k][i];
+        const uint32_t* o = h.blob.data() + si.off;
+        for (uint64_t b = 0; b < (1ull << si.bits); b++) {
+          const double len = double(o[b + 1] - o[b]);
+          s1 += len;
+          s2 += len * len;
+        }
+      }
+      mean[k] = s1 > 0 ? s2 / s1 : 1e30;
+    }
+    const char* force = std::getenv("GPC_LANE_SORT");  // experiments: "1" forces regrouping on, "0" off
+    if (force ? force[0] == '1' : std::min(mean[0], mean[1]) >= kLaneSortMinList) sort_table[st] = uint8_t(bt);
+    if (std::getenv("GPC_IMAGE_DEBUG"))
+      std::fprintf(stderr, "lane sort: stage %d table %u mean lists %.1f %.1f -> %s\n", st + 1, bt, mean[0], mean[1],
+                   sort_table[st] ? "on" : "off");
+  }
+}
+
 static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevImage>* out) {
   auto d = std::make_shared<DevImage>();
   d->s = s;
@@ -156,6 +223,7 @@ static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevIm
       hip_ok(hipMemcpyAsync(d->d_blob, h.blob.data(), d->bytes, hipMemcpyHostToDevice, s)) ||
       hip_ok(hipMemcpyAsync(d->d_hdr, &h.hdr, sizeof(ImageHdr), hipMemcpyHostToDevice, s)))
     return -GPC_EDEV;
+  lane_sort_tables(h, d->sort_table);
   *out = std::move(d);
   return GPC_OK;
 }
@@ -595,7 +663,9 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   if (!ctx->cur.base) return -GPC_EINVAL;  // nothing committed yet
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
   EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.jhdr ? ctx->cur.pool->d_blob : nullptr, ctx->cur.jhdr,
-               ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr};
+               ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr, 0u,
+               {ctx->cur.base->sort_table[0], ctx->cur.base->sort_table[1]},
+               uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count, st);
   if (rc || n == 0) return rc;
@@ -616,7 +686,8 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   std::lock_guard<std::mutex> d(ctx->data);
   if (!ctx->cur.v6) return -GPC_EINVAL;  // IPv6 disabled or nothing committed yet
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm};
+  EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm, {0, 0},
+               uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
   int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, st);
   if (rc || n == 0) return rc;
@@ -717,6 +788,7 @@ int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verd
 int gpc_counters(gpc_ctx* ctx, uint64_t** dev, const uint32_t** slot_conj, size_t* n_slots) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
+  if (int rc = fold_counters(ctx)) return rc;  // the caller sees one array (copy 0)
   if (dev) *dev = reinterpret_cast<uint64_t*>(ctx->d_counters);
   if (slot_conj) *slot_conj = ctx->slot_conj.data();
   if (n_slots) *n_slots = ctx->slot_conj.size();
@@ -728,7 +800,9 @@ int gpc_reset_counters(gpc_ctx* ctx) {
   std::lock_guard<std::mutex> g(ctx->ctl);
   if (!ctx->d_counters) return GPC_OK;
   if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  if (hip_ok(hipDeviceSynchronize()) || hip_ok(hipMemset(ctx->d_counters, 0, ctx->counter_cap * kCounterBytes))) return -GPC_EDEV;
+  if (hip_ok(hipDeviceSynchronize()) ||
+      hip_ok(hipMemset(ctx->d_counters, 0, ctx->counter_cap * kCounterBytes * ctx->counter_copies)))
+    return -GPC_EDEV;
   return GPC_OK;
 }
 
@@ -736,6 +810,7 @@ int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   std::vector<unsigned long long> h(ctx->slot_conj.size() * kCounterWords, 0);
+  if (int rc = fold_counters(ctx)) return rc;
   if (ctx->d_counters && !h.empty()) {
     if (hip_ok(hipSetDevice(ctx->cfg.device)) || hip_ok(hipDeviceSynchronize()) ||
         hip_ok(hipMemcpy(h.data(), ctx->d_counters, h.size() * 8, hipMemcpyDeviceToHost)))
@@ -997,14 +1072,20 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   size_t need = ctx->slots.size() ? ctx->slots.size() : 1;
   unsigned long long* nc = ctx->d_counters;
   bool grow = need > ctx->counter_cap;
+  const size_t new_cap = grow ? std::max(need, ctx->counter_cap * 2) : ctx->counter_cap;
+  const uint32_t new_copies = grow ? counter_copies_for(new_cap) : ctx->counter_copies;
   if (grow) {
-    size_t cap = std::max(need, ctx->counter_cap * 2);
-    if (hip_ok(hipMalloc(&nc, cap * kCounterBytes)) || hip_ok(hipMemset(nc, 0, cap * kCounterBytes))) {
+    const size_t bytes = new_cap * kCounterBytes * new_copies;
+    if (hip_ok(hipMalloc(&nc, bytes)) || hip_ok(hipMemset(nc, 0, bytes))) {
       RetiredEpoch{std::move(ne)}.release(us);
       return -GPC_EDEV;
     }
-    if (ctx->d_counters) {
-      (void)hipDeviceSynchronize();
+    if (ctx->d_counters) {  // carry the totals over in copy 0
+      if ((rc = fold_counters(ctx))) {
+        RetiredEpoch{std::move(ne)}.release(us);
+        (void)hipFree(nc);
+        return rc;
+      }
       (void)hipMemcpy(nc, ctx->d_counters, ctx->counter_cap * kCounterBytes, hipMemcpyDeviceToDevice);
     }
   }
@@ -1021,7 +1102,8 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (grow) {
       old_counters = ctx->d_counters;
       ctx->d_counters = nc;
-      ctx->counter_cap = std::max(need, ctx->counter_cap * 2);
+      ctx->counter_cap = new_cap;
+      ctx->counter_copies = new_copies;
     }
   }
   // the previous epoch is freed once every stream that launched on it has passed that launch
@@ -1031,7 +1113,9 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     (void)hipFree(old_counters);
   }
   for (uint32_t s : ctx->released_slots)
-    if (s < ctx->counter_cap) (void)hipMemsetAsync(ctx->d_counters + kCounterWords * size_t(s), 0, kCounterBytes, us);
+    if (s < ctx->counter_cap)
+      for (uint32_t r = 0; r < ctx->counter_copies; r++)
+        (void)hipMemsetAsync(ctx->d_counters + kCounterWords * (size_t(r) * ctx->counter_cap + s), 0, kCounterBytes, us);
   ctx->released_slots.clear();
   return GPC_OK;
 }

@@ -51,12 +51,65 @@ __device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_
   return c;
 }
 
+// Lane regrouping for a policy stage launch: the candidate scan of a wavefront runs as long as its
+// longest lane (the wave-uniform trip count of eval_part), so when the host saw long driver lists
+// in the stage's main table (api.cpp lane_sort_tables) the block's packets are regrouped by their
+// scan length in that table before any table work: a counting sort of 256 lanes over 64 length
+// bins in LDS, then lane t classifies the packet perm[t] of its block. Verdicts and counters are
+// per packet, so the order never shows. Every thread of the block calls this (barriers); returns
+// the packet index this lane now owns (>= n: none).
+template <int kStage>
+__device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n,
+                                                 const uint4* __restrict__ out, uint64_t i) {
+  constexpr uint32_t kBins = 64;  // one wavefront scans the histogram
+  __shared__ uint32_t hist[kBins];
+  __shared__ uint16_t perm[kBlock];
+  const uint32_t tid = threadIdx.x;
+  uint32_t est = 0;
+  if (i < n) {
+    bool live = true;
+    if (kStage == 2) {  // packets the ingress launch settles without table work weigh nothing
+      const uint32_t ea = out[i].y & 0xffu;
+      live = ea != RV_DROP && ea != RV_REJECT && ea != RV_ISO_DROP && !(pk.dest && pk.dest[i]);
+    }
+    if (live) {
+      const uint32_t src = pk.src[i], dst = pk.dst[i];
+      Pkt p;
+      make_axes(p, src, dst, pk.sport[i], pk.dport[i], pk.proto[i], pk.out_port[i], pk.in_port ? pk.in_port[i] : 0u,
+                pk.svc_group ? pk.svc_group[i] : 0u, pk.tun_id ? pk.tun_id[i] : 0u, pk.ct_src ? pk.ct_src[i] : src,
+                pk.ct_dst ? pk.ct_dst[i] : dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+      const Img im{ep.blob, ep.hdr, nullptr, nullptr};
+      est = scan_estimate(im, ep.sort_table[kStage - 1], p);
+    }
+  }
+  const uint32_t bin = est >> 1 < kBins - 1 ? est >> 1 : kBins - 1;
+  if (tid < kBins) hist[tid] = 0;
+  __syncthreads();
+  const uint32_t r = atomicAdd(&hist[bin], 1u);
+  __syncthreads();
+  if (tid < kBins) {  // exclusive prefix sum over the bins
+    const uint32_t v = hist[tid];
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < kBins; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, kBins);
+      if (tid >= d) x += y;
+    }
+    hist[tid] = x - v;
+  }
+  __syncthreads();
+  perm[hist[bin] + r] = uint16_t(tid);
+  __syncthreads();
+  return uint64_t(blockIdx.x) * kBlock + perm[tid];
+}
+
 // kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
-template <bool kDelta, bool kSvc, int kStage, bool kV6 = false>
+template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count) {
   uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, i);  // its own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
   uint4 prev = make_uint4(0u, 0u, 0u, 0u);
@@ -127,7 +180,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVE
   PacketOut o = classify_packet<kDelta, kStage>(im, p, dest);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
-    count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&counters[w], v); });
+    unsigned long long* const copy = counters + size_t(blockIdx.x & ep.ctr_mask) * ep.ctr_stride;
+    count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&copy[w], v); });
   }
   const VerdictOut e = o.e, g = o.g;
   if (kStage == 2) out[i] = make_uint4(prev.x, prev.y, g.conj, g.packed);
@@ -144,10 +198,33 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
                        reinterpret_cast<uint4*>(out), lb_out, counters, count);
     return;
   }
-  hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), lb_out, counters, count);
-  hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), lb_out, counters, count);
+  if (ep.sort_table[0])
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep,
+                       pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
+  else
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                       reinterpret_cast<uint4*>(out), lb_out, counters, count);
+  if (ep.sort_table[1])
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep,
+                       pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
+  else
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
+                       reinterpret_cast<uint4*>(out), lb_out, counters, count);
+}
+
+__global__ void fold_counters_kernel(unsigned long long* __restrict__ c, uint64_t stride, uint32_t copies) {
+  const uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (w >= stride) return;
+  // atomics: a classification running concurrently on another stream loses no update
+  unsigned long long sum = 0;
+  for (uint32_t r = 1; r < copies; r++) sum += atomicExch(&c[r * stride + w], 0ull);
+  if (sum) atomicAdd(&c[w], sum);
+}
+
+int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t copies, hipStream_t stream) {
+  if (!counters || copies <= 1 || stride == 0) return 0;
+  hipLaunchKernelGGL(fold_counters_kernel, dim3(uint32_t((stride + 255) / 256)), dim3(256), 0, stream, counters, stride, copies);
+  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,

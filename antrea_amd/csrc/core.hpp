@@ -510,6 +510,23 @@ GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
   return l4 & bl & iv;
 }
 
+// Scan length of one table for the packet (the driver clause's candidate count, as eval_part picks
+// it): the kernel can group lanes of similar length into the same wavefront (classify.hip).
+GPC_HD uint32_t scan_estimate(const Img& im, uint32_t table, const Pkt& p) {
+  const TableHdr& th = im.hdr->t[table - 1];
+  uint32_t cnt[2] = {th.always_n[0], th.always_n[1]};
+#pragma unroll
+  for (int k = 0; k < 2; k++)
+#pragma unroll
+    for (int i = 0; i < kIdxPerClause; i++) {
+      if (uint32_t(i) >= th.n_idx[k]) break;
+      const SubIdx& si = th.idx[k][i];
+      const uint32_t* o = im.blob + si.off + bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
+      cnt[k] += o[1] - o[0];
+    }
+  return cnt[0] < cnt[1] ? cnt[0] : cnt[1];
+}
+
 constexpr int kLists = kIdxPerClause + 1;  // always list + sub-indexes of the driver clause
 #ifndef GPC_SCAN_UNROLL
 #define GPC_SCAN_UNROLL 4
@@ -1067,8 +1084,8 @@ GPC_HD void count_packet(const PacketOut& o, uint32_t len, uint32_t ct_state, Ad
 }
 
 // Column loads -> axes (kernel and emulation share the defaults of gpc_pkt_soa).
-GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto, uint32_t out_port,
-                     uint32_t in_port, uint32_t svc_group, uint32_t tun_id, uint32_t ct_src, uint32_t ct_dst, uint32_t ct_state) {
+GPC_HD void make_axes(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto, uint32_t out_port,
+                      uint32_t in_port, uint32_t svc_group, uint32_t tun_id, uint32_t ct_src, uint32_t ct_dst, uint32_t ct_state) {
   p.ax[AX_SRC] = src;
   p.ax[AX_DST] = dst;
   p.ax[AX_CTSRC] = ct_src;
@@ -1081,6 +1098,10 @@ GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_
   p.ax[AX_L4D] = (proto << 16) | (ported ? dport : 0u);
   p.ax[AX_L4S] = (proto << 16) | (ported ? sport : 0u);
   p.ax[AX_CTST] = ct_state;
+}
+GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto, uint32_t out_port,
+                     uint32_t in_port, uint32_t svc_group, uint32_t tun_id, uint32_t ct_src, uint32_t ct_dst, uint32_t ct_state) {
+  make_axes(p, src, dst, sport, dport, proto, out_port, in_port, svc_group, tun_id, ct_src, ct_dst, ct_state);
 #pragma unroll
   for (uint32_t a = 0; a < 8; a++) p.fm[a] = filt_pkt_axis(a, p.ax[a]);
   p.l4m = filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12) |

@@ -15,7 +15,12 @@ struct EpochArgs {
   uint32_t jhdr;          // JournalHdr word offset of this epoch
   const uint32_t* svc;    // null: no Services (AntreaProxy stage skipped)
   uint32_t v6_lpm;        // IPv6 image: word offset of its V6Lpm block (host copy of ImageHdr.v6_lpm)
+  uint8_t sort_table[2];  // per policy stage launch: table (1-6) whose scan length groups lanes, 0 = none
+  uint32_t ctr_stride;    // per-rule counters: words per copy (counter_cap * kCounterWords)
+  uint32_t ctr_mask;      // number of striped copies - 1 (a block updates copy blockIdx & mask)
 };
+// Sums counter copies 1..copies-1 into copy 0 and zeroes them (stride words per copy).
+int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t copies, hipStream_t stream);
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, hipStream_t stream);
 // IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).

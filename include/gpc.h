@@ -374,7 +374,9 @@ int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_ve
 /* Per-rule counters as a device buffer of n_slots x {packets, bytes, sessions} uint64 (for an
  * RCCL all-reduce by the caller), plus the slot -> conj id map (host, valid until the next commit).
  * Sessions as the Metric flows count them: ct_state=+new packets for allow rules, every packet for
- * deny rules (pipeline.go:1604-1670, network_policy.go:1917-1980). */
+ * deny rules (pipeline.go:1604-1670, network_policy.go:1917-1980). Internally the kernels update
+ * striped replicas of the array (few rules: many same-address atomics); this call folds them into
+ * the returned buffer (synchronizes the device), so call it again to see later classifications. */
 int gpc_counters(gpc_ctx* ctx, uint64_t** dev_counters, const uint32_t** slot_conj, size_t* n_slots);
 int gpc_reset_counters(gpc_ctx* ctx);
 
