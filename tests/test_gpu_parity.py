@@ -75,11 +75,11 @@ def test_gpu_counters_match_oracle_metrics():
     assert {k: v for k, v in got_m.items()} == {k: v for k, v in want_m.items()}
 
 
-def test_gpu_counters_wave_aggregated_c2():
-    """Full C2 (1k rules, 876 counter slots: many lanes of a wave hit the same rule, so the
-    kernel's wave-aggregated counter updates do real merging): per-rule packets / bytes /
-    sessions equal the host emulation's per-packet accumulation, with a random len column and
-    a mix of +new / -new packets."""
+def test_gpu_counters_striped_c2():
+    """Full C2 (1k rules, 876 counter slots, so the kernel stripes its atomics over 64 replicas of
+    the counter array and gpc_counters folds them): per-rule packets / bytes / sessions equal the
+    host emulation's per-packet accumulation, with a random len column and a mix of +new / -new
+    packets."""
     wl = workload.config2()
     n = 300_000
     cols = workload.gen_packets(wl, n, seed=7)
@@ -94,6 +94,28 @@ def test_gpu_counters_wave_aggregated_c2():
     exp = {conj: tuple(int(x) for x in arr[i]) for i, conj in enumerate(slots) if conj and arr[i].any()}
     assert len(exp) > 50 and sum(v[0] for v in exp.values()) > n // 20
     assert {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)} == exp
+
+
+def test_gpu_counters_fold_accumulates_and_resets():
+    """C1 (30 counter slots: 64 striped replicas): metrics read between two counted batches fold
+    the replicas without losing or double-counting (second read = both batches), and
+    gpc_reset_counters clears every replica."""
+    wl = workload.config1(seed=9)
+    n = 50_000
+    cols = workload.gen_packets(wl, n, seed=9)
+    cols["len"] = np.random.default_rng(9).integers(0, 65536, n).astype(np.uint16)
+    got, c = _gpu(wl.rules, cols, count=True)
+    _, slots = c.counters()
+    arr = np.zeros((len(slots), 3), dtype=np.uint64)
+    emu.classify(c, cols, counters=arr)
+    one = {conj: tuple(int(x) for x in arr[i]) for i, conj in enumerate(slots) if conj and arr[i].any()}
+    assert one and {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)} == one
+    c.classify_host(cols, count=True)
+    two = {k: tuple(2 * x for x in v) for k, v in one.items()}
+    assert {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)} == two
+    c.reset_counters()
+    c.classify_host(cols, count=True)
+    assert {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)} == one
 
 
 def test_gpu_matches_image_emulation_large():
