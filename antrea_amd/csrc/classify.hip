@@ -16,9 +16,15 @@ namespace gpc {
 #define GPC_WAVES_PER_EU 6
 #endif
 #ifndef GPC_BLOCK
-#define GPC_BLOCK 256
+#define GPC_BLOCK 64
 #endif
+// One wavefront per block for the plain kernels (C3: 14.73 ms at 256 threads, 14.36 at 128, 14.24
+// at 64 -- finished waves free their slot without waiting for block siblings); the lane-regrouping
+// kernels sort 256 packets across 4 waves, which needs the larger block.
 constexpr int kBlock = GPC_BLOCK;
+constexpr int kSortBlock = 256;
+template <bool kSort>
+constexpr int block_threads() { return kSort ? kSortBlock : kBlock; }
 
 // kDelta = false: a base-only epoch (no tombstones, no journal); kSvc = false: no Services. The
 // machinery of either folds away at compile time so the common case pays nothing for it.
@@ -63,7 +69,7 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
                                                  const uint4* __restrict__ out, uint64_t i) {
   constexpr uint32_t kBins = 64;  // one wavefront scans the histogram
   __shared__ uint32_t hist[kBins];
-  __shared__ uint16_t perm[kBlock];
+  __shared__ uint16_t perm[kSortBlock];
   const uint32_t tid = threadIdx.x;
   uint32_t est = 0;
   if (i < n) {
@@ -100,15 +106,15 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
   __syncthreads();
   perm[hist[bin] + r] = uint16_t(tid);
   __syncthreads();
-  return uint64_t(blockIdx.x) * kBlock + perm[tid];
+  return uint64_t(blockIdx.x) * kSortBlock + perm[tid];
 }
 
 // kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
 template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
+__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count) {
-  uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  uint64_t i = uint64_t(blockIdx.x) * block_threads<kSort>() + threadIdx.x;
   if (kSort) i = sorted_index<kStage>(ep, pk, n, out, i);  // its own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
@@ -198,15 +204,16 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
                        reinterpret_cast<uint4*>(out), lb_out, counters, count);
     return;
   }
+  const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
   if (ep.sort_table[0])
-    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep,
-                       pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
+                       ep, pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
                        reinterpret_cast<uint4*>(out), lb_out, counters, count);
   if (ep.sort_table[1])
-    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep,
-                       pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
+                       ep, pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
                        reinterpret_cast<uint4*>(out), lb_out, counters, count);
