@@ -6,9 +6,14 @@
 hipcc cross-compiles the kernel for gfx950 without a GPU; host C++ (compiler.cpp, image.cpp) is
 compiled with the same toolchain. The .so is git-ignored but travels to the GPU box in the gpurun
 snapshot (it is not listed in .gpurunignore).
+
+Rebuilds are decided by content, not mtime: every object carries a stamp file with the SHA-256 of
+its compile command, source and headers, so a snapshot whose sources differ from the ones a
+travelling .so was built from is rebuilt, and one that matches is not.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -23,15 +28,30 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HOST_SRCS = ["compiler.cpp", "image.cpp", "flowtext.cpp", "service.cpp"]
 HIP_SRCS = ["classify.hip", "api.cpp"]
-HEADERS = ["model.hpp", "compiler.hpp", "core.hpp", "image.hpp", "launch.hpp", "service.hpp"]
+HEADERS = ["model.hpp", "compiler.hpp", "core.hpp", "image.hpp", "launch.hpp", "oplog.hpp", "service.hpp"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 
-def _newer(dst, srcs):
-    if not os.path.exists(dst):
+def _digest(cmd, srcs):
+    h = hashlib.sha256(" ".join(cmd).encode())
+    for s in srcs:
+        with open(s, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stale(dst, cmd, srcs):
+    """True when dst is missing or was built from other inputs (its .sha256 stamp differs)."""
+    stamp = dst + ".sha256"
+    if not os.path.exists(dst) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(dst)
-    return any(os.path.getmtime(s) > t for s in srcs)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(cmd, srcs)
+
+
+def _stamp(dst, cmd, srcs):
+    with open(dst + ".sha256", "w") as f:
+        f.write(_digest(cmd, srcs) + "\n")
 
 
 def _run(cmd):
@@ -50,21 +70,27 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", defines
     for s in HOST_SRCS:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OUT, s + ".o")
-        if force or _newer(obj, [src] + hdrs):
-            _run(["g++"] + CXXFLAGS + ["-c", src, "-o", obj])
+        cmd = ["g++"] + CXXFLAGS + ["-c", src, "-o", obj]
+        if force or _stale(obj, cmd, [src] + hdrs):
+            _run(cmd)
+            _stamp(obj, cmd, [src] + hdrs)
         objs.append(obj)
     for s in HIP_SRCS:
         src = os.path.join(CSRC, s)
         tag = "_" + variant if (variant and s.endswith(".hip")) else ""
         obj = os.path.join(OUT, s + tag + ".o")
-        if force or _newer(obj, [src] + hdrs):
-            lang = ["-x", "hip"] if s.endswith(".hip") else []
-            dfl = ["-D" + d for d in defines] if s.endswith(".hip") else []
-            _run([HIPCC, "--offload-arch=" + ARCH] + CXXFLAGS + dfl + lang + ["-c", src, "-o", obj])
+        lang = ["-x", "hip"] if s.endswith(".hip") else []
+        dfl = ["-D" + d for d in defines] if s.endswith(".hip") else []
+        cmd = [HIPCC, "--offload-arch=" + ARCH] + CXXFLAGS + dfl + lang + ["-c", src, "-o", obj]
+        if force or _stale(obj, cmd, [src] + hdrs):
+            _run(cmd)
+            _stamp(obj, cmd, [src] + hdrs)
         objs.append(obj)
     lib = os.path.join(OUT, "libgpc_%s.so" % variant) if variant else LIB
-    if force or _newer(lib, objs):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs
+    if force or _stale(lib, cmd, objs):
+        _run(cmd)
+        _stamp(lib, cmd, objs)
     if verbose:
         print(lib)
     return lib

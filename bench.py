@@ -12,13 +12,20 @@ latency (op due -> commit returned) percentiles next to the Mpps measured under 
 One process per GPU (torchrun for N > 1). Each rank builds the same rule set (C3 = 100k rules),
 classifies its own packet shard (weak scaling: `--packets` per GPU, inputs resident in HBM before
 the timed region) and, when counters are on, all-reduces the per-rule counters over RCCL at the
-end of the run (the only collective of the path). A step = one gpc_classify launch
-over the whole per-GPU batch. Rank 0 prints one JSON line.
+end of the run (the only collective of the path). A step = one gpc_classify call
+over the whole per-GPU batch (two kernel launches without Services: egress stage, ingress stage).
+
+Rank 0 at N = 1 also (all after the timed region, none of it timed):
+  * parity: a 64k-packet strided sample of the timed batch and its device verdicts are checked
+    packet for packet against the C oracle (oracle/ovs_cls.c over the ORACLE compiler's flows),
+    which a spawned CPU process prepares while the GPU works -> "parity": {checked, mismatches};
+  * cpu_baseline: the same C oracle timed on the host cores (bounded sample, see oracle/parity.py);
+  * roofline: measured L2<->fabric bytes per step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate
+    child passes, MI355X_MICROARCH.md HBM section) / kernel time, against 8 TB/s.
 """
 from __future__ import annotations
 
 import argparse
-import copy
 import json
 import os
 import sys
@@ -28,11 +35,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+PARITY_SAMPLE = 1 << 16
+# rocprofv3 passes (one run each: FETCH_SIZE takes 3 of the 4 TCC counter slots)
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"))
+
+
+def _log(msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    print("[bench %.0fs] %s" % (time.time() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.time()
 
 
 def _lbar(wl, clf, n=20000, family=4):
     """Mean distinct 64-B image lines one packet's evaluation reads (instrumented host emulation of
-    the same image, tests/csrc/emu.cpp), i.e. L-bar of SURVEY §8(d)."""
+    the same image, tests/csrc/emu.cpp), i.e. L-bar of SURVEY §8(d) -- a diagnostic of the
+    algorithm, not a measured byte count."""
     try:
         from tests import emu
         from antrea_amd import workload
@@ -46,15 +65,6 @@ def _lbar(wl, clf, n=20000, family=4):
         return s[6] / max(1, s[7])
     except Exception as e:  # pragma: no cover - g++ missing
         print("L-bar unavailable: %s" % e, file=sys.stderr)
-        return None
-
-
-def _cpu_baseline(wl, seconds):
-    try:
-        from oracle import cbaseline
-        return cbaseline.run(wl, seconds)
-    except Exception as e:
-        print("cpu baseline unavailable: %s" % e, file=sys.stderr)
         return None
 
 
@@ -94,10 +104,11 @@ def _churn_loop(clf, wl, rate, max_batch, stop, rec, seed):
         issued += due
 
 
-def _pmc_pass(counter, args):
+def _pmc_pass(counters, args):
     """One rocprofv3 PMC pass over a short child run of this bench (same workload and packet
-    count, counters as configured); returns the mean per-launch counter value of classify_kernel.
-    Run before this process touches the GPU (the child is a separate process, not an exec)."""
+    count, counters as configured). Returns {counter: mean value per step} plus the per-kernel
+    means ("by_kernel"). Run before this process touches the GPU (the child is a separate
+    process, not an exec)."""
     import csv
     import glob
     import shutil
@@ -106,28 +117,84 @@ def _pmc_pass(counter, args):
     if not shutil.which("rocprofv3"):
         return None
     d = tempfile.mkdtemp(prefix="gpc_pmc_")
-    cmd = ["rocprofv3", "--pmc", counter, "--kernel-include-regex", "classify_kernel", "-d", d, "-o", "pmc",
-           "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline", "--no-traffic", "--config", args.config, "--packets", str(args.packets),
-           "--family", str(args.family)]
+    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel", "-d", d, "-o", "pmc",
+                                                       "--output-format", "csv", "--", sys.executable,
+                                                       os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
+                                                       "--no-cpu-baseline", "--no-traffic", "--no-parity", "--config",
+                                                       args.config, "--packets", str(args.packets), "--family",
+                                                       str(args.family)]
     if args.no_count:
         cmd.append("--no-count")
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600, check=True)
-        vals = []
+        rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    if "classify_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                        vals.append(float(row["Counter_Value"]))
+                rows += [r for r in csv.DictReader(fh) if "classify_kernel" in r.get("Kernel_Name", "")]
         # one step = two launches without Services (egress stage, ingress stage), one with them
         per_step = 1.0 if args.config == "C4" else 2.0
-        return sum(vals) / (len(vals) / per_step) if vals else None
+        out, by_kernel = {}, {}
+        for c in counters:
+            vals = [float(r["Counter_Value"]) for r in rows if r.get("Counter_Name") == c]
+            if vals:
+                out[c] = sum(vals) / (len(vals) / per_step)
+            for r in rows:
+                if r.get("Counter_Name") != c:
+                    continue
+                k = by_kernel.setdefault(r["Kernel_Name"], {}).setdefault(c, [])
+                k.append(float(r["Counter_Value"]))
+        out["by_kernel"] = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in by_kernel.items()}
+        return out
     except Exception as e:
-        print("PMC pass %s failed: %s" % (counter, e), file=sys.stderr)
+        print("PMC pass %s failed: %s" % (counters, e), file=sys.stderr)
         return None
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+def _host_sample(cols, idx):
+    """Device packet columns -> numpy (unsigned dtypes) at the sample indices."""
+    import numpy as np
+    import torch
+    out = {}
+    for k, t in cols.items():
+        if t.dtype == getattr(torch, "uint32", None):
+            t = t.view(torch.int32)
+        a = t[idx].cpu().numpy()
+        out[k] = a.view({4: np.uint32, 2: np.uint16, 1: np.uint8}[a.dtype.itemsize])
+    return out
+
+
+def _roofline(pmc, kern_ms, n, b_in, b_out, lbar):
+    """Measured-bytes roofline of one step (all its launches). `achieved` = counter bytes per step
+    (FETCH_SIZE doubled on gfx950 + WRITE_SIZE; L2 <-> fabric traffic, Infinity-Cache hits
+    included, so an upper bound of the HBM bytes) / kernel time; frac <= 1 is enforced. B_alg /
+    L-bar stay as diagnostics: they price every image line the algorithm touches at
+    HBM cost although most are L2 / MALL hits."""
+    pps_kernel = n / (kern_ms / 1e3)
+    b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
+    rl = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+          "basis": "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per step (2 launches w/o Services) / HIP-event kernel time"}
+    f, w = pmc.get("FETCH_SIZE"), pmc.get("WRITE_SIZE")
+    if f is not None and w is not None:
+        traffic = (2.0 * f + w) * 1024.0  # counters are in KB
+        gbs = traffic / (kern_ms / 1e3) / 1e9
+        frac = gbs / HBM_PEAK_GBS
+        if frac > 1.0:
+            raise RuntimeError("roofline sanity: measured %.0f GB/s exceeds the HBM peak" % gbs)
+        rl.update(achieved=round(gbs, 1), frac=round(frac, 4), traffic=int(traffic),
+                  traffic_per_packet=round(traffic / n, 1))
+    hit, miss = pmc.get("TCC_HIT_sum"), pmc.get("TCC_MISS_sum")
+    if hit is not None and miss is not None and hit + miss > 0:
+        rl["l2_hit_rate"] = round(hit / (hit + miss), 4)
+        rl["l2_miss_bytes_per_packet"] = round(miss * 128.0 / n, 1)  # 128-B L2 lines
+    rl["algorithmic"] = {"bytes_per_packet": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
+                         "gbs_if_uncached": round(pps_kernel * b_alg / 1e9, 1),
+                         "compulsory_bytes_per_packet": b_in + b_out,
+                         "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
+    rl["pmc_by_kernel"] = {k: {c: round(v, 1) for c, v in cs.items()} for p in pmc.get("_passes", [])
+                           for k, cs in (p or {}).get("by_kernel", {}).items()} or None
+    return rl
 
 
 def main():
@@ -140,6 +207,7 @@ def main():
     ap.add_argument("--no-count", action="store_true", help="disable per-rule counters")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed batch")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
@@ -149,23 +217,35 @@ def main():
     if args.family == 6 and args.config in ("C4", "C5"):
         ap.error("--family 6: C1-C3 only (no IPv6 AntreaProxy stage / delta epochs)")
     churn = args.config == "C5"
-    if args.config == "C4" or args.family == 6:  # the C oracle has no AntreaProxy stage / IPv6
+    if args.config == "C4":  # the C oracle has no AntreaProxy stage: no comparable CPU timing
         args.no_cpu_baseline = True
-    if churn:
+    if churn:  # the timed batch sees many epochs; see DESIGN.md for C5's correctness check
         args.no_traffic = True
         args.no_cpu_baseline = True
-
-    import torch
-    import torch.distributed as dist
+        args.no_parity = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    worker = None
+    if world == 1 and not (args.no_parity and args.no_cpu_baseline):
+        # the CPU oracle (oracle compiler + C classifier) is prepared in a spawned process while
+        # this one profiles and times the GPU; it never touches the GPU
+        from oracle.parity import OracleWorker
+        worker = OracleWorker("C3" if churn else args.config)
+
+    import torch
+    import torch.distributed as dist
+
     pmc = {}
     if world == 1 and not args.no_traffic:
-        # HBM traffic per launch (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE in
-        # separate passes (TCC slots), kilobytes; FETCH_SIZE doubled for gfx950.
-        pmc = {c: _pmc_pass(c, args) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+        passes = []
+        for c in PMC_PASSES:
+            _log("rocprofv3 PMC pass %s" % " ".join(c))
+            passes.append(_pmc_pass(c, args))
+        for p in passes:
+            pmc.update({k: v for k, v in (p or {}).items() if k != "by_kernel"})
+        pmc["_passes"] = passes
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -182,6 +262,7 @@ def main():
     if world > 1:
         dist.barrier()
 
+    _log("building the %s rule set" % args.config)
     t0 = time.time()
     wl = workload.CONFIGS["C3" if churn else args.config]()
     v6 = args.family == 6
@@ -194,9 +275,8 @@ def main():
     t_build = time.time() - t0
 
     n = args.packets
-    cols = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + rank, device=dev)
-    if v6:
-        cols = workload.packets_to_v6_torch(cols)
+    cols4 = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + rank, device=dev)
+    cols = workload.packets_to_v6_torch(cols4) if v6 else cols4
     classify = clf.classify6_device if v6 else clf.classify_device
     out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
     soa = gpc.pkt_soa_device(cols)
@@ -223,6 +303,7 @@ def main():
         while len(lat) < 5:  # control loop running before the timed region
             time.sleep(0.01)
         lat.clear()
+    _log("timed region: %d steps of %d packets" % (args.steps, n))
     t_start = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
@@ -273,35 +354,39 @@ def main():
             dist.destroy_process_group()
         return
 
-    v = out.view(torch.uint8).reshape(n, 2, 8)[: min(n, 1 << 20)].cpu().numpy()
+    import numpy as np
+    from antrea_amd.gpc import VERDICT_DTYPE
+    v8 = out.view(torch.uint8).reshape(n, 2, 8)
+    v = v8[: min(n, 1 << 20)].cpu().numpy()
     mix = {}
     names = ["NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "BYPASS"]
     for j, stage in enumerate(("egress", "ingress")):
-        import numpy as np
         a, c = np.unique(v[:, j, 4], return_counts=True)
         mix[stage] = {names[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
+
+    parity = None
+    if worker is not None and not args.no_parity:
+        idx = torch.linspace(0, n - 1, min(n, PARITY_SAMPLE), device=dev).long()
+        sample = _host_sample(cols4, idx)
+        got = np.ascontiguousarray(v8[idx].cpu().numpy()).view(VERDICT_DTYPE).reshape(-1, 2)
+        _log("parity check of %d sampled packets (waiting for the oracle process)" % len(idx))
+        parity = worker.check(sample, got)
+        parity["sample"] = "%d packets, stride %.0f over the timed batch (last step's verdicts)%s" % (
+            len(idx), n / len(idx), "; IPv6 packets vs the IPv4 oracle (fd00:10::/96 embedding)" if v6 else "")
+        if parity.get("mismatches"):
+            print("PARITY FAILURE: %s" % json.dumps(parity), file=sys.stderr)
 
     lbar = _lbar(wl, clf, family=args.family)
     b_in, b_out = (19 if getattr(wl, "services", None) else 17), 16  # +2 B len for C4
     if v6:
         b_in += 24  # 16-B instead of 4-B src / dst
-    b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
-    pps_kernel = n / (kern_ms / 1e3)
-    achieved = pps_kernel * b_alg / 1e9
-    traffic = None
-    if pmc.get("FETCH_SIZE") is not None and pmc.get("WRITE_SIZE") is not None:
-        traffic = int((2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_per_packet": round(traffic / n, 1) if traffic else None,
-                # measured HBM-side rate (PMC bytes of a step / kernel time): what the DRAM actually
-                # moved, as opposed to `achieved`, which prices every image line the algorithm touches
-                "traffic_gbs": round(traffic / (kern_ms / 1e3) / 1e9, 1) if traffic else None,
-                "traffic_frac": round(traffic / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-                "pmc_kb_raw": pmc or None,
-                "bytes_per_packet_alg": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
-                "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
-    cpu = None if (args.no_cpu_baseline or world > 1) else _cpu_baseline(wl, args.cpu_seconds)  # rank 0, N=1 only
+    roofline = _roofline(pmc, kern_ms, n, b_in, b_out, lbar)
+    cpu = None
+    if worker is not None and not args.no_cpu_baseline:  # rank 0, N=1 only
+        _log("CPU baseline (%.0f s)" % args.cpu_seconds)
+        cpu = worker.baseline(args.cpu_seconds)
+    if worker is not None:
+        worker.close()
     st = clf.image_stats()
     res = {
         "metric": "Mpps classified (5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW",
@@ -317,6 +402,7 @@ def main():
         "launches_per_step": 1 if getattr(wl, "services", None) else 2,
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "parity": parity,
     }
     if getattr(wl, "services", None):
         res["metric"] = "Mpps classified (AntreaProxy ServiceLB/EndpointDNAT + policy) @100k rules, 10k Services"

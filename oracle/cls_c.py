@@ -2,6 +2,8 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
+import zlib
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -18,15 +20,14 @@ TABLE_IDS = {"AntreaPolicyEgressRule": 1, "EgressRule": 2, "EgressDefaultRule": 
              "ConntrackCommit": 10, "Output": 11}
 A_CONJ, A_SET_REG, A_CT_COMMIT, A_GOTO, A_GROUP = 1, 2, 3, 4, 5
 
-
-class OFlow(C.Structure):
-    _fields_ = [("table", C.c_int32), ("priority", C.c_uint32), ("val", C.c_uint32 * NF), ("mask", C.c_uint32 * NF),
-                ("act_off", C.c_int32), ("n_act", C.c_int32), ("soft", C.c_int32)]
-
-
-class OAction(C.Structure):
-    _fields_ = [("kind", C.c_uint8), ("reg", C.c_uint8), ("a", C.c_uint32), ("b", C.c_uint32), ("c", C.c_uint32),
-                ("lv", C.c_uint64), ("lm", C.c_uint64)]
+# numpy twins of the C records (same layout as ocls_flow / ocls_action)
+FLOW_DT = np.dtype([("table", "<i4"), ("priority", "<u4"), ("val", "<u4", (NF,)), ("mask", "<u4", (NF,)),
+                    ("act_off", "<i4"), ("n_act", "<i4"), ("soft", "<i4"), ("sig", "<u4")])
+ACT_DT = np.dtype({"names": ["kind", "reg", "a", "b", "c", "lv", "lm"],
+                   "formats": ["u1", "u1", "<u4", "<u4", "<u4", "<u8", "<u8"],
+                   "offsets": [0, 1, 4, 8, 12, 16, 24], "itemsize": 32})
+STAT_NAMES = ("lookups", "subtables_probed", "subtables_skipped_by_trie", "soft_matches", "soft_levels",
+              "conj_actions_hashed")
 
 
 class OPkts(C.Structure):
@@ -42,89 +43,134 @@ def load():
     if _lib is None:
         _lib = C.CDLL(cbuild.build())
         _lib.ocls_create.restype = C.c_void_p
-        _lib.ocls_create.argtypes = [C.POINTER(OFlow), C.c_int, C.POINTER(OAction), C.c_int, C.c_void_p, C.c_void_p,
-                                     C.c_int]
+        _lib.ocls_create.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         _lib.ocls_destroy.argtypes = [C.c_void_p]
         _lib.ocls_classify.argtypes = [C.c_void_p, C.POINTER(OPkts), C.c_size_t, C.c_void_p, C.c_int, C.c_int]
         _lib.ocls_counters.restype = C.POINTER(C.c_uint64)
         _lib.ocls_counters.argtypes = [C.c_void_p]
+        _lib.ocls_stats.argtypes = [C.c_void_p, C.c_void_p]
+        _lib.ocls_n_subtables.argtypes = [C.c_void_p, C.c_int]
     return _lib
 
 
-def _convert(flow_lines: List[str]):
-    flows, acts, parsed = [], [], []
-    for line in flow_lines:
+def _verdict_sig(actions) -> int:
+    """Signature of a hard flow's verdict (oracle/ovs_cls.py _verdict_sig): equal-priority
+    overlapping hard flows with different signatures are a TIE."""
+    acts = [a for a in actions if a[0] in ("drop", "goto_table", "ct_commit", "group")]
+    sig = tuple(a[0] + str(a[1] if len(a) > 1 else "") for a in acts) or ("drop",)
+    return zlib.crc32(repr(sig).encode())
+
+
+def _convert_lines(flow_lines: List[str]):
+    """Flow text -> (flow records, action records, index of each kept flow in flow_lines)."""
+    flows = np.zeros(len(flow_lines), FLOW_DT)
+    acts = []
+    kept = []
+    k = 0
+    for li, line in enumerate(flow_lines):
         f = parse_flow(line)
         t = TABLE_IDS.get(f["table"], 0)
         if not (1 <= t <= 8):
             continue
         m = f["match"]
-        if any(k.startswith("ipv6") or k.startswith("ct_ipv6") for k in m) or m.get("dl_type", (0x800, 0))[0] != 0x800:
+        if any(x.startswith("ipv6") or x.startswith("ct_ipv6") for x in m) or m.get("dl_type", (0x800, 0))[0] != 0x800:
             continue  # never matches the IPv4 packets this checker classifies
-        of = OFlow()
-        of.table = t
-        of.priority = f["priority"]
+        rec = flows[k]
         ok = True
-        for k, (v, mk) in m.items():
-            if k == "ct_label":
+        for key, (v, mk) in m.items():
+            if key == "ct_label":
                 full = (1 << 64) - 1 if mk is None else mk
-                of.val[16], of.mask[16] = v & 0xFFFFFFFF, full & 0xFFFFFFFF
-                of.val[17], of.mask[17] = (v >> 32) & 0xFFFFFFFF, (full >> 32) & 0xFFFFFFFF
+                rec["val"][16], rec["mask"][16] = v & 0xFFFFFFFF, full & 0xFFFFFFFF
+                rec["val"][17], rec["mask"][17] = (v >> 32) & 0xFFFFFFFF, (full >> 32) & 0xFFFFFFFF
                 continue
-            if k not in F:
+            if key not in F:
                 ok = False
                 break
-            i = F[k]
+            i = F[key]
             if mk is None:
                 mk = 0xFFFFFFFF
-            if k == "tun_id" and v > 0xFFFFFFFF:
+            if key == "tun_id" and v > 0xFFFFFFFF:
                 ok = False
                 break
-            of.val[i] = v & mk & 0xFFFFFFFF
-            of.mask[i] = mk & 0xFFFFFFFF
+            rec["val"][i] = v & mk & 0xFFFFFFFF
+            rec["mask"][i] = mk & 0xFFFFFFFF
         if not ok:
+            rec["val"][:] = 0
+            rec["mask"][:] = 0
             continue
-        of.act_off = len(acts)
+        rec["table"] = t
+        rec["priority"] = f["priority"]
+        off = len(acts)
         soft = bool(f["actions"])
         for a in f["actions"]:
-            oa = OAction()
             if a[0] == "conjunction":
-                oa.kind, oa.a, oa.b, oa.c = A_CONJ, a[1], a[2], a[3]
-            else:
-                soft = False
-                if a[0] == "set_reg":
-                    oa.kind, oa.reg, oa.a, oa.b = A_SET_REG, a[1], a[2], 0xFFFFFFFF if a[3] is None else a[3]
-                elif a[0] == "ct_commit":
-                    oa.kind, oa.a = A_CT_COMMIT, TABLE_IDS.get(a[1], 0)
-                    if a[2]:
-                        oa.lv, oa.lm = a[2][0]
-                elif a[0] == "goto_table":
-                    oa.kind, oa.a = A_GOTO, TABLE_IDS.get(a[1], 0)
-                elif a[0] == "group":
-                    oa.kind, oa.a = A_GROUP, a[1]
-                else:
-                    continue
-            acts.append(oa)
-        of.n_act = len(acts) - of.act_off
-        of.soft = int(soft)
-        flows.append(of)
-    return flows, acts
+                acts.append((A_CONJ, 0, a[1], a[2], a[3], 0, 0))
+                continue
+            soft = False
+            if a[0] == "set_reg":
+                acts.append((A_SET_REG, a[1], a[2] & 0xFFFFFFFF, 0xFFFFFFFF if a[3] is None else a[3], 0, 0, 0))
+            elif a[0] == "ct_commit":
+                lv, lm = a[2][0] if a[2] else (0, 0)
+                acts.append((A_CT_COMMIT, 0, TABLE_IDS.get(a[1], 0), 0, 0, lv, lm))
+            elif a[0] == "goto_table":
+                acts.append((A_GOTO, 0, TABLE_IDS.get(a[1], 0), 0, 0, 0, 0))
+            elif a[0] == "group":
+                acts.append((A_GROUP, 0, a[1], 0, 0, 0, 0))
+        rec["act_off"] = off
+        rec["n_act"] = len(acts) - off
+        rec["soft"] = int(soft)
+        rec["sig"] = 0 if soft else _verdict_sig(f["actions"])
+        kept.append(li)
+        k += 1
+    return flows[:k].copy(), np.array(acts, dtype=ACT_DT) if acts else np.zeros(0, ACT_DT), kept
+
+
+def _convert_chunk(args):
+    lines, base = args
+    fl, ac, kept = _convert_lines(lines)
+    return fl, ac, [base + i for i in kept]
+
+
+def _convert(flow_lines: List[str], procs: Optional[int] = None):
+    """Parallel conversion of large dumps (a fork pool over chunks; the oracle never touches a GPU)."""
+    n = len(flow_lines)
+    procs = procs if procs is not None else min(16, os.cpu_count() or 1)
+    if n < 50000 or procs <= 1:
+        return _convert_lines(flow_lines)
+    import multiprocessing as mp
+    step = (n + 4 * procs - 1) // (4 * procs)
+    chunks = [(flow_lines[i:i + step], i) for i in range(0, n, step)]
+    with mp.get_context("fork").Pool(procs) as pool:
+        parts = pool.map(_convert_chunk, chunks)
+    flows, acts, kept = [], [], []
+    off = 0
+    for fl, ac, kp in parts:
+        fl = fl.copy()
+        fl["act_off"] += off
+        off += len(ac)
+        flows.append(fl)
+        acts.append(ac)
+        kept.extend(kp)
+    # concatenate packs the padded action dtype: restore the C layout
+    return np.concatenate(flows).astype(FLOW_DT), np.concatenate(acts).astype(ACT_DT), kept
 
 
 class CPipeline:
-    def __init__(self, flow_lines: List[str], tiers: Optional[Dict[int, int]] = None):
+    def __init__(self, flow_lines: List[str], tiers: Optional[Dict[int, int]] = None, procs: Optional[int] = None):
         lib = load()
-        flows, acts = _convert(flow_lines)
-        self._flows = (OFlow * max(1, len(flows)))(*flows)
-        self._acts = (OAction * max(1, len(acts)))(*acts)
+        flow_lines = list(flow_lines)
+        flows, acts, kept = _convert(flow_lines, procs)
+        self._flows = np.ascontiguousarray(flows, dtype=FLOW_DT)
+        self._acts = np.ascontiguousarray(acts, dtype=ACT_DT)
+        assert self._flows.dtype.itemsize == 168 and self._acts.dtype.itemsize == 32
         tiers = tiers or {}
         keys = np.array(sorted(tiers), dtype=np.uint32)
         vals = np.array([max(0, min(255, tiers[int(k)])) for k in keys], dtype=np.uint8)
         self._tk, self._tv = keys, vals
         self.n_flows = len(flows)
-        self.h = lib.ocls_create(self._flows, len(flows), self._acts, len(acts), keys.ctypes.data, vals.ctypes.data,
-                                 len(keys))
-        self.flow_meta = flows
+        self._metric_lines = [(i, flow_lines[li]) for i, li in enumerate(kept) if flows[i]["table"] in (7, 8)]
+        self.h = lib.ocls_create(self._flows.ctypes.data, len(flows), self._acts.ctypes.data, len(acts),
+                                 keys.ctypes.data, vals.ctypes.data, len(keys))
 
     def __del__(self):
         try:
@@ -149,3 +195,25 @@ class CPipeline:
         load().ocls_classify(self.h, C.byref(p), n, out.ctypes.data, threads, int(count))
         return out.view(np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"),
                                   ("flags", "u1")])).reshape(n, 2)
+
+    def stats(self) -> Dict[str, int]:
+        out = np.zeros(8, np.uint64)
+        load().ocls_stats(self.h, out.ctypes.data)
+        return {k: int(v) for k, v in zip(STAT_NAMES, out)}
+
+    def n_subtables(self) -> List[int]:
+        return [load().ocls_n_subtables(self.h, t) for t in range(1, 9)]
+
+    def metric_dumps(self) -> Dict[str, List[str]]:
+        """ovs-ofctl dump of the two Metric tables with the packet / byte counters accumulated by
+        classify(count=True), in the text NetworkPolicyMetrics parses (network_policy.go:2034)."""
+        cnt = load().ocls_counters(self.h)
+        out = {"EgressMetric": [], "IngressMetric": []}
+        for i, line in self._metric_lines:
+            f = parse_flow(line)
+            head, _, acts = line.partition(" actions=")
+            toks = [t for t in head.replace(", ", ",").split(",") if t and not t.startswith(("n_packets=", "n_bytes="))]
+            toks = [t for t in toks if not t.startswith("table=")]
+            out[f["table"]].append("table=%s, n_packets=%d, n_bytes=%d, %s actions=%s" % (
+                f["table"], cnt[2 * i], cnt[2 * i + 1], ",".join(toks), acts))
+        return out

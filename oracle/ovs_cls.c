@@ -3,18 +3,30 @@
  *
  * Plain-C restatement of the OVS 2.17.7 userspace classifier (lib/classifier.c; third-party, not
  * vendored in the reference) as Antrea's policy tables exercise it, plus the Antrea policy-stage
- * walk. Same semantics as oracle/ovs_cls.py, organised the way OVS organises it:
+ * walk. Same verdicts as oracle/ovs_cls.py, organised the way OVS organises the lookup:
  *
  *   - tuple-space search: one subtable per distinct match mask, each a hash table keyed by the
  *     masked field vector; a bucket holds the flows with identical match, highest priority first;
- *   - subtables visited in descending max-priority order, skipping those that cannot beat the best
- *     hard match found so far (PVECTOR_FOR_EACH_PRIORITY(subtable, hard_pri + 1, ...));
- *   - soft (conjunction-only) matches collected per subtable head; the highest soft level above the
- *     hard match is resolved by clause bitmaps; if nothing completes, each soft entry at that level
- *     steps to the next lower flow with identical match (next_visible_rule_in_list) and the loop
- *     repeats; a completed conjunction triggers a lookup with conj_id set that ignores soft flows.
- *   - tie (several conjunctions completing at one priority; order is implementation-defined in
- *     OVS): the lowest conj id whose conj_id lookup succeeds wins and TIE is reported.
+ *   - subtables visited in descending max-priority order, stopping below the best hard match found
+ *     so far (classifier_lookup__: PVECTOR_FOR_EACH_PRIORITY(subtable, hard_pri + 1, ...); this
+ *     restatement scans down to hard_pri itself so that equal-priority hard flows with different
+ *     actions are reported as a TIE, as the Python oracle and the device do);
+ *   - prefix tries on nw_src / nw_dst (OVS's default classifier prefix fields): a subtable whose
+ *     mask on the field is a /L prefix is skipped when no flow of the table has a /L prefix on that
+ *     field containing the packet's address (the trie lookup of find_match_wc);
+ *   - soft (conjunction-only) matches collected per subtable head; the `again` loop: drop soft
+ *     entries at or below the hard match, take the highest soft priority and the number of soft
+ *     matches at it (n_soft_pri), accumulate clause bitmaps per conjunction id in a hash map
+ *     (find_conjunctive_match: skipped when n_soft_pri < the set's min_n_clauses, and for
+ *     conjunctions with more clauses than n_soft_pri), try the completed ids' conj_id lookups, and
+ *     otherwise step every entry at that priority to the next lower flow with identical match
+ *     (next_visible_rule_in_list; a hard flow there becomes a hard candidate and ends the chain);
+ *   - tie (several conjunctions completing at one priority; the order is implementation-defined in
+ *     OVS, docs/antrea-network-policy.md:1966-1980): the lowest conj id whose conj_id lookup
+ *     succeeds wins and TIE is reported.
+ *
+ * Every buffer grows on demand; nothing is truncated. An allocation failure aborts the process (a
+ * checker must not silently drop work).
  *
  * The Antrea walk (docs/design/ovs-pipeline.md:1159-1330, 1633-1812): {AntreaPolicy,,Default}Rule
  * tables with miss = next table, Pass -> {Egress,Ingress}Rule, allow / deny -> Metric, drop flows,
@@ -24,6 +36,7 @@
  */
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -47,6 +60,7 @@ typedef struct {
   uint32_t val[NF], mask[NF];
   int32_t act_off, n_act;
   int32_t soft;              /* conjunction-only */
+  uint32_t sig;              /* verdict signature of a hard flow (equal-priority overlap = TIE) */
 } ocls_flow;
 
 typedef struct {
@@ -59,10 +73,36 @@ typedef struct {
   const uint16_t* len;
 } ocls_pkts;
 
+static void* xmalloc(size_t n) {
+  void* p = malloc(n ? n : 1);
+  if (!p) {
+    fprintf(stderr, "ovs_cls: out of memory (%zu bytes)\n", n);
+    abort();
+  }
+  return p;
+}
+static void* xcalloc(size_t n, size_t sz) {
+  void* p = calloc(n ? n : 1, sz ? sz : 1);
+  if (!p) {
+    fprintf(stderr, "ovs_cls: out of memory (%zu x %zu bytes)\n", n, sz);
+    abort();
+  }
+  return p;
+}
+static void* xrealloc(void* q, size_t n) {
+  void* p = realloc(q, n ? n : 1);
+  if (!p) {
+    fprintf(stderr, "ovs_cls: out of memory (%zu bytes)\n", n);
+    abort();
+  }
+  return p;
+}
+
 /* ------------------------------------------------------------------------------------ model */
 typedef struct {
   uint32_t mask[NF];
   uint32_t max_pri;
+  int8_t plen_src, plen_dst; /* prefix length of the mask on nw_src / nw_dst (-1: not a prefix / 0) */
   uint32_t nb;               /* buckets (power of two) */
   int32_t* head;             /* bucket -> first entry index (-1) */
   int32_t* next;             /* entry -> next entry in bucket chain */
@@ -71,23 +111,53 @@ typedef struct {
   uint32_t* key;             /* entry -> masked key [NF] */
   int32_t n_entries;
   int32_t* lists;            /* flow indices, priority desc */
+  uint32_t* lpri;            /* per list slot: priority << 1 | soft (the soft loop reads only this) */
 } subtable;
+
+typedef struct {             /* binary prefix trie of one field of one table */
+  int32_t (*child)[2];
+  uint8_t* ends;             /* a prefix of the table ends at this node */
+  int32_t n, cap;
+} trie;
 
 typedef struct {
   subtable* st;
   int n_st;
+  trie tr[2];                /* nw_src, nw_dst */
 } table_t;
 
 typedef struct ocls {
   ocls_flow* flows;
   int n_flows;
   ocls_action* acts;
+  uint8_t* min_ncl;          /* per flow: min n_clauses of its conjunction actions (OVS min_n_clauses) */
   table_t tables[9];
   uint32_t* tier_conj;       /* sorted conj ids */
   uint8_t* tier_val;
   int n_tier;
   uint64_t* cnt;             /* per flow: packets, bytes (metric flows) */
+  uint64_t stats[8];         /* summed over classify calls: see ocls_stats */
 } ocls;
+
+/* per-thread lookup workspace */
+typedef struct {
+  const int32_t* list;
+  const uint32_t* pri;       /* lpri of the same list */
+  int n, pos;
+} soft_ent;
+
+typedef struct {
+  soft_ent* soft;
+  int soft_cap;
+  uint32_t* hkey;            /* conjunction id hash map (open addressing; gen-stamped) */
+  uint64_t* hbits;
+  uint32_t* hgen;
+  uint32_t hcap, gen;
+  uint32_t* done;
+  int done_cap;
+  uint64_t stats[8];         /* 0 lookups, 1 subtables probed, 2 subtables skipped by tries,
+                                3 soft matches collected, 4 soft-loop levels, 5 conj actions hashed */
+} ws_t;
 
 static uint64_t mixk(const uint32_t* k) {
   uint64_t h = 1469598103934665603ull;
@@ -99,76 +169,151 @@ static uint64_t mixk(const uint32_t* k) {
   return h;
 }
 
-static int cmp_pri_desc(const void* a, const void* b, void* ctx) {
-  const ocls_flow* f = (const ocls_flow*)ctx;
+static const ocls_flow* g_sort_flows;
+static int cmp_pri_desc_g(const void* a, const void* b) {
+  const ocls_flow* f = g_sort_flows;
   int x = *(const int*)a, y = *(const int*)b;
   if (f[x].priority != f[y].priority) return f[x].priority < f[y].priority ? 1 : -1;
   return x < y ? -1 : x > y;
 }
 
-static const ocls_flow* g_sort_flows;
-static int cmp_pri_desc_g(const void* a, const void* b) { return cmp_pri_desc(a, b, (void*)g_sort_flows); }
-
 static int same_mask(const uint32_t* a, const uint32_t* b) { return memcmp(a, b, sizeof(uint32_t) * NF) == 0; }
+
+static int prefix_len(uint32_t m) { /* 1..32 for a CIDR mask, 0 for none, -1 otherwise */
+  if (m == 0) return 0;
+  int l = 0;
+  while (l < 32 && (m >> (31 - l)) & 1u) l++;
+  uint32_t want = l == 32 ? 0xffffffffu : ~(0xffffffffu >> l);
+  return m == want ? l : -1;
+}
+
+static int trie_node(trie* t) {
+  if (t->n == t->cap) {
+    t->cap = t->cap ? 2 * t->cap : 64;
+    t->child = (int32_t(*)[2])xrealloc(t->child, sizeof(int32_t[2]) * (size_t)t->cap);
+    t->ends = (uint8_t*)xrealloc(t->ends, (size_t)t->cap);
+  }
+  t->child[t->n][0] = t->child[t->n][1] = -1;
+  t->ends[t->n] = 0;
+  return t->n++;
+}
+static void trie_insert(trie* t, uint32_t v, int len) {
+  if (!t->n) trie_node(t);
+  int x = 0;
+  for (int d = 0; d < len; d++) {
+    int b = (v >> (31 - d)) & 1u;
+    if (t->child[x][b] < 0) {
+      int y = trie_node(t);
+      t->child[x][b] = y;
+    }
+    x = t->child[x][b];
+  }
+  t->ends[x] = 1;
+}
+/* bit L (1..32) set: a /L prefix of the table contains `v` */
+static uint64_t trie_lookup(const trie* t, uint32_t v) {
+  uint64_t m = 0;
+  if (!t->n) return 0;
+  int x = 0;
+  for (int d = 0; d < 32; d++) {
+    x = t->child[x][(v >> (31 - d)) & 1u];
+    if (x < 0) break;
+    if (t->ends[x]) m |= 1ull << (d + 1);
+  }
+  return m;
+}
 
 ocls* ocls_create(const ocls_flow* flows, int n_flows, const ocls_action* acts, int n_acts, const uint32_t* tier_conj,
                   const uint8_t* tier_val, int n_tier) {
-  ocls* c = (ocls*)calloc(1, sizeof(ocls));
-  c->flows = (ocls_flow*)malloc(sizeof(ocls_flow) * (n_flows ? n_flows : 1));
-  memcpy(c->flows, flows, sizeof(ocls_flow) * n_flows);
+  ocls* c = (ocls*)xcalloc(1, sizeof(ocls));
+  c->flows = (ocls_flow*)xmalloc(sizeof(ocls_flow) * (size_t)n_flows);
+  memcpy(c->flows, flows, sizeof(ocls_flow) * (size_t)n_flows);
   c->n_flows = n_flows;
-  c->acts = (ocls_action*)malloc(sizeof(ocls_action) * (n_acts ? n_acts : 1));
-  memcpy(c->acts, acts, sizeof(ocls_action) * n_acts);
-  c->tier_conj = (uint32_t*)malloc(4 * (n_tier ? n_tier : 1));
-  c->tier_val = (uint8_t*)malloc(n_tier ? n_tier : 1);
-  memcpy(c->tier_conj, tier_conj, 4 * n_tier);
-  memcpy(c->tier_val, tier_val, n_tier);
+  c->acts = (ocls_action*)xmalloc(sizeof(ocls_action) * (size_t)n_acts);
+  memcpy(c->acts, acts, sizeof(ocls_action) * (size_t)n_acts);
+  c->min_ncl = (uint8_t*)xcalloc((size_t)n_flows, 1);
+  for (int i = 0; i < n_flows; i++) {
+    uint32_t mn = 255;
+    for (int a = 0; a < flows[i].n_act; a++) {
+      const ocls_action* ac = &acts[flows[i].act_off + a];
+      if (ac->kind == A_CONJ && ac->c < mn) mn = ac->c;
+      if (ac->kind == A_CONJ && (ac->c < 1 || ac->c > 64 || ac->b < 1 || ac->b > ac->c)) {
+        fprintf(stderr, "ovs_cls: malformed conjunction(%u,%u/%u)\n", ac->a, ac->b, ac->c);
+        abort();
+      }
+    }
+    c->min_ncl[i] = (uint8_t)mn;
+  }
+  c->tier_conj = (uint32_t*)xmalloc(4 * (size_t)n_tier);
+  c->tier_val = (uint8_t*)xmalloc((size_t)n_tier);
+  memcpy(c->tier_conj, tier_conj, 4 * (size_t)n_tier);
+  memcpy(c->tier_val, tier_val, (size_t)n_tier);
   c->n_tier = n_tier;
-  c->cnt = (uint64_t*)calloc(2 * (size_t)(n_flows ? n_flows : 1), 8);
+  c->cnt = (uint64_t*)xcalloc(2 * (size_t)n_flows, 8);
+  int* idx = (int*)xmalloc(sizeof(int) * (size_t)n_flows);
+  int* owner = (int*)xmalloc(sizeof(int) * (size_t)n_flows);
   for (int t = 1; t <= 8; t++) {
-    /* group flows by mask */
-    int* idx = (int*)malloc(sizeof(int) * (n_flows ? n_flows : 1));
     int n = 0;
     for (int i = 0; i < n_flows; i++)
       if (c->flows[i].table == t) idx[n++] = i;
+    /* group flows by mask: hash of the mask -> subtable */
     subtable* sts = NULL;
-    int nst = 0;
-    int* owner = (int*)malloc(sizeof(int) * (n ? n : 1));
+    int nst = 0, stcap = 0;
+    uint32_t mnb = 1;
+    while (mnb < 2u * (uint32_t)n + 2u) mnb <<= 1;
+    int32_t* mhead = (int32_t*)xmalloc(sizeof(int32_t) * mnb);
+    int32_t* mnext = NULL;
+    for (uint32_t b = 0; b < mnb; b++) mhead[b] = -1;
     for (int j = 0; j < n; j++) {
       const ocls_flow* f = &c->flows[idx[j]];
+      uint32_t b = (uint32_t)mixk(f->mask) & (mnb - 1);
       int s;
-      for (s = 0; s < nst; s++)
+      for (s = mhead[b]; s >= 0; s = mnext[s])
         if (same_mask(sts[s].mask, f->mask)) break;
-      if (s == nst) {
-        sts = (subtable*)realloc(sts, sizeof(subtable) * (nst + 1));
-        memset(&sts[nst], 0, sizeof(subtable));
-        memcpy(sts[nst].mask, f->mask, sizeof(uint32_t) * NF);
-        nst++;
+      if (s < 0) {
+        if (nst == stcap) {
+          stcap = stcap ? 2 * stcap : 16;
+          sts = (subtable*)xrealloc(sts, sizeof(subtable) * (size_t)stcap);
+          mnext = (int32_t*)xrealloc(mnext, sizeof(int32_t) * (size_t)stcap);
+        }
+        s = nst++;
+        memset(&sts[s], 0, sizeof(subtable));
+        memcpy(sts[s].mask, f->mask, sizeof(uint32_t) * NF);
+        sts[s].plen_src = (int8_t)prefix_len(f->mask[F_NW_SRC]);
+        sts[s].plen_dst = (int8_t)prefix_len(f->mask[F_NW_DST]);
+        mnext[s] = mhead[b];
+        mhead[b] = s;
       }
       owner[j] = s;
       if (f->priority > sts[s].max_pri) sts[s].max_pri = f->priority;
+      if (sts[s].plen_src > 0) trie_insert(&c->tables[t].tr[0], f->val[F_NW_SRC], sts[s].plen_src);
+      if (sts[s].plen_dst > 0) trie_insert(&c->tables[t].tr[1], f->val[F_NW_DST], sts[s].plen_dst);
     }
+    free(mhead);
+    free(mnext);
+    /* per subtable: flow count, then entries */
+    int* cnt = (int*)xcalloc((size_t)nst, sizeof(int));
+    for (int j = 0; j < n; j++) cnt[owner[j]]++;
+    int** members = (int**)xmalloc(sizeof(int*) * (size_t)nst);
+    int* fill = (int*)xcalloc((size_t)nst, sizeof(int));
+    for (int s = 0; s < nst; s++) members[s] = (int*)xmalloc(sizeof(int) * (size_t)cnt[s]);
+    for (int j = 0; j < n; j++) members[owner[j]][fill[owner[j]]++] = idx[j];
     for (int s = 0; s < nst; s++) {
       subtable* st = &sts[s];
-      int m = 0;
-      for (int j = 0; j < n; j++) m += owner[j] == s;
+      const int m = cnt[s];
       uint32_t nb = 1;
       while (nb < (uint32_t)m * 2) nb <<= 1;
       st->nb = nb;
-      st->head = (int32_t*)malloc(sizeof(int32_t) * nb);
+      st->head = (int32_t*)xmalloc(sizeof(int32_t) * nb);
       for (uint32_t b = 0; b < nb; b++) st->head[b] = -1;
-      st->next = (int32_t*)malloc(sizeof(int32_t) * (m ? m : 1));
-      st->list_off = (int32_t*)malloc(sizeof(int32_t) * (m ? m : 1));
-      st->list_n = (int32_t*)calloc(m ? m : 1, sizeof(int32_t));
-      st->key = (uint32_t*)malloc(sizeof(uint32_t) * NF * (m ? m : 1));
-      st->lists = (int32_t*)malloc(sizeof(int32_t) * (m ? m : 1));
-      /* entries: distinct masked values; first pass count */
-      int* fent = (int*)malloc(sizeof(int) * (m ? m : 1));
-      int* fidx = (int*)malloc(sizeof(int) * (m ? m : 1));
-      int k = 0;
-      for (int j = 0; j < n; j++) {
-        if (owner[j] != s) continue;
-        const ocls_flow* f = &c->flows[idx[j]];
+      st->next = (int32_t*)xmalloc(sizeof(int32_t) * (size_t)m);
+      st->list_off = (int32_t*)xmalloc(sizeof(int32_t) * (size_t)m);
+      st->list_n = (int32_t*)xcalloc((size_t)m, sizeof(int32_t));
+      st->key = (uint32_t*)xmalloc(sizeof(uint32_t) * NF * (size_t)m);
+      st->lists = (int32_t*)xmalloc(sizeof(int32_t) * (size_t)m);
+      int* fent = (int*)xmalloc(sizeof(int) * (size_t)m);
+      for (int k = 0; k < m; k++) {
+        const ocls_flow* f = &c->flows[members[s][k]];
         uint32_t key[NF];
         for (int q = 0; q < NF; q++) key[q] = f->val[q] & f->mask[q];
         uint32_t b = (uint32_t)mixk(key) & (nb - 1);
@@ -183,8 +328,6 @@ ocls* ocls_create(const ocls_flow* flows, int n_flows, const ocls_action* acts, 
         }
         st->list_n[e]++;
         fent[k] = e;
-        fidx[k] = idx[j];
-        k++;
       }
       int off = 0;
       for (int e = 0; e < st->n_entries; e++) {
@@ -192,15 +335,20 @@ ocls* ocls_create(const ocls_flow* flows, int n_flows, const ocls_action* acts, 
         off += st->list_n[e];
         st->list_n[e] = 0;
       }
-      for (int q = 0; q < k; q++) {
-        int e = fent[q];
-        st->lists[st->list_off[e] + st->list_n[e]++] = fidx[q];
+      for (int k = 0; k < m; k++) {
+        int e = fent[k];
+        st->lists[st->list_off[e] + st->list_n[e]++] = members[s][k];
       }
       g_sort_flows = c->flows;
-      for (int e = 0; e < st->n_entries; e++) qsort(st->lists + st->list_off[e], st->list_n[e], sizeof(int32_t), cmp_pri_desc_g);
+      for (int e = 0; e < st->n_entries; e++) qsort(st->lists + st->list_off[e], (size_t)st->list_n[e], sizeof(int32_t), cmp_pri_desc_g);
+      st->lpri = (uint32_t*)xmalloc(sizeof(uint32_t) * (size_t)m);
+      for (int k = 0; k < m; k++) st->lpri[k] = (c->flows[st->lists[k]].priority << 1) | (c->flows[st->lists[k]].soft ? 1u : 0u);
       free(fent);
-      free(fidx);
+      free(members[s]);
     }
+    free(members);
+    free(fill);
+    free(cnt);
     /* subtables by max priority, descending (pvector order) */
     for (int a = 1; a < nst; a++)
       for (int b = a; b > 0 && sts[b].max_pri > sts[b - 1].max_pri; b--) {
@@ -210,9 +358,9 @@ ocls* ocls_create(const ocls_flow* flows, int n_flows, const ocls_action* acts, 
       }
     c->tables[t].st = sts;
     c->tables[t].n_st = nst;
-    free(idx);
-    free(owner);
   }
+  free(idx);
+  free(owner);
   return c;
 }
 
@@ -227,11 +375,17 @@ void ocls_destroy(ocls* c) {
       free(st->list_n);
       free(st->key);
       free(st->lists);
+      free(st->lpri);
     }
     free(c->tables[t].st);
+    for (int k = 0; k < 2; k++) {
+      free(c->tables[t].tr[k].child);
+      free(c->tables[t].tr[k].ends);
+    }
   }
   free(c->flows);
   free(c->acts);
+  free(c->min_ncl);
   free(c->tier_conj);
   free(c->tier_val);
   free(c->cnt);
@@ -239,129 +393,199 @@ void ocls_destroy(ocls* c) {
 }
 
 /* find_match: the bucket list of `st` matching packet vector `pv`, or NULL */
-static const int32_t* find_match(const subtable* st, const uint32_t* pv, int* n) {
+static const int32_t* find_match(const subtable* st, const uint32_t* pv, int* n, const uint32_t** pri) {
   uint32_t key[NF];
   for (int q = 0; q < NF; q++) key[q] = pv[q] & st->mask[q];
   uint32_t b = (uint32_t)mixk(key) & (st->nb - 1);
   for (int e = st->head[b]; e >= 0; e = st->next[e])
     if (memcmp(st->key + (size_t)e * NF, key, sizeof key) == 0) {
       *n = st->list_n[e];
+      *pri = st->lpri + st->list_off[e];
       return st->lists + st->list_off[e];
     }
   return NULL;
 }
 
-typedef struct {
-  const int32_t* list;
-  int n, pos;
-} soft_ent;
+static void ws_soft_push(ws_t* w, int* n_soft, const int32_t* list, const uint32_t* pri, int n, int pos) {
+  if (*n_soft == w->soft_cap) {
+    w->soft_cap = w->soft_cap ? 2 * w->soft_cap : 256;
+    w->soft = (soft_ent*)xrealloc(w->soft, sizeof(soft_ent) * (size_t)w->soft_cap);
+  }
+  w->soft[*n_soft].list = list;
+  w->soft[*n_soft].pri = pri;
+  w->soft[*n_soft].n = n;
+  w->soft[*n_soft].pos = pos;
+  (*n_soft)++;
+}
 
-#define MAX_SOFT 256
+/* conjunction-id map: clause bitmap of id (initialised as OVS does, UINT64_MAX << n_clauses) */
+static uint64_t* ws_conj(ws_t* w, uint32_t id, uint32_t n_clauses) {
+  uint32_t m = w->hcap - 1, h = (id * 0x9e3779b1u) & m;
+  while (w->hgen[h] == w->gen && w->hkey[h] != id) h = (h + 1) & m;
+  if (w->hgen[h] != w->gen) {
+    w->hgen[h] = w->gen;
+    w->hkey[h] = id;
+    w->hbits[h] = n_clauses >= 64 ? 0 : (~0ull << n_clauses);
+  }
+  return &w->hbits[h];
+}
+static void ws_conj_reset(ws_t* w, size_t need) {
+  if (w->hcap < 2 * need + 16) {
+    uint32_t cap = 64;
+    while (cap < 2 * need + 16) cap <<= 1;
+    free(w->hkey);
+    free(w->hbits);
+    free(w->hgen);
+    w->hkey = (uint32_t*)xmalloc(4 * (size_t)cap);
+    w->hbits = (uint64_t*)xmalloc(8 * (size_t)cap);
+    w->hgen = (uint32_t*)xcalloc(cap, 4);
+    w->hcap = cap;
+    w->gen = 0;
+  }
+  if (++w->gen == 0) { /* stamp wrap: clear */
+    memset(w->hgen, 0, 4 * (size_t)w->hcap);
+    w->gen = 1;
+  }
+}
+static void ws_done_push(ws_t* w, int* nd, uint32_t id) {
+  if (*nd == w->done_cap) {
+    w->done_cap = w->done_cap ? 2 * w->done_cap : 64;
+    w->done = (uint32_t*)xrealloc(w->done, 4 * (size_t)w->done_cap);
+  }
+  w->done[(*nd)++] = id;
+}
+static int cmp_u32(const void* a, const void* b) {
+  uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return x < y ? -1 : x > y;
+}
 
-/* classifier_lookup__ restated. Returns flow index or -1; *tie set on conj ties. */
-static int lookup(const ocls* c, int table, uint32_t* pv, int allow_conj, int* tie) {
+/* classifier_lookup__ restated. Returns flow index or -1; *tie set on conj ties (and on
+ * equal-priority hard flows with different actions when no conjunction decides). */
+static int lookup(const ocls* c, ws_t* w, int table, uint32_t* pv, int allow_conj, int* tie) {
   const table_t* T = &c->tables[table];
-  int hard = -1;
-  int64_t hard_pri = -1;
-  soft_ent soft[MAX_SOFT];
+  const ocls_flow* F = c->flows;
+  int hard = -1, htie = 0;
+  int64_t hard_pri = -1, soft_pri = -1;
   int n_soft = 0;
+  w->stats[0]++;
+  const uint64_t tsrc = trie_lookup(&T->tr[0], pv[F_NW_SRC]);
+  const uint64_t tdst = trie_lookup(&T->tr[1], pv[F_NW_DST]);
   for (int s = 0; s < T->n_st; s++) {
     const subtable* st = &T->st[s];
-    if ((int64_t)st->max_pri < hard_pri + 1) break;
+    if ((int64_t)st->max_pri < hard_pri) break;
+    if ((st->plen_src > 0 && !((tsrc >> st->plen_src) & 1)) || (st->plen_dst > 0 && !((tdst >> st->plen_dst) & 1))) {
+      w->stats[2]++;
+      continue;
+    }
+    w->stats[1]++;
     int n;
-    const int32_t* l = find_match(st, pv, &n);
+    const uint32_t* lp;
+    const int32_t* l = find_match(st, pv, &n, &lp);
     if (!l) continue;
-    int pos = 0;
-    const ocls_flow* f = &c->flows[l[pos]];
-    if (!allow_conj && f->soft) continue; /* soft heads are ignored, not stepped past (OVS) */
-    if ((int64_t)f->priority <= hard_pri) continue;
-    if (!f->soft) {
-      hard = l[pos];
+    const ocls_flow* f = &F[l[0]];
+    if (f->soft) {
+      if (!allow_conj || (int64_t)f->priority <= hard_pri) continue; /* OVS: ignored, not stepped past */
+      ws_soft_push(w, &n_soft, l, lp, n, 0);
+      if ((int64_t)f->priority > soft_pri) soft_pri = f->priority;
+      continue;
+    }
+    if ((int64_t)f->priority > hard_pri) {
+      hard = l[0];
       hard_pri = f->priority;
-    } else if (n_soft < MAX_SOFT) {
-      soft[n_soft].list = l;
-      soft[n_soft].n = n;
-      soft[n_soft].pos = pos;
-      n_soft++;
+      htie = 0;
+    } else if ((int64_t)f->priority == hard_pri && f->sig != F[hard].sig) {
+      htie = 1;
     }
   }
-  if (!allow_conj || n_soft == 0) return hard;
+  w->stats[3] += (uint64_t)n_soft;
+  if (!allow_conj || hard_pri >= soft_pri) {
+    if (hard >= 0 && htie) *tie = 1;
+    return hard;
+  }
+  soft_ent* soft = w->soft;
   for (;;) {
-    /* drop soft entries at or below the hard match */
-    int m = 0;
-    for (int i = 0; i < n_soft; i++)
-      if (soft[i].pos < soft[i].n && (int64_t)c->flows[soft[i].list[soft[i].pos]].priority > hard_pri) soft[m++] = soft[i];
-    n_soft = m;
-    if (!n_soft) return hard;
+    soft = w->soft;
+    /* delete chain ends and soft matches at or below the hard match */
+    for (int i = 0; i < n_soft;) {
+      if (soft[i].pos >= soft[i].n || (int64_t)(soft[i].pri[soft[i].pos] >> 1) <= hard_pri) soft[i] = soft[--n_soft];
+      else i++;
+    }
+    if (!n_soft) break;
+    w->stats[4]++;
+    /* highest soft priority and the number of soft matches at it */
     uint32_t top = 0;
+    int n_top = 0;
     for (int i = 0; i < n_soft; i++) {
-      uint32_t p = c->flows[soft[i].list[soft[i].pos]].priority;
-      if (p > top) top = p;
+      uint32_t p = soft[i].pri[soft[i].pos] >> 1;
+      if (p > top) {
+        top = p;
+        n_top = 1;
+      } else if (p == top) {
+        n_top++;
+      }
     }
-    /* conjunction completion at `top` (find_conjunctive_match): clause bitmaps per conj id */
-    uint32_t ids[MAX_SOFT * 8];
-    uint64_t bits[MAX_SOFT * 8];
-    uint32_t ncl[MAX_SOFT * 8];
-    int nid = 0;
+    /* find_conjunctive_match over the soft matches at `top` */
+    size_t n_acts = 0;
     for (int i = 0; i < n_soft; i++) {
-      const ocls_flow* f = &c->flows[soft[i].list[soft[i].pos]];
-      if (f->priority != top) continue;
-      for (int a = 0; a < f->n_act; a++) {
-        const ocls_action* ac = &c->acts[f->act_off + a];
-        if (ac->kind != A_CONJ) continue;
-        int j;
-        for (j = 0; j < nid; j++)
-          if (ids[j] == ac->a) break;
-        if (j == nid) {
-          if (nid >= MAX_SOFT * 8) continue;
-          ids[nid] = ac->a;
-          bits[nid] = 0;
-          ncl[nid] = ac->c;
-          nid++;
+      if ((soft[i].pri[soft[i].pos] >> 1) != top) continue;
+      const int fi = soft[i].list[soft[i].pos];
+      if ((uint32_t)n_top >= c->min_ncl[fi]) n_acts += (size_t)F[fi].n_act;
+    }
+    int nd = 0;
+    if (n_acts) {
+      ws_conj_reset(w, n_acts);
+      w->stats[5] += n_acts;
+      for (int i = 0; i < n_soft; i++) {
+        if ((soft[i].pri[soft[i].pos] >> 1) != top) continue;
+        const int fi = soft[i].list[soft[i].pos];
+        const ocls_flow* f = &F[fi];
+        if ((uint32_t)n_top < c->min_ncl[fi]) continue;
+        for (int a = 0; a < f->n_act; a++) {
+          const ocls_action* ac = &c->acts[f->act_off + a];
+          if (ac->kind != A_CONJ || ac->c > (uint32_t)n_top) continue;
+          uint64_t* cm = ws_conj(w, ac->a, ac->c);
+          const uint64_t before = *cm;
+          *cm |= 1ull << (ac->b - 1);
+          if (*cm == ~0ull && before != ~0ull) ws_done_push(w, &nd, ac->a);
         }
-        bits[j] |= 1ull << (ac->b - 1);
       }
     }
-    /* completed ids, ascending */
-    int ndone = 0;
-    uint32_t done[MAX_SOFT * 8];
-    for (int j = 0; j < nid; j++) {
-      uint64_t full = ncl[j] >= 64 ? ~0ull : ((1ull << ncl[j]) - 1);
-      if ((bits[j] & full) == full) done[ndone++] = ids[j];
-    }
-    for (int a = 1; a < ndone; a++)
-      for (int b = a; b > 0 && done[b] < done[b - 1]; b--) {
-        uint32_t t = done[b];
-        done[b] = done[b - 1];
-        done[b - 1] = t;
-      }
-    for (int d = 0; d < ndone; d++) {
-      uint32_t saved = pv[F_CONJ_ID];
-      pv[F_CONJ_ID] = done[d];
-      int dummy = 0;
-      int r = lookup(c, table, pv, 0, &dummy);
-      pv[F_CONJ_ID] = saved;
-      if (r >= 0) {
-        if (ndone > 1) *tie = 1;
-        return r;
+    if (nd) {
+      qsort(w->done, (size_t)nd, 4, cmp_u32);
+      for (int d = 0; d < nd; d++) {
+        uint32_t saved = pv[F_CONJ_ID];
+        pv[F_CONJ_ID] = w->done[d];
+        int dummy = 0;
+        int r = lookup(c, w, table, pv, 0, &dummy);
+        pv[F_CONJ_ID] = saved;
+        if (r >= 0) {
+          if (nd > 1) *tie = 1;
+          return r;
+        }
       }
     }
     /* next_visible_rule_in_list for every entry at `top` */
+    soft = w->soft;
     for (int i = 0; i < n_soft; i++) {
-      if (c->flows[soft[i].list[soft[i].pos]].priority != top) continue;
+      if ((soft[i].pri[soft[i].pos] >> 1) != top) continue;
       soft[i].pos++;
-      if (soft[i].pos < soft[i].n) {
-        int fi = soft[i].list[soft[i].pos];
-        if (!c->flows[fi].soft) {
-          if ((int64_t)c->flows[fi].priority > hard_pri) {
+      if (soft[i].pos < soft[i].n && !(soft[i].pri[soft[i].pos] & 1u)) {
+        const int fi = soft[i].list[soft[i].pos];
+        {
+          if ((int64_t)F[fi].priority > hard_pri) {
             hard = fi;
-            hard_pri = c->flows[fi].priority;
+            hard_pri = F[fi].priority;
+            htie = 0;
+          } else if ((int64_t)F[fi].priority == hard_pri && hard >= 0 && F[fi].sig != F[hard].sig) {
+            htie = 1;
           }
           soft[i].pos = soft[i].n; /* a hard flow ends the chain */
         }
       }
     }
   }
+  if (hard >= 0 && htie) *tie = 1;
+  return hard;
 }
 
 static uint8_t tier_of(const ocls* c, uint32_t conj) {
@@ -377,14 +601,15 @@ static uint8_t tier_of(const ocls* c, uint32_t conj) {
 enum { ACT_NONE, ACT_NO_MATCH, ACT_ALLOW, ACT_DROP, ACT_REJECT, ACT_ISO_DROP, ACT_BYPASS };
 
 /* one policy stage; tables t1,t2,t3 then metric (7 egress / 8 ingress). Returns packed verdict. */
-static void stage(const ocls* c, int base, uint32_t* pv, uint32_t len, uint64_t* cnt, uint32_t* out_conj, uint32_t* out_packed) {
+static void stage(const ocls* c, ws_t* w, int base, uint32_t* pv, uint32_t len, uint64_t* cnt, uint32_t* out_conj,
+                  uint32_t* out_packed) {
   int metric = base == 0 ? 7 : 8;
   int t = base + 1;
   uint32_t flags = 0, conj = 0, tindex = 0, action = ACT_NO_MATCH;
   int t2 = base + 2;
   while (t != metric) {
     int tie = 0;
-    int fi = lookup(c, t, pv, 1, &tie);
+    int fi = lookup(c, w, t, pv, 1, &tie);
     if (fi < 0) {
       t = t == base + 3 ? metric : t + 1;
       continue;
@@ -437,7 +662,7 @@ static void stage(const ocls* c, int base, uint32_t* pv, uint32_t len, uint64_t*
     t = go;
   }
   int tie = 0;
-  int mf = lookup(c, metric, pv, 0, &tie);
+  int mf = lookup(c, w, metric, pv, 0, &tie);
   if (mf >= 0 && cnt) {
     cnt[2 * mf] += 1;
     cnt[2 * mf + 1] += len;
@@ -447,7 +672,7 @@ static void stage(const ocls* c, int base, uint32_t* pv, uint32_t len, uint64_t*
   *out_packed = action | (tindex << 8) | ((conj ? tier_of(c, conj) : 0u) << 16) | (flags << 24);
 }
 
-static void classify_range(const ocls* c, const ocls_pkts* p, size_t lo, size_t hi, uint32_t* out, uint64_t* cnt) {
+static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo, size_t hi, uint32_t* out, uint64_t* cnt) {
   for (size_t i = lo; i < hi; i++) {
     uint32_t pv[NF];
     memset(pv, 0, sizeof pv);
@@ -468,7 +693,7 @@ static void classify_range(const ocls* c, const ocls_pkts* p, size_t lo, size_t 
     pv[F_CT_STATE] = p->ct_state ? p->ct_state[i] : 0x21;
     uint32_t len = p->len ? p->len[i] : 0;
     uint32_t ec, ep, gc, gp;
-    stage(c, 0, pv, len, cnt, &ec, &ep);
+    stage(c, w, 0, pv, len, cnt, &ec, &ep);
     uint32_t ea = ep & 0xff;
     if (ea == ACT_DROP || ea == ACT_REJECT || ea == ACT_ISO_DROP) {
       gc = 0;
@@ -480,7 +705,7 @@ static void classify_range(const ocls* c, const ocls_pkts* p, size_t lo, size_t 
       pv[F_REG0] = 0;
       pv[F_REG3] = 0;
       pv[F_CONJ_ID] = 0;
-      stage(c, 3, pv, len, cnt, &gc, &gp);
+      stage(c, w, 3, pv, len, cnt, &gc, &gp);
     }
     out[4 * i + 0] = ec;
     out[4 * i + 1] = ep;
@@ -495,40 +720,57 @@ typedef struct {
   size_t lo, hi;
   uint32_t* out;
   uint64_t* cnt;
+  ws_t ws;
 } job;
 
 static void* worker(void* arg) {
   job* j = (job*)arg;
-  classify_range(j->c, j->p, j->lo, j->hi, j->out, j->cnt);
+  classify_range(j->c, &j->ws, j->p, j->lo, j->hi, j->out, j->cnt);
   return NULL;
 }
 
 /* out: 4 uint32 per packet (egress conj, egress packed, ingress conj, ingress packed). */
 int ocls_classify(ocls* c, const ocls_pkts* p, size_t n, uint32_t* out, int threads, int count) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t th[256];
-  job jobs[256];
-  uint64_t* cnts[256];
+  if ((size_t)threads > n && n) threads = (int)n;
+  pthread_t* th = (pthread_t*)xmalloc(sizeof(pthread_t) * (size_t)threads);
+  job* jobs = (job*)xcalloc((size_t)threads, sizeof(job));
   for (int t = 0; t < threads; t++) {
-    cnts[t] = count ? (uint64_t*)calloc(2 * (size_t)(c->n_flows ? c->n_flows : 1), 8) : NULL;
+    jobs[t].cnt = count ? (uint64_t*)xcalloc(2 * (size_t)c->n_flows, 8) : NULL;
     jobs[t].c = c;
     jobs[t].p = p;
-    jobs[t].lo = n * t / threads;
-    jobs[t].hi = n * (t + 1) / threads;
+    jobs[t].lo = n * (size_t)t / (size_t)threads;
+    jobs[t].hi = n * (size_t)(t + 1) / (size_t)threads;
     jobs[t].out = out;
-    jobs[t].cnt = cnts[t];
-    if (threads == 1) worker(&jobs[t]);
-    else pthread_create(&th[t], NULL, worker, &jobs[t]);
+    if (threads == 1) {
+      worker(&jobs[t]);
+    } else if (pthread_create(&th[t], NULL, worker, &jobs[t]) != 0) {
+      fprintf(stderr, "ovs_cls: pthread_create failed\n");
+      abort();
+    }
   }
   for (int t = 0; t < threads; t++) {
     if (threads > 1) pthread_join(th[t], NULL);
     if (count) {
-      for (int f = 0; f < 2 * c->n_flows; f++) c->cnt[f] += cnts[t][f];
-      free(cnts[t]);
+      for (int f = 0; f < 2 * c->n_flows; f++) c->cnt[f] += jobs[t].cnt[f];
+      free(jobs[t].cnt);
     }
+    for (int k = 0; k < 8; k++) c->stats[k] += jobs[t].ws.stats[k];
+    free(jobs[t].ws.soft);
+    free(jobs[t].ws.hkey);
+    free(jobs[t].ws.hbits);
+    free(jobs[t].ws.hgen);
+    free(jobs[t].ws.done);
   }
+  free(th);
+  free(jobs);
   return 0;
 }
 
 const uint64_t* ocls_counters(const ocls* c) { return c->cnt; }
+
+/* Lookup statistics summed over every classify call (profiling the baseline): 0 table lookups,
+ * 1 subtables probed, 2 subtables skipped by the prefix tries, 3 soft matches collected, 4 soft-loop
+ * levels, 5 conjunction actions hashed. */
+void ocls_stats(const ocls* c, uint64_t* out) { memcpy(out, c->stats, sizeof c->stats); }
+int ocls_n_subtables(const ocls* c, int table) { return (table >= 1 && table <= 8) ? c->tables[table].n_st : 0; }

@@ -1,0 +1,194 @@
+"""Oracle verdicts for whole workloads (TEST / MEASUREMENT INFRASTRUCTURE ONLY).
+
+* `oracle_pipeline(wl)`   -- the C restatement of the OVS classifier (ovs_cls.c) loaded with the
+                             flows the ORACLE compiler (oracle/compiler.py) emits for `wl.rules`;
+                             never the product compiler's dump, so a product compiler bug cannot
+                             hide on both sides of a comparison.
+* `oracle_metrics(pipe)`  -- NetworkPolicyMetrics of the counters the C oracle accumulated
+                             (parsed exactly as network_policy.go:1917-1980, 2034 parse the dump).
+* `non_service_mask`      -- packets of a workload with Services that do not hit a ServiceLB flow
+                             (the C oracle has no AntreaProxy stage; those packets' policy verdicts
+                             are comparable directly).
+* `OracleWorker`          -- the same in a separate CPU process (spawned, never touches a GPU):
+                             bench.py starts it before its GPU work, then asks it to check a sample
+                             of the timed batch (parity stamp) and to time the CPU baseline.
+"""
+from __future__ import annotations
+
+import copy
+import os
+import platform
+import time
+from typing import Dict, Optional
+
+import numpy as np
+
+VERDICT_NP = np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"), ("flags", "u1")])
+
+
+def cpu_threads() -> int:
+    """Threads of the CPU legs: the process's CPU share (OMP_NUM_THREADS when the box sets it,
+    else the CPUs this process may run on)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def host_info() -> dict:
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+
+
+def tiers_of(wl) -> Dict[int, int]:
+    return {r["flow_id"]: int(r.get("tier_priority") or 0) for r in wl.rules}
+
+
+def oracle_flows(wl):
+    from . import compiler as oc
+    fnp = oc.FeatureNetworkPolicy()
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    return fnp.dump_flows()
+
+
+def oracle_pipeline(wl, procs: Optional[int] = None):
+    from .cls_c import CPipeline
+    return CPipeline(oracle_flows(wl), tiers_of(wl), procs=procs)
+
+
+def oracle_metrics(pipe) -> Dict[int, tuple]:
+    from . import compiler as oc
+    d = pipe.metric_dumps()
+    return oc.network_policy_metrics(d["EgressMetric"], d["IngressMetric"])
+
+
+def non_service_mask(wl, cols) -> np.ndarray:
+    """True for packets that match no ServiceLB flow of wl (proto, Service IP, port)."""
+    sm = getattr(wl, "svc_meta", None)
+    n = len(cols["src"])
+    if sm is None:
+        return np.ones(n, bool)
+    keys = set(zip(sm["proto"].astype(np.int64).tolist(), sm["ip"].astype(np.int64).tolist(),
+                   sm["port"].astype(np.int64).tolist()))
+    p, d, dp = (cols[k].astype(np.int64).tolist() for k in ("proto", "dst", "dport"))
+    return np.array([(a, b, c) not in keys for a, b, c in zip(p, d, dp)], bool)
+
+
+def compare(got: np.ndarray, want: np.ndarray, mask: Optional[np.ndarray] = None) -> dict:
+    """Packet-for-packet verdict comparison: (n, 2) verdict records (8 B each)."""
+    g = np.ascontiguousarray(got).view(np.uint64).reshape(-1, 2)
+    w = np.ascontiguousarray(want).view(np.uint64).reshape(-1, 2)
+    idx = np.arange(len(g)) if mask is None else np.nonzero(mask)[0]
+    bad = idx[(g[idx] != w[idx]).any(axis=1)]
+    res = {"checked": int(len(idx)), "mismatches": int(len(bad))}
+    if len(bad):
+        i = int(bad[0])
+        res["first"] = {"index": i, "device": [int(x) for x in g[i]], "oracle": [int(x) for x in w[i]]}
+    return res
+
+
+# ------------------------------------------------------------------------------ worker process
+def _serve(conn, config: str, procs: int):
+    from antrea_amd import workload
+    t0 = time.time()
+    wl = workload.CONFIGS[config]()
+    pipe = oracle_pipeline(wl, procs=procs)
+    conn.send({"ready": True, "setup_s": round(time.time() - t0, 1), "flows": pipe.n_flows})
+    while True:
+        msg = conn.recv()
+        if msg[0] == "check":
+            _, cols, verdicts = msg
+            t = time.time()
+            want = pipe.classify(cols, threads=procs)
+            res = compare(verdicts, want, non_service_mask(wl, cols))
+            res["oracle_s"] = round(time.time() - t, 2)
+            conn.send(res)
+        elif msg[0] == "baseline":
+            _, seconds, chunk = msg
+            conn.send(time_baseline(wl, pipe, seconds, chunk, procs))
+        else:
+            conn.send(None)
+            return
+
+
+def time_baseline(wl, pipe, seconds: float, chunk: int, threads: int) -> dict:
+    """The bench `cpu_baseline` object: the C oracle timed on the host cores over chunks of the
+    same synthetic workload until `seconds` of wall time have elapsed (setup untimed)."""
+    from antrea_amd import workload
+    done, elapsed, seed = 0, 0.0, workload.PKT_SEED
+    s0 = pipe.stats()
+    pipe.classify(workload.gen_packets(wl, 256, seed=seed - 1), threads=threads, count=True)  # warm
+    while elapsed < seconds:
+        cols = workload.gen_packets(wl, chunk, seed=seed)
+        seed += 1
+        t = time.perf_counter()
+        pipe.classify(cols, threads=threads, count=True)
+        elapsed += time.perf_counter() - t
+        done += chunk
+    s1 = pipe.stats()
+    per = {k: round((s1[k] - s0[k]) / max(1, done + 256), 1) for k in s1}
+    out = {"value": round(done / elapsed / 1e6, 6), "unit": "Mpps", "cores": threads, "kind": "port",
+           "sample": "%d packets of the same synthetic workload (%d-packet chunks), %.1f s, counters on; C restatement "
+                     "of OVS 2.17.7 classifier_lookup (TSS + prefix tries + conjunction soft loop) over the %d flows "
+                     "the oracle compiler emits" % (done, chunk, elapsed, pipe.n_flows),
+           "per_packet": per}
+    out.update(host_info())
+    return out
+
+
+class OracleWorker:
+    """CPU oracle in a spawned process (bench.py: parity stamp + CPU baseline)."""
+
+    def __init__(self, config: str, procs: Optional[int] = None):
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        self.procs = procs or cpu_threads()
+        self.conn, child = ctx.Pipe()
+        self.p = ctx.Process(target=_serve, args=(child, config, self.procs), daemon=True)
+        self.p.start()
+        self.info = None
+
+    def _ready(self, timeout=1800):
+        if self.info is None:
+            if not self.conn.poll(timeout):
+                raise TimeoutError("oracle worker setup")
+            self.info = self.conn.recv()
+        return self.info
+
+    def check(self, cols: Dict[str, np.ndarray], verdicts: np.ndarray) -> dict:
+        info = self._ready()
+        self.conn.send(("check", cols, verdicts))
+        res = self.conn.recv()
+        res["oracle_setup_s"] = info["setup_s"]
+        return res
+
+    def baseline(self, seconds: float, chunk: int = 4096) -> dict:
+        self._ready()
+        self.conn.send(("baseline", seconds, chunk))
+        return self.conn.recv()
+
+    def close(self):
+        try:
+            self.conn.send(("stop",))
+            self.conn.recv()
+        except Exception:
+            pass
+        self.p.join(timeout=10)
+        if self.p.is_alive():
+            self.p.terminate()

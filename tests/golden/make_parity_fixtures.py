@@ -1,0 +1,97 @@
+"""Generates tests/golden/parity_<config>.npz: the C oracle's verdicts and per-rule metrics for
+full-size workloads (TEST INFRASTRUCTURE; run here, on the CPU, never on the GPU box).
+
+    python tests/golden/make_parity_fixtures.py [C1 C2 C3 C4 ...]
+
+For each config: the workload (antrea_amd.workload, rule seed 0xA1E47) compiled by the ORACLE
+compiler (oracle/compiler.py), loaded into the C restatement of the OVS classifier
+(oracle/ovs_cls.c), which classifies N packets of the seeded generator (seed below) with counters
+on. Stored: the verdicts (n x 2 records of 8 B, gpc_verdict layout), the metrics
+{conj: (packets, bytes, sessions)} as NetworkPolicyMetrics parses the Metric-table dump, a SHA-256
+of the packet columns and of the rule list (so a generator change is detected instead of silently
+comparing different inputs), and for C4 the mask of packets that hit no Service (the oracle has no
+AntreaProxy stage; only those are comparable).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from antrea_amd import workload  # noqa: E402
+from oracle import parity  # noqa: E402
+
+SPECS = {  # config -> (packets, packet seed)
+    "C1": (100_000, 0xF1C1),
+    "C2": (100_000, 0xF1C2),
+    "C3": (100_000, 0xF1C3),
+    "C4": (100_000, 0xF1C4),
+}
+COLS = ("src", "dst", "sport", "dport", "proto", "out_port", "len")
+
+
+def cols_digest(cols) -> str:
+    h = hashlib.sha256()
+    for k in COLS:
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(cols[k]).tobytes())
+    return h.hexdigest()
+
+
+def rules_digest(wl) -> str:
+    return hashlib.sha256(json.dumps(wl.rules, sort_keys=True, default=str).encode()).hexdigest()
+
+
+def path(config: str) -> str:
+    return os.path.join(HERE, "parity_%s.npz" % config)
+
+
+def packets(config: str, wl=None):
+    n, seed = SPECS[config]
+    wl = wl or workload.CONFIGS[config]()
+    return wl, workload.gen_packets(wl, n, seed=seed)
+
+
+def make(config: str):
+    t0 = time.time()
+    wl, cols = packets(config)
+    pipe = parity.oracle_pipeline(wl)
+    t1 = time.time()
+    want = pipe.classify(cols, threads=parity.cpu_threads(), count=True)
+    t2 = time.time()
+    mask = parity.non_service_mask(wl, cols)
+    if getattr(wl, "svc_meta", None) is not None:
+        # counters of packets that hit a Service are not comparable: classify the non-Service ones
+        # again with counters on a fresh pipeline
+        pipe = parity.oracle_pipeline(wl)
+        sub = {k: v[mask] for k, v in cols.items()}
+        pipe.classify(sub, threads=parity.cpu_threads(), count=True)
+    m = parity.oracle_metrics(pipe)
+    conj = np.array(sorted(m), np.uint32)
+    met = np.array([m[int(c)] for c in conj], np.uint64).reshape(-1, 3)
+    np.savez_compressed(path(config), verdicts=np.ascontiguousarray(want).view(np.uint32).reshape(-1, 4),
+                        metric_conj=conj, metric_val=met, mask=mask, cols_sha256=cols_digest(cols),
+                        rules_sha256=rules_digest(wl), n_flows=pipe.n_flows)
+    print("%s: %d packets, %d flows, oracle setup %.0f s, classify %.1f s, %d comparable, %d metric rules"
+          % (config, len(cols["src"]), pipe.n_flows, t1 - t0, t2 - t1, int(mask.sum()), len(conj)))
+
+
+def load(config: str) -> dict:
+    with np.load(path(config), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["verdicts"] = np.ascontiguousarray(d["verdicts"]).view(parity.VERDICT_NP).reshape(-1, 2)
+    d["metrics"] = {int(c): tuple(int(x) for x in v) for c, v in zip(d["metric_conj"], d["metric_val"])}
+    return d
+
+
+if __name__ == "__main__":
+    for c in sys.argv[1:] or sorted(SPECS):
+        make(c)

@@ -1,0 +1,93 @@
+"""GPU tier at the BASELINE sizes: the HIP path (gpc_classify through the C-ABI) against the C
+oracle's verdicts and per-rule metrics, packet for packet.
+
+The oracle side is the committed fixture tests/golden/parity_<config>.npz, generated on the CPU by
+tests/golden/make_parity_fixtures.py: the ORACLE compiler's flows for the full workload (C2: 1k
+rules over AddressGroups of up to 1000 Pod IPs; C3: 100k rules, 1.67M flows; C4: C3 + 10k
+Services), classified by the C restatement of the OVS classifier (oracle/ovs_cls.c) with counters.
+Each test regenerates the same seeded inputs and first checks their SHA-256 against the fixture's,
+so the device and the oracle always classify identical packets under identical rules."""
+import copy
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from oracle import parity
+from tests.golden import make_parity_fixtures as fx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from antrea_amd.build import build
+    build()
+    import torch
+    assert torch.cuda.is_available(), "GPU tier needs a HIP device"
+
+
+def _classifier(wl, ipv6=False, rules=None):
+    c = gpc.Classifier(ipv4=not ipv6, ipv6=ipv6)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(rules if rules is not None else wl.rules))
+    if getattr(wl, "services", None):
+        workload.install_services(c, wl)
+    c.commit()
+    return c
+
+
+def _inputs(config):
+    f = fx.load(config)
+    wl, cols = fx.packets(config)
+    assert fx.cols_digest(cols) == str(f["cols_sha256"]), "packet generator drifted from the fixture"
+    assert fx.rules_digest(wl) == str(f["rules_sha256"]), "rule generator drifted from the fixture"
+    return f, wl, cols
+
+
+def _nonzero(m):
+    return {int(k): tuple(int(x) for x in v) for k, v in m.items() if any(v)}
+
+
+@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4"])
+def test_device_vs_oracle_fullscale(config):
+    """Verdicts (conj id, action, table, tier, flags) and NetworkPolicyMetrics of 100k packets at
+    full scale equal the C oracle's exactly (C4: the packets that hit no Service, with the Service
+    stage live in the kernel)."""
+    f, wl, cols = _inputs(config)
+    mask = f["mask"].astype(bool)
+    sub = cols if mask.all() else {k: v[mask] for k, v in cols.items()}
+    c = _classifier(wl)
+    got = c.classify_host(sub, count=True)
+    res = parity.compare(got, f["verdicts"][mask])
+    assert res["mismatches"] == 0, res
+    assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
+    acts = np.unique(got["action"])
+    assert {1, 2, 3} <= set(int(a) for a in acts), acts  # NO_MATCH, ALLOW and DROP all exercised
+
+
+def test_device_ipv6_vs_oracle_fullscale_c3():
+    """gpc_classify6 on full C3 embedded in fd00:10::/96 (IPv6 image, device LPM) equals the C
+    oracle's IPv4 verdicts of the same packets (the embedding preserves every match)."""
+    f, wl, cols = _inputs("C3")
+    c = _classifier(wl, ipv6=True, rules=workload.to_ipv6(wl).rules)
+    got = c.classify6_host(workload.packets_to_v6(cols), count=True)
+    res = parity.compare(got, f["verdicts"])
+    assert res["mismatches"] == 0, res
+    assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
+
+
+@pytest.mark.parametrize("dual", [False, True])
+def test_device_ipv6_vs_python_oracle_c1(dual):
+    """gpc_classify6 directly against the Python oracle over the oracle compiler's IPv6 flows
+    (ipv6_src / ipv6_dst / tcp6 ...), C1 and C1 dual-stack."""
+    from tests.test_ipv6 import _oracle6
+    wl = workload.config1(seed=4)
+    w6 = workload.to_ipv6(wl, dual=dual)
+    n = 2000
+    cols6 = workload.packets_to_v6(workload.gen_packets(wl, n, seed=4))
+    want = _oracle6(w6.rules, cols6, n)
+    c = _classifier(w6, ipv6=True)
+    got = c.classify6_host(cols6)
+    res = parity.compare(got, want)
+    assert res["mismatches"] == 0, res

@@ -49,51 +49,5 @@ def test_c_vs_python_oracle(name, seed):
         for j, v in enumerate((e, g)):
             assert tuple(got[i, j][["action", "conj_id", "table", "tier", "flags"]].item()) == v, (i, j)
 
-
-@pytest.fixture(scope="module")
-def full_c3():
-    """Full-size C3 (100k rules). The C oracle consumes the product compiler's flow dump; that dump
-    is itself pinned against the oracle compiler (tests/test_abi_compiler.py)."""
-    from antrea_amd import gpc
-    wl = workload.config3()
-    clf = gpc.Classifier()
-    clf.initialize()
-    clf.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
-    flows = clf.dump_flows()
-    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in wl.rules}
-    return wl, clf, CPipeline(flows, tiers)
-
-
-def test_emu_vs_c_oracle_full_c3(full_c3):
-    from tests import emu
-    wl, clf, pipe = full_c3
-    emu.commit_host(clf)
-    n = 4000
-    cols = workload.gen_packets(wl, n, seed=77)
-    want = pipe.classify(cols, threads=8)
-    got = emu.classify(clf, cols)
-    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
-    assert len(bad) == 0, (len(bad), got[bad[0]], want[bad[0]])
-
-
-def test_emu_vs_c_oracle_full_c2():
-    """Full-size C2 (1k rules over AddressGroups of 50-1000 Pod IPs): the group clauses are point
-    sets in the image's point hash and the driver entries probe them during the candidate scan;
-    verdicts equal the C oracle's."""
-    from antrea_amd import gpc
-    from tests import emu
-    wl = workload.config2()
-    clf = gpc.Classifier()
-    clf.initialize()
-    clf.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
-    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in wl.rules}
-    pipe = CPipeline(clf.dump_flows(), tiers)
-    emu.commit_host(clf)
-    assert clf.image_stats()["bytes"]["hash"] > 1 << 20  # the group clauses did go to the point hash
-    n = 20000
-    cols = workload.gen_packets(wl, n, seed=78)
-    want = pipe.classify(cols, threads=8)
-    got = emu.classify(clf, cols)
-    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
-    assert len(bad) == 0, (len(bad), got[bad[0]], want[bad[0]])
-    assert (got["action"] == ACT["ALLOW"]).sum() > n // 50
+# Full-size C2 / C3 parity of the product (host emulation and device) against the C oracle fed by
+# the ORACLE compiler's flows: tests/test_parity_fixtures.py and tests/test_gpu_fullscale.py.

@@ -1,0 +1,73 @@
+"""CPU tier around the full-scale oracle fixtures (tests/golden/parity_<config>.npz).
+
+* The seeded generators still produce exactly the fixture's inputs (SHA-256 of rules and packets).
+* The product's image, evaluated by the host emulation of the kernel body (tests/csrc/emu.cpp
+  includes the same core.hpp), equals the oracle's verdicts and metrics at full scale -- the CPU
+  half of what tests/test_gpu_fullscale.py checks on the device.
+* GPC_SLOW=1: regenerate a fixture from scratch (oracle compiler + C oracle) and compare.
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from oracle import parity
+from tests import emu
+from tests.golden import make_parity_fixtures as fx
+
+
+@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4"])
+def test_fixture_inputs_stable(config):
+    f = fx.load(config)
+    wl, cols = fx.packets(config)
+    assert fx.cols_digest(cols) == str(f["cols_sha256"])
+    assert fx.rules_digest(wl) == str(f["rules_sha256"])
+    assert f["verdicts"].shape == (len(cols["src"]), 2)
+
+
+@pytest.mark.parametrize("config", ["C2", "C3"])
+def test_emu_vs_oracle_fixture(config):
+    f = fx.load(config)
+    wl, cols = fx.packets(config)
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    emu.commit_host(c)
+    _, slots = c.counters()
+    arr = np.zeros((max(1, len(slots)), 3), dtype=np.uint64)
+    got = emu.classify(c, cols, counters=arr)
+    res = parity.compare(got, f["verdicts"])
+    assert res["mismatches"] == 0, res
+    m = {int(s): tuple(int(x) for x in arr[i]) for i, s in enumerate(slots) if s and arr[i].any()}
+    assert m == {k: v for k, v in f["metrics"].items() if any(v)}
+
+
+def test_c_oracle_metrics_parse_like_the_reference():
+    """The C oracle's Metric dump parses with the reference parser restated in oracle/compiler.py
+    into the same metrics the Python oracle reports for the same packets (C1)."""
+    from oracle import compiler as oc
+    from oracle import ovs_cls
+    wl = workload.config1(seed=3)
+    cols = workload.gen_packets(wl, 500, seed=3)
+    u = np.random.default_rng(3).random(500)
+    cols["ct_state"] = np.where(u < 0.7, 0x21, np.where(u < 0.9, 0x20, 0x22)).astype(np.uint8)
+    pipe = parity.oracle_pipeline(wl)
+    pipe.classify(cols, threads=2, count=True)
+    py = ovs_cls.Pipeline(parity.oracle_flows(wl), parity.tiers_of(wl))
+    for i in range(500):
+        py.classify({k: int(v[i]) for k, v in cols.items()})
+    d = py.metric_dumps()
+    assert parity.oracle_metrics(pipe) == oc.network_policy_metrics(d["EgressMetric"], d["IngressMetric"])
+
+
+@pytest.mark.skipif(os.environ.get("GPC_SLOW") != "1", reason="regenerates a fixture (minutes); GPC_SLOW=1")
+@pytest.mark.parametrize("config", ["C1", "C2", "C3"])
+def test_fixture_regenerates(config):
+    f = fx.load(config)
+    wl, cols = fx.packets(config)
+    pipe = parity.oracle_pipeline(wl)
+    want = pipe.classify(cols, threads=parity.cpu_threads(), count=True)
+    assert parity.compare(want, f["verdicts"])["mismatches"] == 0
+    assert parity.oracle_metrics(pipe) == f["metrics"]

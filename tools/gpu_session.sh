@@ -1,0 +1,67 @@
+#!/bin/bash
+# One GPU session on the gpurun box (run from the repo root):
+#   tools/gpu_session.sh TAG [STEPS...]
+# STEPS (default "tests smoke bench kt"):
+#   tests   pytest -m gpu (one process, per-test timeout)
+#   smoke   __graft_entry__.smoke()
+#   bench   python bench.py (default C3 line: PMC passes, parity stamp, CPU baseline)
+#   cfg:X   bench.py --config X (C1, C2, C4, C5) ; v6 = C3 in IPv6
+#   kt      rocprofv3 --kernel-trace --stats over a short bench run
+#   sq      rocprofv3 SQ counters ; tcc  TCC hit / miss ; fetch / write  FETCH_SIZE / WRITE_SIZE
+# Outputs under gpurun_out/TAG/. Every GPU step has its own time limit; the script stops at the
+# first failure (no retries).
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+export TMPDIR=/tmp
+TAG=${1:?tag}
+shift
+STEPS=${*:-tests smoke bench kt}
+O=gpurun_out/$TAG
+mkdir -p "$O"
+step() { echo "== $1 ($(date +%T))"; }
+KT_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-traffic --no-parity"
+pmc() {  # name, counters...
+  local name=$1; shift
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex classify -d "$O/pmc_$name" -o pmc \
+    --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-traffic --no-parity \
+    ${PMC_CFG:+--config $PMC_CFG} > "$O/pmc_$name.log" 2>&1
+}
+for s in $STEPS; do
+  case $s in
+    tests)
+      step tests
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread \
+        > "$O/gpu_tests.log" 2>&1; rc=$?
+      tail -5 "$O/gpu_tests.log"; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      step smoke
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || exit $?
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      step bench
+      timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
+      cat "$O/bench.json" ;;
+    cfg:*)
+      c=${s#cfg:}; step "bench $c"
+      if [ "$c" = v6 ]; then a="--family 6"; else a="--config $c"; fi
+      timeout -k 10 900 python -u bench.py $a > "$O/bench_$c.json" 2> "$O/bench_$c.err" || { tail -20 "$O/bench_$c.err"; exit 1; }
+      cat "$O/bench_$c.json" ;;
+    kt)
+      step "rocprof kernel trace"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- \
+        python3 bench.py $KT_ARGS ${PMC_CFG:+--config $PMC_CFG} > "$O/kt.log" 2>&1 || exit $?
+      tail -1 "$O/kt.log" ;;
+    sq)
+      step "rocprof SQ"
+      pmc sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
+        SQ_INSTS_VMEM_RD SQ_WAVES || exit $? ;;
+    tcc)
+      step "rocprof TCC"; pmc tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum || exit $? ;;
+    fetch)
+      step "rocprof FETCH_SIZE"; pmc fetch FETCH_SIZE || exit $? ;;
+    write)
+      step "rocprof WRITE_SIZE"; pmc write WRITE_SIZE || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+find "$O" -name "*.csv" | head -40
+echo "== done"
