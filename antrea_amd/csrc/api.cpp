@@ -623,6 +623,54 @@ int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   return GPC_OK;
 }
 
+int gpc_new_dns_conjunction(gpc_ctx* ctx, uint32_t id) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  try {
+    int rc = ctx->np.new_dns_conjunction(id);
+    Op op;
+    op.kind = Op::DNS_NEW;
+    op.id = id;
+    log_op(ctx, std::move(op));
+    return rc;
+  } catch (...) {
+    return -GPC_ENOMEM;
+  }
+}
+
+// AddAddressToDNSConjunction / DeleteAddressFromDNSConjunction (network_policy.go:781-789): the
+// Add/DeletePolicyRuleAddress of the DNS conjunction's to clause at priority 64991.
+int gpc_add_dns_conj_addrs(gpc_ctx* ctx, uint32_t id, const gpc_addr* addrs, size_t n) {
+  const uint16_t prio = kPriorityDNSIntercept;
+  return gpc_add_rule_addrs(ctx, id, GPC_DST_ADDRESS, addrs, n, &prio, 0, 0);
+}
+
+int gpc_del_dns_conj_addrs(gpc_ctx* ctx, uint32_t id, const gpc_addr* addrs, size_t n) {
+  const uint16_t prio = kPriorityDNSIntercept;
+  return gpc_del_rule_addrs(ctx, id, GPC_DST_ADDRESS, addrs, n, &prio);
+}
+
+int gpc_network_policy_flow_keys(gpc_ctx* ctx, const char* name, const char* ns, uint8_t policy_type, char* buf,
+                                 size_t cap, size_t* needed, size_t* n_keys) {
+  if (!ctx || !name || !ns) return -GPC_EINVAL;
+  std::string s;
+  size_t n = 0;
+  try {
+    std::lock_guard<std::mutex> g(ctx->ctl);  // the replayMutex write lock of the reference
+    for (auto& k : ctx->np.flow_keys(name, ns, policy_type)) {
+      if (n++) s += "\n";
+      s += k;
+    }
+  } catch (...) {
+    return -GPC_ENOMEM;
+  }
+  if (needed) *needed = s.size() + 1;
+  if (n_keys) *n_keys = n;
+  if (!buf || cap < s.size() + 1) return -GPC_ERANGE;
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return GPC_OK;
+}
+
 int gpc_get_policy_info(gpc_ctx* ctx, uint32_t rule_id, gpc_policy_info* out) {
   if (!ctx || !out) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);

@@ -27,7 +27,8 @@ static const char* kTableNames[TB_COUNT] = {"",
                                             "ServiceLB",
                                             "EndpointDNAT",
                                             "SNATMark",
-                                            "SNAT"};
+                                            "SNAT",
+                                            "IngressSecurityClassifier"};
 
 const char* table_name(uint8_t t) { return t < TB_COUNT ? kTableNames[t] : "?"; }
 
@@ -134,6 +135,11 @@ std::string Match::str(uint16_t priority) const {  // getFlowModMatch, utils.go:
     for (int i = 0; i < 8; i++)
       if (ct_mask & (1u << i)) s += std::string((ct_data & (1u << i)) ? "+" : "-") + cts[i];
   }
+  if (has_ct_mark) {  // matchCtMarkToString (utils.go:287), Uint32Message data / mask
+    if (ct_mark_m == 0xffffffffu) std::snprintf(buf, sizeof buf, ",ct_mark=0x%x", ct_mark_v);
+    else std::snprintf(buf, sizeof buf, ",ct_mark=0x%x/0x%x", ct_mark_v, ct_mark_m);
+    s += buf;
+  }
   if (has_ct_label) {
     std::snprintf(buf, sizeof buf, ",ct_label=0x%llx/0x%llx", (unsigned long long)label_v, (unsigned long long)label_m);
     s += buf;
@@ -194,6 +200,15 @@ std::string Action::str() const {  // utils.go:600-760 (the subset NP flows use)
                     table_name(uint8_t(a)), b);
       return buf;
     case ACT_RESUBMIT: return std::string("resubmit:") + table_name(uint8_t(a));
+    case ACT_METER: return "meter:" + std::to_string(a);
+    case ACT_CONTROLLER: {  // nxActionController2ToString (utils.go:800-838)
+      std::string ud;
+      for (uint32_t i = 0; i < a && i < 4; i++) {
+        std::snprintf(buf, sizeof buf, "%s%02x", i ? "." : "", (b >> (8 * i)) & 0xffu);
+        ud += buf;
+      }
+      return "controller(id=" + std::to_string(kControllerId) + ",reason=no_match,userdata=" + ud + ",max_len=65535)";
+    }
   }
   return "";
 }
@@ -712,7 +727,10 @@ int FeatureNP::load_flows(const std::vector<Flow>& flows, bool replace) {
   return GPC_OK;
 }
 
-int FeatureNP::initialize() {  // skipPolicyRuleCheckFlows (network_policy.go:2167-2211)
+// featureNetworkPolicy.initFlows (network_policy.go:2126-2142): ingressClassifierFlows on a K8s
+// Node (pipeline.go:2144-2182), skipPolicyRuleCheckFlows (network_policy.go:2167-2211) and
+// initLoggingFlows (:2249-2269).
+int FeatureNP::initialize() {
   uint8_t eg = TB_EGRESS, in = TB_INGRESS;
   uint16_t prio = kPriorityHigh;
   if (cfg_.enable_antrea_policy) {
@@ -721,6 +739,42 @@ int FeatureNP::initialize() {  // skipPolicyRuleCheckFlows (network_policy.go:21
     prio = kPriorityTopAntreaPolicy;
   }
   std::vector<Flow> flows;
+  if (!cfg_.external_node) {
+    for (uint32_t mark : {kToGatewayMark, kToTunnelMark, kToUplinkMark}) {
+      Flow f;
+      f.table = TB_INGRESS_CLASSIFIER;
+      f.priority = kPriorityNormal;
+      f.cookie = cfg_.cookie;
+      f.m.set_reg(0, mark, 0xf0);
+      f.acts = {go(TB_INGRESS_METRIC)};
+      flows.push_back(f);
+    }
+    Flow h;  // hairpin Service connections skip to stageConntrack
+    h.table = TB_INGRESS_CLASSIFIER;
+    h.priority = kPriorityNormal;
+    h.cookie = cfg_.cookie;
+    h.m.has_ct_mark = true;
+    h.m.ct_mark_v = h.m.ct_mark_m = kHairpinCTMark;
+    h.acts = {go(TB_CONNTRACK_COMMIT)};
+    flows.push_back(h);
+  }
+  for (uint32_t ops = 1; ops <= 7; ops++) {  // logging | store-deny | reject operations -> packet-in
+    Flow f;
+    f.table = TB_OUTPUT;
+    f.priority = kPriorityNormal;
+    f.cookie = cfg_.cookie;
+    f.m.set_reg(0, (ops << 25) | (2u << 21), 0xfe600000u);
+    if (cfg_.ovs_meters) {
+      Action m{ACT_METER};
+      m.a = kMeterNP;
+      f.acts.push_back(m);
+    }
+    Action c{ACT_CONTROLLER};
+    c.a = 2;
+    c.b = kPacketInCategoryNP | (ops << 8);
+    f.acts.push_back(c);
+    flows.push_back(f);
+  }
   for (uint8_t fam : ip_protocols_) {
     for (auto tm : {std::make_pair(eg, uint8_t(TB_EGRESS_METRIC)), std::make_pair(in, uint8_t(TB_INGRESS_METRIC))}) {
       for (int bit : {1, 2}) {  // est, rel
@@ -1338,6 +1392,108 @@ int FeatureNP::policy_info(uint32_t id, gpc_policy_info* out) const {
   std::snprintf(out->rule_name, sizeof out->rule_name, "%s", c.rule_name.c_str());
   std::snprintf(out->log_label, sizeof out->log_label, "%s", c.log_label.c_str());
   return GPC_OK;
+}
+
+// dnsPacketInFlow (pipeline.go:2080-2093)
+Flow FeatureNP::dns_packet_in_flow(uint32_t id) const {
+  Flow f;
+  f.table = TB_AP_INGRESS;
+  f.priority = kPriorityDNSIntercept;
+  f.cookie = cfg_.cookie;
+  f.m.has_conj = true;
+  f.m.conj_id = id;
+  if (cfg_.ovs_meters) {
+    Action m{ACT_METER};
+    m.a = kMeterDNS;
+    f.acts.push_back(m);
+  }
+  Action c{ACT_CONTROLLER};
+  c.a = 1;
+  c.b = kPacketInCategoryDNS;
+  f.acts.push_back(c);
+  f.acts.push_back(go(TB_INGRESS_METRIC));
+  return f;
+}
+
+// NewDNSPacketInConjunction (network_policy.go:697-779): a conjunction without NetworkPolicy
+// reference whose service clause (1/2) matches solicited DNS responses (ct_state=+rpl+trk, TCP and
+// UDP source port 53 per IP family) and whose to clause (2/2) gets the FQDN policy's Pod addresses
+// through AddAddressToDNSConjunction.
+int FeatureNP::new_dns_conjunction(uint32_t id) {
+  if (policy_cache_.count(id)) return GPC_OK;  // "DNS Conjunction has already been added to cache"
+  auto c = std::make_shared<Conjunction>();
+  c->id = id;
+  c->has_ref = false;
+  c->rule_table = TB_AP_INGRESS;
+  c->action_flows.push_back(dns_packet_in_flow(id));
+  auto mk = [&](uint8_t clause) {
+    auto cl = std::make_unique<Clause>();
+    cl->action.conj_id = id;
+    cl->action.clause_id = clause;
+    cl->action.n_clause = 2;
+    cl->rule_table = TB_AP_INGRESS;
+    cl->drop_table = 0;
+    return cl;
+  };
+  c->svc = mk(1);
+  c->to = mk(2);
+  std::vector<const Flow*> add{&c->action_flows[0]};
+  apply_bundle(add, {});
+  std::vector<CtxChange> chs;
+  for (uint8_t fam : ip_protocols_) {
+    for (MatchKeyId k : {fam == 4 ? MK_TCP_SRC : MK_TCPV6_SRC, fam == 4 ? MK_UDP_SRC : MK_UDPV6_SRC}) {
+      ConjMatch m;
+      m.table = TB_AP_INGRESS;
+      m.has_prio = true;
+      m.prio = kPriorityDNSIntercept;
+      MatchValue ct;
+      ct.tag = V_CTSTATE;
+      ct.u = 0x28;  // +rpl+trk
+      ct.mask = 0x28;
+      MatchValue port;
+      port.tag = V_BITRANGE;
+      port.u = 53;
+      port.mask = -1;
+      m.pairs = {{MK_CT_STATE, ct}, {k, port}};
+      CtxChange ch;
+      if (add_conj_match_flow(c->svc.get(), m, false, false, &ch)) chs.push_back(std::move(ch));
+    }
+  }
+  apply_changes(chs);
+  policy_cache_[id] = c;
+  return GPC_OK;
+}
+
+static std::string flow_dump_key(const Flow& f) {  // getFlowDumpKey (pipeline.go:385-387, utils.go:1226-1242)
+  std::string m = f.m.str(f.priority), out;
+  size_t pos = 0;
+  while (pos <= m.size()) {
+    size_t e = m.find(',', pos);
+    if (e == std::string::npos) e = m.size();
+    std::string part = m.substr(pos, e - pos);
+    if (part.compare(0, 8, "priority") != 0) out += (out.empty() ? "" : ",") + part;
+    pos = e + 1;
+  }
+  return std::string("table=") + table_name(f.table) + "," + out;
+}
+
+// GetNetworkPolicyFlowKeys (network_policy.go:1712-1736) over getAllFlowKeys (:1520-1545): per rule
+// of the policy its action flows, conjunctive match flows, then drop flows; duplicates kept.
+std::vector<std::string> FeatureNP::flow_keys(const std::string& name, const std::string& ns, uint8_t type) const {
+  std::vector<std::string> keys;
+  for (auto& kv : policy_cache_) {
+    const Conjunction& c = *kv.second;
+    if (!c.has_ref || c.pname != name || c.ns != ns || c.policy_type != type) continue;
+    std::vector<std::string> drops;
+    for (auto& f : c.action_flows) keys.push_back(flow_dump_key(f));
+    for (Clause* cl : c.clauses())
+      for (auto& m : cl->matches) {
+        if (m.second->flow) keys.push_back(flow_dump_key(*m.second->flow));
+        if (m.second->drop_flow) drops.push_back(flow_dump_key(*m.second->drop_flow));
+      }
+    keys.insert(keys.end(), drops.begin(), drops.end());
+  }
+  return keys;
 }
 
 std::string FeatureNP::dump() const {

@@ -119,6 +119,8 @@ class FeatureNP {
   int del_rule_addrs(uint32_t id, int addr_type, const gpc_addr* a, size_t n, const uint16_t* prio);
   int reassign_priorities(const uint16_t* from, const uint16_t* to, size_t n, uint8_t table);
   int policy_info(uint32_t id, gpc_policy_info* out) const;
+  int new_dns_conjunction(uint32_t id);
+  std::vector<std::string> flow_keys(const std::string& name, const std::string& ns, uint8_t type) const;
 
   const std::map<std::string, Flow>& installed() const { return installed_; }
   // Flow-text ingest: applies parsed flows as one bundle. replace = drop the
@@ -156,6 +158,7 @@ class FeatureNP {
   Flow conjunction_pass_flow(uint32_t id, uint8_t table, uint16_t prio, bool logging) const;
   std::vector<Flow> allow_metric_flows(uint32_t id, bool ingress) const;
   Flow deny_metric_flow(uint32_t id, bool ingress) const;
+  Flow dns_packet_in_flow(uint32_t id) const;
   void add_flow_match(Match& m, const MatchPair& p) const;
 
   // clause logic

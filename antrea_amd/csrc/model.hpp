@@ -36,14 +36,20 @@ enum TableId : uint8_t {
   TB_ENDPOINT_DNAT = 13,
   TB_SNAT_MARK = 14,
   TB_SNAT = 15,
-  TB_COUNT = 16
+  TB_INGRESS_CLASSIFIER = 16,  // IngressSecurityClassifier (pipeline.go:2144-2182)
+  TB_COUNT = 17
 };
 const char* table_name(uint8_t t);
 inline bool is_egress_table(uint8_t t) { return t == TB_AP_EGRESS || t == TB_EGRESS || t == TB_EGRESS_DEFAULT || t == TB_EGRESS_METRIC; }
 uint8_t next_table(uint8_t t);
 
 constexpr uint16_t kPriorityHigh = 210, kPriorityNormal = 200, kPriorityLow = 190;
-constexpr uint16_t kPriorityTopAntreaPolicy = 64990;
+constexpr uint16_t kPriorityTopAntreaPolicy = 64990, kPriorityDNSIntercept = 64991;
+constexpr uint32_t kControllerId = 32776;                      // the agent's OpenFlow controller id
+constexpr uint32_t kMeterNP = 256, kMeterDNS = 258;            // client.go:851-858 packet-in meters
+constexpr uint32_t kPacketInCategoryNP = 1, kPacketInCategoryDNS = 2;  // packetin.go:44-52
+// PktDestinationField reg0[4..7] values (fields.go:54-57) and HairpinCTMark ct_mark[6] (:211-213)
+constexpr uint32_t kToTunnelMark = 0x10, kToGatewayMark = 0x20, kToUplinkMark = 0x40, kHairpinCTMark = 0x40;
 constexpr uint32_t kCtZone = 0xfff0, kCtZoneV6 = 0xffe6;
 constexpr uint32_t kUnknownLabelIdentity = 0xffffff;
 constexpr uint16_t kEthIP = 0x0800, kEthIPv6 = 0x86dd;
@@ -71,6 +77,8 @@ struct Match {
   uint32_t conj_id = 0;
   bool has_ct_state = false;
   uint8_t ct_data = 0, ct_mask = 0;
+  bool has_ct_mark = false;
+  uint32_t ct_mark_v = 0, ct_mark_m = 0xffffffffu;
   bool has_ct_label = false;
   uint64_t label_v = 0, label_m = 0;  // ct_label[0..63]
   IPMatch ct_nw_src, ct_nw_dst;
@@ -102,7 +110,9 @@ enum ActKind : uint8_t {
   ACT_CONJ, ACT_SET_REG, ACT_CT_COMMIT, ACT_GOTO, ACT_GROUP, ACT_DROP,
   ACT_CT_DNAT,     // ct(commit,table=a,zone=b,nat(dst=c:lv),exec(ServiceCTMark, reg0[0..3]->ct_mark))
   ACT_CT_HAIRPIN,  // ct(commit,table=a,zone=b,exec(ConnSNATCTMark, HairpinCTMark))
-  ACT_RESUBMIT     // resubmit:a (group buckets)
+  ACT_RESUBMIT,    // resubmit:a (group buckets)
+  ACT_METER,       // meter:a
+  ACT_CONTROLLER   // controller(id=32776,reason=no_match,userdata=<a bytes of b, low first>,max_len=65535)
 };
 
 struct Action {

@@ -43,7 +43,7 @@ struct OwnedRule {
 };
 
 struct Op {
-  enum Kind { INIT, INSTALL, BATCH, UNINSTALL, ADD, DEL, REASSIGN, LOAD, COMMIT } kind = COMMIT;
+  enum Kind { INIT, INSTALL, BATCH, UNINSTALL, ADD, DEL, REASSIGN, LOAD, DNS_NEW, COMMIT } kind = COMMIT;
   std::vector<OwnedRule> rules;
   uint32_t id = 0;
   int32_t addr_type = 0;
@@ -76,6 +76,7 @@ struct Op {
       case DEL: return np.del_rule_addrs(id, addr_type, addrs.data(), addrs.size(), has_prio ? &prio : nullptr);
       case REASSIGN: return np.reassign_priorities(from.data(), to.data(), from.size(), table);
       case LOAD: return np.load_flows(flows, replace);
+      case DNS_NEW: return np.new_dns_conjunction(id);
       case COMMIT: return GPC_OK;
     }
     return GPC_OK;

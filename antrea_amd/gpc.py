@@ -39,7 +39,8 @@ VTABLE_ENDPOINT_DNAT = 4
 class gpc_config(C.Structure):
     _fields_ = [("ipv4_enabled", C.c_int32), ("ipv6_enabled", C.c_int32), ("enable_antrea_policy", C.c_int32),
                 ("enable_deny_tracking", C.c_int32), ("cookie", C.c_uint64), ("device", C.c_int32),
-                ("compact_after", C.c_int32), ("reserved", C.c_int32 * 6)]
+                ("compact_after", C.c_int32), ("ovs_meters", C.c_int32), ("external_node", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 class gpc_addr(C.Structure):
@@ -68,7 +69,7 @@ class gpc_rule(C.Structure):
 class gpc_pkt_soa(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("src", "dst", "sport", "dport", "proto", "out_port", "in_port", "svc_group",
                                           "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "len",
-                                          "src6", "dst6", "ct_src6", "ct_dst6")]
+                                          "src6", "dst6", "ct_src6", "ct_dst6", "ct_mark")]
 
 
 class gpc_policy_info(C.Structure):
@@ -110,7 +111,8 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_install_service_group", "gpc_uninstall_service_group", "gpc_install_endpoint_flows",
            "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
-           "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6"]
+           "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
+           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys"]
 
 _lib = None
 
@@ -162,6 +164,11 @@ def load(path: str = LIB_PATH):
     lib.gpc_classify6.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32, vp]
     lib.gpc_classify6_host.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32]
     lib.gpc_debug_image6.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp), C.POINTER(sz)]
+    lib.gpc_new_dns_conjunction.argtypes = [vp, C.c_uint32]
+    lib.gpc_add_dns_conj_addrs.argtypes = [vp, C.c_uint32, C.POINTER(gpc_addr), sz]
+    lib.gpc_del_dns_conj_addrs.argtypes = [vp, C.c_uint32, C.POINTER(gpc_addr), sz]
+    lib.gpc_network_policy_flow_keys.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_uint8, C.c_char_p, sz, C.POINTER(sz),
+                                                 C.POINTER(sz)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -293,7 +300,7 @@ PKT_COLUMNS = {"src": np.uint32, "dst": np.uint32, "sport": np.uint16, "dport": 
                "out_port": np.uint32, "in_port": np.uint32, "svc_group": np.uint32, "tun_id": np.uint32,
                "ct_src": np.uint32, "ct_dst": np.uint32, "ct_state": np.uint8, "dest": np.uint8, "len": np.uint16,
                # IPv6 batches: (n, 16) uint8, network byte order
-               "src6": np.uint8, "dst6": np.uint8, "ct_src6": np.uint8, "ct_dst6": np.uint8}
+               "src6": np.uint8, "dst6": np.uint8, "ct_src6": np.uint8, "ct_dst6": np.uint8, "ct_mark": np.uint8}
 
 
 def pkt_soa_host(cols: Dict[str, np.ndarray]):
@@ -329,12 +336,13 @@ class Classifier:
     """One gpc context (one GPU)."""
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
-                 cookie=0x1020000000000, device=0, compact_after=0):
+                 cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True):
         self.lib = load()
         cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
                          enable_antrea_policy=int(enable_antrea_policy),
                          enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device,
-                         compact_after=int(compact_after))
+                         compact_after=int(compact_after), ovs_meters=int(ovs_meters),
+                         external_node=int(not k8s_node))
         h = C.c_void_p()
         _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
         self.h = h
@@ -395,6 +403,30 @@ class Classifier:
         ref = ({v: k for k, v in POLICY_TYPES.items()}[info.policy_type], info.policy_namespace.decode(),
                info.policy_name.decode(), info.policy_uid.decode())
         return (True, ref, str(info.of_priority), info.rule_name.decode(), info.log_label.decode())
+
+    # --- DNS packet-in conjunction (client.go:310-317)
+    def new_dns_packet_in_conjunction(self, conj_id: int):
+        _check(self.lib.gpc_new_dns_conjunction(self.h, conj_id), "NewDNSPacketInConjunction")
+
+    def add_address_to_dns_conjunction(self, conj_id: int, addrs):
+        arr = (gpc_addr * max(1, len(addrs)))(*[_addr(a) for a in addrs])
+        _check(self.lib.gpc_add_dns_conj_addrs(self.h, conj_id, arr, len(addrs)), "AddAddressToDNSConjunction")
+
+    def delete_address_from_dns_conjunction(self, conj_id: int, addrs):
+        arr = (gpc_addr * max(1, len(addrs)))(*[_addr(a) for a in addrs])
+        _check(self.lib.gpc_del_dns_conj_addrs(self.h, conj_id, arr, len(addrs)), "DeleteAddressFromDNSConjunction")
+
+    def get_network_policy_flow_keys(self, name: str, namespace: str, policy_type: str) -> List[str]:
+        need, nk = C.c_size_t(), C.c_size_t()
+        args = (self.h, name.encode(), namespace.encode(), POLICY_TYPES[policy_type])
+        rc = self.lib.gpc_network_policy_flow_keys(*args, None, 0, C.byref(need), C.byref(nk))
+        if rc not in (0, -GPC_ERANGE):
+            _check(rc, "GetNetworkPolicyFlowKeys")
+        buf = C.create_string_buffer(need.value)
+        _check(self.lib.gpc_network_policy_flow_keys(*args, buf, need.value, C.byref(need), C.byref(nk)),
+               "GetNetworkPolicyFlowKeys")
+        text = buf.value.decode()
+        return text.split("\n") if nk.value else []
 
     def network_policy_metrics(self) -> Dict[int, tuple]:
         n = C.c_size_t()

@@ -366,7 +366,10 @@ def main():
 
     parity = None
     if worker is not None and not args.no_parity:
-        idx = torch.linspace(0, n - 1, min(n, PARITY_SAMPLE), device=dev).long()
+        k = min(n, PARITY_SAMPLE)
+        idx_h = (torch.arange(k, dtype=torch.int64) * n) // k  # integer stride: every index < n
+        assert int(idx_h.max()) < n and int(idx_h.min()) >= 0
+        idx = idx_h.to(dev)
         sample = _host_sample(cols4, idx)
         got = np.ascontiguousarray(v8[idx].cpu().numpy()).view(VERDICT_DTYPE).reshape(-1, 2)
         _log("parity check of %d sampled packets (waiting for the oracle process)" % len(idx))

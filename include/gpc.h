@@ -4,7 +4,7 @@
  * Drop-in boundary for the NetworkPolicy half of Antrea's `openflow.Client`
  * (reference: pkg/agent/openflow/client.go:56-414; NP methods :128-148, 215-223, 240-251, 310-317;
  * implementation pkg/agent/openflow/network_policy.go). A Go `pkg/agent/gpuclassify` layer binds
- * these symbols over cgo; C++ callers use include/gpc_client.hpp; the Python
+ * these symbols over cgo; C++ callers include this header directly; the Python
  * test harness and bench use ctypes.
  *
  * Conventions
@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GPC_ABI_VERSION 2
+#define GPC_ABI_VERSION 3
 
 /* ---------------------------------------------------------------------------- error codes */
 #define GPC_OK 0
@@ -101,6 +101,9 @@ enum gpc_verdict_action {
 #define GPC_VFLAG_PASS 0x1    /* a Pass rule of the AntreaPolicy table was hit on the way      */
 #define GPC_VFLAG_TIE 0x2     /* >1 conjunction completed at the winning priority (OVS-defined
                                  order; resolved to the lowest conj id)                        */
+#define GPC_VFLAG_PACKETIN 0x4 /* the deciding flow sends the packet to the controller (the DNS
+                                  interception flow, pipeline.go:2080-2093: paused, resumed at
+                                  IngressMetric)                                               */
 
 /* Packet destination class, as IngressSecurityClassifier sees reg0 (fields.go PktDestinationField). */
 enum gpc_dest { GPC_DEST_POD = 0, GPC_DEST_GATEWAY = 1, GPC_DEST_TUNNEL = 2, GPC_DEST_UPLINK = 3 };
@@ -109,6 +112,7 @@ enum gpc_dest { GPC_DEST_POD = 0, GPC_DEST_GATEWAY = 1, GPC_DEST_TUNNEL = 2, GPC
 #define GPC_CT_REL 0x04
 #define GPC_CT_RPL 0x08
 #define GPC_CT_TRK 0x20
+#define GPC_CT_MARK_HAIRPIN 0x40 /* HairpinCTMark ct_mark[6] (fields.go:211-213)                */
 
 /* ---------------------------------------------------------------------------- records */
 typedef struct gpc_ctx gpc_ctx;
@@ -122,7 +126,9 @@ typedef struct gpc_config {
   int32_t device;                /* HIP device ordinal used by this context                    */
   int32_t compact_after;         /* live journal rules that start a background compaction
                                     (0: max(2048, rules / 32); < 0: never in the background)   */
-  int32_t reserved[6];
+  int32_t ovs_meters;            /* OVS meters supported: packet-in flows carry meter:256/258    */
+  int32_t external_node;         /* config.ExternalNode: no IngressSecurityClassifier flows      */
+  int32_t reserved[4];
 } gpc_config;
 
 typedef struct gpc_addr {        /* 24 bytes */
@@ -193,6 +199,7 @@ typedef struct gpc_pkt_soa {
   const uint8_t* dst6;           /* ipv6_dst */
   const uint8_t* ct_src6;        /* ct_ipv6_src */
   const uint8_t* ct_dst6;        /* ct_ipv6_dst */
+  const uint8_t* ct_mark;        /* ct_mark[0..7] (0); GPC_CT_MARK_HAIRPIN steers IngressSecurityClassifier */
 } gpc_pkt_soa;
 
 typedef struct gpc_verdict {     /* 8 bytes; gpc_classify writes 2 per packet: [egress, ingress] */
@@ -304,6 +311,20 @@ int gpc_del_rule_addrs(gpc_ctx* ctx, uint32_t rule_id, int32_t addr_type, const 
 int gpc_reassign_priorities(gpc_ctx* ctx, const uint16_t* from, const uint16_t* to, size_t n, uint8_t table);
 /* GetPolicyInfoFromConjunction(ruleID)                        network_policy.go:1555 */
 int gpc_get_policy_info(gpc_ctx* ctx, uint32_t rule_id, gpc_policy_info* out);
+/* NewDNSPacketInConjunction(id) error                        client.go:311, network_policy.go:697-779
+ * A conjunction without NetworkPolicy reference: solicited DNS responses (ct_state=+rpl+trk,
+ * TCP/UDP tp_src=53) to the addresses added below are sent to the controller (paused) and resumed
+ * at IngressMetric (verdict BYPASS + GPC_VFLAG_PACKETIN). A second call with the same id is a no-op. */
+int gpc_new_dns_conjunction(gpc_ctx* ctx, uint32_t id);
+/* AddAddressToDNSConjunction(id, addrs) error                 client.go:314, network_policy.go:781-784 */
+int gpc_add_dns_conj_addrs(gpc_ctx* ctx, uint32_t id, const gpc_addr* addrs, size_t n);
+/* DeleteAddressFromDNSConjunction(id, addrs) error            client.go:317, network_policy.go:786-789 */
+int gpc_del_dns_conj_addrs(gpc_ctx* ctx, uint32_t id, const gpc_addr* addrs, size_t n);
+/* GetNetworkPolicyFlowKeys(npName, npNamespace, npType) []string   client.go:219, network_policy.go:1712-1736
+ * '\n'-separated keys "table=<name>,<match without priority>" (getFlowDumpKey): per rule of the
+ * policy its action flows, conjunctive match flows, then drop flows; duplicates kept. */
+int gpc_network_policy_flow_keys(gpc_ctx* ctx, const char* name, const char* ns, uint8_t policy_type, char* buf,
+                                 size_t cap, size_t* needed, size_t* n_keys);
 /* NetworkPolicyMetrics() map[uint32]*types.RuleMetric          network_policy.go:2034
  * Reads the per-rule device counters of this context. */
 int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n);

@@ -18,7 +18,7 @@ F = {"dl_type": 0, "nw_proto": 1, "nw_src": 2, "nw_dst": 3, "ct_nw_src": 4, "ct_
 TABLE_IDS = {"AntreaPolicyEgressRule": 1, "EgressRule": 2, "EgressDefaultRule": 3, "AntreaPolicyIngressRule": 4,
              "IngressRule": 5, "IngressDefaultRule": 6, "EgressMetric": 7, "IngressMetric": 8, "L3Forwarding": 9,
              "ConntrackCommit": 10, "Output": 11}
-A_CONJ, A_SET_REG, A_CT_COMMIT, A_GOTO, A_GROUP = 1, 2, 3, 4, 5
+A_CONJ, A_SET_REG, A_CT_COMMIT, A_GOTO, A_GROUP, A_CONTROLLER = 1, 2, 3, 4, 5, 6
 
 # numpy twins of the C records (same layout as ocls_flow / ocls_action)
 FLOW_DT = np.dtype([("table", "<i4"), ("priority", "<u4"), ("val", "<u4", (NF,)), ("mask", "<u4", (NF,)),
@@ -32,7 +32,7 @@ STAT_NAMES = ("lookups", "subtables_probed", "subtables_skipped_by_trie", "soft_
 
 class OPkts(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("src", "dst", "sport", "dport", "proto", "out_port", "in_port", "svc_group",
-                                          "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "len")]
+                                          "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "len", "ct_mark")]
 
 
 _lib = None
@@ -116,6 +116,8 @@ def _convert_lines(flow_lines: List[str]):
                 acts.append((A_GOTO, 0, TABLE_IDS.get(a[1], 0), 0, 0, 0, 0))
             elif a[0] == "group":
                 acts.append((A_GROUP, 0, a[1], 0, 0, 0, 0))
+            elif a[0] == "controller":
+                acts.append((A_CONTROLLER, 0, 0, 0, 0, 0, 0))
         rec["act_off"] = off
         rec["n_act"] = len(acts) - off
         rec["soft"] = int(soft)
@@ -184,7 +186,8 @@ class CPipeline:
         n = None
         dts = {"src": np.uint32, "dst": np.uint32, "sport": np.uint16, "dport": np.uint16, "proto": np.uint8,
                "out_port": np.uint32, "in_port": np.uint32, "svc_group": np.uint32, "tun_id": np.uint32,
-               "ct_src": np.uint32, "ct_dst": np.uint32, "ct_state": np.uint8, "dest": np.uint8, "len": np.uint16}
+               "ct_src": np.uint32, "ct_dst": np.uint32, "ct_state": np.uint8, "dest": np.uint8, "len": np.uint16,
+               "ct_mark": np.uint8}
         for k, dt in dts.items():
             if k in cols:
                 a = np.ascontiguousarray(cols[k], dtype=dt)

@@ -13,7 +13,9 @@ Restates, function by function, the NetworkPolicy half of `openflow.Client`:
 * GetPolicyInfoFromConjunction       `network_policy.go:1555-1565`
 * service match pairs / port ranges  `network_policy.go:891-1017`, `third_party/networkpolicy/port_range.go:45-132`
 * flow builders                      `pkg/agent/openflow/pipeline.go:1604-1670, 1718-1886, 1896-2076`
-* skip-policy-rule-check init flows  `network_policy.go:2167-2211`
+* initFlows (classifier, skip, log)  `network_policy.go:2126-2269`, `pipeline.go:2144-2182`
+* DNS packet-in conjunction          `network_policy.go:697-789`, `pipeline.go:2080-2093`
+* GetNetworkPolicyFlowKeys           `network_policy.go:1520-1545, 1712-1736`
 * flow -> ovs-ofctl text             `pkg/ovs/openflow/utils.go:255-580, 748-752, 905-1241`
 
 Input records are plain dicts (the JSON test-vector format, see tests/golden/README.md), so this
@@ -34,6 +36,13 @@ PRIORITY_NORMAL = 200
 PRIORITY_LOW = 190
 PRIORITY_TOP_ANTREA_POLICY = 64990
 PRIORITY_DNS_INTERCEPT = 64991
+DNS_PORT = 53
+PACKET_IN_METER_NP, PACKET_IN_METER_DNS = 256, 258          # client.go:851-858 meter ids
+PACKET_IN_CATEGORY_NP, PACKET_IN_CATEGORY_DNS = 1, 2       # packetin.go:44-52
+CONTROLLER_ID = 32776                                       # the agent's OpenFlow controller id
+# IngressSecurityClassifier marks (fields.go PktDestinationField reg0[4..7], HairpinCTMark ct_mark[6])
+TO_GATEWAY, TO_TUNNEL, TO_UPLINK = 0x20, 0x10, 0x40
+HAIRPIN_CT_MARK = 0x40
 
 CT_ZONE = 0xFFF0
 CT_ZONE_V6 = 0xFFE6
@@ -401,6 +410,9 @@ def match_to_string(f: Flow) -> str:
             if mk & (1 << i):
                 s += ("+" if d & (1 << i) else "-") + _CT_STATES[i]
         parts.append("ct_state=" + s)
+    if "ct_mark" in m:
+        d, mk = m["ct_mark"]
+        parts.append("ct_mark=0x%x/0x%x" % (d, mk) if mk is not None and mk != 0xFFFFFFFF else "ct_mark=0x%x" % d)
     if "ct_label" in m:
         d, mk = m["ct_label"]
         parts.append("ct_label=0x%x/0x%x" % (d, mk) if mk != (1 << 128) - 1 else "ct_label=0x%x" % d)
@@ -460,6 +472,11 @@ def _action_to_string(a) -> str:
         return "group:%d" % a[1]
     if kind == "drop":
         return "drop"
+    if kind == "meter":            # ("meter", id)                       utils.go:623
+        return "meter:%d" % a[1]
+    if kind == "controller":       # ("controller", userdata bytes)      utils.go:800-838
+        return "controller(id=%d,reason=no_match,userdata=%s,max_len=65535)" % (
+            CONTROLLER_ID, ".".join("%02x" % b for b in a[1]))
     raise ValueError(kind)
 
 
@@ -469,6 +486,13 @@ def flow_to_string(f: Flow) -> str:
     acts = [_action_to_string(a) for a in f.actions if a[0] != "drop"]
     astr = "actions=" + (",".join(acts) if acts else "drop")
     return "%s, %s %s" % (base, match_to_string(f), astr)
+
+
+def flow_dump_key(f: Flow) -> str:
+    """getFlowDumpKey (pipeline.go:385-387, utils.go:1226-1242): the match without its priority,
+    prefixed by the table (named here: the build has no numeric OVS table ids)."""
+    parts = [p for p in match_to_string(f).split(",") if not p.startswith("priority")]
+    return "table=%s,%s" % (f.table, ",".join(parts))
 
 
 def flow_identity(f: Flow):
@@ -561,8 +585,10 @@ class FeatureNetworkPolicy:
     realized on OVS (the `installed` map stands in for ovs-vswitchd's flow table)."""
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
-                 cookie=0x1020000000000, bundle_fail=False):
+                 cookie=0x1020000000000, bundle_fail=False, ovs_meters=False, k8s_node=True):
         self.ip_protocols = (["ip"] if ipv4 else []) + (["ipv6"] if ipv6 else [])
+        self.ovs_meters = ovs_meters
+        self.k8s_node = k8s_node
         self.enable_antrea_policy = enable_antrea_policy
         self.enable_deny_tracking = enable_deny_tracking
         self.cookie = cookie
@@ -588,6 +614,25 @@ class FeatureNetworkPolicy:
             self.installed[flow_identity(f)] = f
 
     def init_flows(self) -> List[Flow]:
+        """featureNetworkPolicy.initFlows (network_policy.go:2126-2142): ingressClassifierFlows on a K8s
+        Node (pipeline.go:2144-2182), skipPolicyRuleCheckFlows (:2167-2211), initLoggingFlows
+        (:2249-2269)."""
+        flows = []
+        if self.k8s_node:
+            for mark in (TO_GATEWAY, TO_TUNNEL, TO_UPLINK):
+                flows.append(Flow("IngressSecurityClassifier", PRIORITY_NORMAL, {"reg0": (mark, 0xF0)},
+                                  [("goto_table", "IngressMetric")], self.cookie))
+            flows.append(Flow("IngressSecurityClassifier", PRIORITY_NORMAL, {"ct_mark": (HAIRPIN_CT_MARK, HAIRPIN_CT_MARK)},
+                              [("goto_table", "ConntrackCommit")], self.cookie))
+        flows += self.skip_flows()
+        for ops in range(1, 8):  # logging + store-deny + reject operations
+            acts = [("meter", PACKET_IN_METER_NP)] if self.ovs_meters else []
+            acts.append(("controller", (PACKET_IN_CATEGORY_NP, ops)))
+            flows.append(Flow("Output", PRIORITY_NORMAL, {"reg0": ((ops << 25) | (2 << 21), 0xFE600000)}, acts,
+                              self.cookie))
+        return flows
+
+    def skip_flows(self) -> List[Flow]:
         """skipPolicyRuleCheckFlows (network_policy.go:2167-2211)."""
         flows = []
         eg, ing, prio = "EgressRule", "IngressRule", PRIORITY_HIGH
@@ -1073,6 +1118,71 @@ class FeatureNetworkPolicy:
                     new_matches[ctx.match.key()] = ctx
                     self.global_cache[ctx.match.key()] = ctx
                 cl.matches = new_matches
+
+    # ----- DNS packet-in conjunction (network_policy.go:697-789) ----------------------------
+    def dns_packet_in_flow(self, cid) -> Flow:
+        """pipeline.go:2080-2093: conj_id=id -> [meter,] paused packet-in to the FQDN controller, then
+        IngressMetric."""
+        acts = [("meter", PACKET_IN_METER_DNS)] if self.ovs_meters else []
+        acts += [("controller", (PACKET_IN_CATEGORY_DNS,)), ("goto_table", "IngressMetric")]
+        return Flow("AntreaPolicyIngressRule", PRIORITY_DNS_INTERCEPT, {"conj_id": (cid, None)}, acts, self.cookie)
+
+    def new_dns_packet_in_conjunction(self, cid):
+        """NewDNSPacketInConjunction (network_policy.go:697-779): service clause 1/2 = solicited DNS
+        responses (ct_state=+rpl+trk, tcp/udp tp_src=53 per IP family), to clause 2/2 filled by
+        AddAddressToDNSConjunction; no NetworkPolicyReference."""
+        if cid in self.policy_cache:
+            return
+        table = "AntreaPolicyIngressRule"
+        conj = Conjunction(cid)
+        conj.np_ref = None
+        conj.rule_table = table
+        conj.action_flows = [self.dns_packet_in_flow(cid)]
+        self._apply(add=conj.action_flows)
+        conj.service_clause = Clause(ConjAction(cid, 1, 2), table, None)
+        conj.to_clause = Clause(ConjAction(cid, 2, 2), table, None)
+        ct = (MatchCTState, ("ctstate", 0b00101000, 0b00101000))
+        changes = []
+        for ipp in self.ip_protocols:
+            tcp, udp = (MatchTCPSrcPort, MatchUDPSrcPort) if ipp == "ip" else (MatchTCPv6SrcPort, MatchUDPv6SrcPort)
+            for key in (tcp, udp):
+                m = ConjunctiveMatch(table, PRIORITY_DNS_INTERCEPT, [ct, (key, ("bitrange", DNS_PORT, None))])
+                ch = self._add_conjunctive_match_flow(conj.service_clause, m, False, False)
+                if ch is not None:
+                    changes.append(ch)
+        self._apply_changes(changes)
+        self.policy_cache[cid] = conj
+
+    def add_address_to_dns_conjunction(self, cid, addresses):
+        """AddAddressToDNSConjunction (network_policy.go:781-784)."""
+        self.add_policy_rule_address(cid, "dst", addresses, PRIORITY_DNS_INTERCEPT)
+
+    def delete_address_from_dns_conjunction(self, cid, addresses):
+        """DeleteAddressFromDNSConjunction (network_policy.go:786-789)."""
+        self.delete_policy_rule_address(cid, "dst", addresses, PRIORITY_DNS_INTERCEPT)
+
+    # ----- flow keys (network_policy.go:1520-1545, 1712-1736) ------------------------------
+    def get_network_policy_flow_keys(self, name, namespace, policy_type) -> List[str]:
+        """GetNetworkPolicyFlowKeys: per rule of the policy, action flows, conjunctive match flows,
+        then drop flows (getAllFlowKeys); duplicates kept (shared contexts)."""
+        keys = []
+        for conj in self.policy_cache.values():
+            if conj.np_ref is None:
+                continue
+            ptype, ns, pname = conj.np_ref[0], conj.np_ref[1], conj.np_ref[2]
+            if (pname, ns, ptype) != (name, namespace, policy_type):
+                continue
+            fk, dk = [flow_dump_key(f) for f in conj.action_flows], []
+            for cl in (conj.from_clause, conj.to_clause, conj.service_clause):
+                if cl is None:
+                    continue
+                for ctx in cl.matches.values():
+                    if ctx.flow is not None:
+                        fk.append(flow_dump_key(ctx.flow))
+                    if ctx.drop_flow is not None:
+                        dk.append(flow_dump_key(ctx.drop_flow))
+            keys += fk + dk
+        return keys
 
     def get_policy_info_from_conjunction(self, rule_id):
         """GetPolicyInfoFromConjunction (network_policy.go:1555-1565)."""

@@ -100,6 +100,12 @@ def parse_actions(s: str):
             acts.append(("goto_table", t))
         elif a.startswith("group:"):
             acts.append(("group", int(a[6:])))
+        elif a.startswith("meter:"):
+            acts.append(("meter", int(a[6:])))
+        elif a.startswith("controller(") and a.endswith(")"):
+            kv = dict(x.split("=", 1) for x in _split_top(a[len("controller("):-1]) if "=" in x)
+            ud = tuple(int(b, 16) for b in kv["userdata"].split(".")) if "userdata" in kv else ()
+            acts.append(("controller", ud))
         else:
             acts.append(("other", a))
     return acts
@@ -155,8 +161,8 @@ def parse_flow(line: str) -> dict:
                 if sign == "+":
                     data |= b
             m["ct_state"] = (data, mask)
-        elif k == "ct_label":
-            m["ct_label"] = _vm(v)
+        elif k in ("ct_label", "ct_mark"):
+            m[k] = _vm(v)
         elif k in ("nw_src", "nw_dst", "ct_nw_src", "ct_nw_dst"):
             m[k] = _ip(v, 32)
         elif k in ("ipv6_src", "ipv6_dst", "ct_ipv6_src", "ct_ipv6_dst"):

@@ -46,7 +46,7 @@ enum {
 };
 
 /* flow action kinds (decoded by oracle/cls_c.py from the flow text) */
-enum { A_CONJ = 1, A_SET_REG = 2, A_CT_COMMIT = 3, A_GOTO = 4, A_GROUP = 5 };
+enum { A_CONJ = 1, A_SET_REG = 2, A_CT_COMMIT = 3, A_GOTO = 4, A_GROUP = 5, A_CONTROLLER = 6 };
 
 typedef struct {
   uint8_t kind, reg;
@@ -71,6 +71,7 @@ typedef struct {
   const uint32_t *in_port, *svc_group, *tun_id, *ct_src, *ct_dst;
   const uint8_t *ct_state, *dest;
   const uint16_t* len;
+  const uint8_t* ct_mark;    /* HairpinCTMark = 0x40 (NULL: 0) */
 } ocls_pkts;
 
 static void* xmalloc(size_t n) {
@@ -615,7 +616,7 @@ static void stage(const ocls* c, ws_t* w, int base, uint32_t* pv, uint32_t len, 
       continue;
     }
     const ocls_flow* f = &c->flows[fi];
-    int go = -1, deny = 0, reject = 0, group = 0;
+    int go = -1, deny = 0, reject = 0, group = 0, commit = 0;
     for (int a = 0; a < f->n_act; a++) {
       const ocls_action* ac = &c->acts[f->act_off + a];
       if (ac->kind == A_SET_REG) {
@@ -624,7 +625,10 @@ static void stage(const ocls* c, ws_t* w, int base, uint32_t* pv, uint32_t len, 
         if (fld >= 0) pv[fld] = (pv[fld] & ~m) | (v & m);
         if (ac->reg == 0 && (v & m & 0x400)) deny = 1;
         if (ac->reg == 0 && m == 0xfe000000u && ((v >> 25) & 4)) reject = 1;
+      } else if (ac->kind == A_CONTROLLER) {
+        flags |= 4; /* packet-in (paused for the DNS interception flow) */
       } else if (ac->kind == A_CT_COMMIT) {
+        commit = 1;
         pv[F_LABEL_LO] = (pv[F_LABEL_LO] & ~(uint32_t)ac->lm) | ((uint32_t)ac->lv & (uint32_t)ac->lm);
         pv[F_LABEL_HI] = (pv[F_LABEL_HI] & ~(uint32_t)(ac->lm >> 32)) | ((uint32_t)(ac->lv >> 32) & (uint32_t)(ac->lm >> 32));
         go = (int)ac->a;
@@ -638,16 +642,21 @@ static void stage(const ocls* c, ws_t* w, int base, uint32_t* pv, uint32_t len, 
     tindex = (uint32_t)(t - base);
     uint32_t cid = f->mask[F_CONJ_ID] ? f->val[F_CONJ_ID] : 0;
     if (cid) {
-      conj = cid;
       if (deny) {
+        conj = cid;
         action = reject ? ACT_REJECT : ACT_DROP;
         go = metric;
       } else if (go == t2 || (group && ((pv[F_REG0] >> 11) & 3) == 3)) {
+        conj = cid;
         flags |= 1;
         t = t2;
         continue;
-      } else {
+      } else if (commit) {
+        conj = cid;
         action = ACT_ALLOW;
+        go = metric;
+      } else { /* conj_id flow straight to the Metric table, no commit (DNS interception) */
+        action = ACT_BYPASS;
         go = metric;
       }
     } else {
@@ -698,7 +707,7 @@ static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo
     if (ea == ACT_DROP || ea == ACT_REJECT || ea == ACT_ISO_DROP) {
       gc = 0;
       gp = ACT_NONE;
-    } else if (p->dest && p->dest[i] != 0) {
+    } else if ((p->dest && p->dest[i] != 0) || (p->ct_mark && (p->ct_mark[i] & 0x40))) {
       gc = 0;
       gp = ACT_BYPASS;
     } else {

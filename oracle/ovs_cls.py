@@ -25,7 +25,8 @@ from .flowtext import parse_flow, parse_group
 
 # verdict action codes (must equal include/gpc.h GPC_ACT_*)
 ACT_NONE, ACT_NO_MATCH, ACT_ALLOW, ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP, ACT_BYPASS = range(7)
-FLAG_PASS, FLAG_TIE = 1, 2
+FLAG_PASS, FLAG_TIE, FLAG_PACKETIN = 1, 2, 4
+HAIRPIN_CT_MARK = 0x40  # fields.go HairpinCTMark (ct_mark[6]): IngressSecurityClassifier -> ConntrackCommit
 # packet destination classes seen by IngressSecurityClassifier (fields.go PktDestinationField)
 DEST_POD, DEST_GATEWAY, DEST_TUNNEL, DEST_UPLINK = 0, 1, 2, 3
 CT_NEW, CT_EST, CT_REL, CT_RPL, CT_TRK = 1, 2, 4, 8, 32
@@ -96,6 +97,8 @@ def _field(pkt: dict, st: dict, name: str):
         return st["conj_id"]
     if name == "ct_label":
         return st["ct_label"]
+    if name == "ct_mark":
+        return pkt.get("ct_mark", 0)
     if name == "reg1":
         return pkt.get("out_port", 0)
     if name == "reg7":
@@ -243,6 +246,7 @@ class Pipeline:
             goto = None
             deny = False
             reject = False
+            commit = False
             for a in f["actions"]:
                 if a[0] == "set_reg":
                     _, r, v, m = a
@@ -256,6 +260,9 @@ class Pipeline:
                     for v, m in a[2]:
                         st["ct_label"] = (st["ct_label"] & ~m) | (v & m)
                     goto = a[1]
+                    commit = True
+                elif a[0] == "controller":  # packet-in (paused for the DNS interception flow)
+                    flags |= FLAG_PACKETIN
                 elif a[0] == "goto_table":
                     goto = a[1]
                 elif a[0] == "group":
@@ -265,18 +272,25 @@ class Pipeline:
                 flags |= FLAG_TIE
             tindex = order.index(t) + 1
             if cid:
-                conj = cid
                 if deny:
+                    conj = cid
                     action = ACT_REJECT if reject else ACT_DROP
                     goto = metric
                 elif goto in (t2,) or (goto == "group" and not deny and st["regs"].get(0, 0) & 0x1800 == 0x1800):
                     # Pass: the conj id stays in reg5/reg6 (traceflow readback) unless a later
                     # table's rule overwrites it
+                    conj = cid
                     flags |= FLAG_PASS
                     t = t2
                     continue
-                else:
+                elif commit:
+                    conj = cid
                     action = ACT_ALLOW
+                    goto = metric
+                else:
+                    # a conj_id flow straight to the Metric table without a commit (the DNS
+                    # interception flow, pipeline.go:2080-2093): no rule verdict in the registers
+                    action = ACT_BYPASS
                     goto = metric
             else:
                 if goto is None or goto == "Output":  # drop, or logging drop via packet-in
@@ -308,8 +322,9 @@ class Pipeline:
         if e[0] in (ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP):
             return ev, (ACT_NONE, 0, 0, 0, 0)
         st = {"regs": {}, "ct_label": st["ct_label"], "conj_id": 0}
-        if pkt.get("dest", DEST_POD) != DEST_POD:
-            # IngressSecurityClassifier: to gateway / tunnel / uplink -> IngressMetric
+        if pkt.get("dest", DEST_POD) != DEST_POD or pkt.get("ct_mark", 0) & HAIRPIN_CT_MARK:
+            # IngressSecurityClassifier (pipeline.go:2144-2182): to gateway / tunnel / uplink ->
+            # IngressMetric; hairpin connections -> ConntrackCommit
             return ev, (ACT_BYPASS, 0, 0, 0, 0)
         i = self._stage(INGRESS, pkt, st)
         iv = (i[0], i[1], i[2], self.tiers.get(i[1], 0) if i[1] else 0, i[3])

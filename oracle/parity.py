@@ -111,7 +111,10 @@ def _serve(conn, config: str, procs: int):
     pipe = oracle_pipeline(wl, procs=procs)
     conn.send({"ready": True, "setup_s": round(time.time() - t0, 1), "flows": pipe.n_flows})
     while True:
-        msg = conn.recv()
+        try:
+            msg = conn.recv()
+        except EOFError:  # the parent went away
+            return
         if msg[0] == "check":
             _, cols, verdicts = msg
             t = time.time()
@@ -160,9 +163,12 @@ class OracleWorker:
         ctx = mp.get_context("spawn")
         self.procs = procs or cpu_threads()
         self.conn, child = ctx.Pipe()
-        self.p = ctx.Process(target=_serve, args=(child, config, self.procs), daemon=True)
+        # not a daemon: the worker forks a pool to convert large flow dumps
+        self.p = ctx.Process(target=_serve, args=(child, config, self.procs), daemon=False)
         self.p.start()
         self.info = None
+        import atexit
+        atexit.register(self.close)  # runs before multiprocessing joins its children
 
     def _ready(self, timeout=1800):
         if self.info is None:
@@ -184,11 +190,16 @@ class OracleWorker:
         return self.conn.recv()
 
     def close(self):
+        if not self.p.is_alive():
+            return
         try:
-            self.conn.send(("stop",))
-            self.conn.recv()
+            if self.info is not None:  # idle between requests: ask it to stop
+                self.conn.send(("stop",))
+                if self.conn.poll(10):
+                    self.conn.recv()
         except Exception:
             pass
-        self.p.join(timeout=10)
+        self.p.join(timeout=5)
         if self.p.is_alive():
             self.p.terminate()
+            self.p.join(timeout=5)
