@@ -318,6 +318,10 @@ static void compactor_main(gpc_ctx* ctx) {
         } while (!at_marker);
         if (rc) break;
         FeatureNP::Dirty d = shadow.take_dirty();
+        if (d.hard_tables & FeatureNP::kDirtyClassifier) {  // the base no longer matches: give up this round
+          rc = -GPC_EINVAL;
+          break;
+        }
         std::string err;
         if ((!d.conj.empty() || d.hard_tables) && jn->apply(shadow, ctx->slots, d.conj, d.hard_tables, &err) != GPC_OK)
           rc = -GPC_EINVAL;
@@ -776,6 +780,7 @@ int gpc_classify6_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdic
   up(pk->ct_state, 1, (const void**)&d.ct_state);
   up(pk->dest, 1, (const void**)&d.dest);
   up(pk->len, 2, (const void**)&d.len);
+  up(pk->ct_mark, 1, (const void**)&d.ct_mark);
   void* dout = nullptr;
   if (!rc && hip_ok(hipMalloc(&dout, n * 2 * sizeof(gpc_verdict)))) rc = -GPC_EDEV;
   if (!rc) rc = gpc_classify6(ctx, &d, n, (gpc_verdict*)dout, count, nullptr);
@@ -819,6 +824,7 @@ int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verd
   up(pk->ct_state, 1, (const void**)&d.ct_state);
   up(pk->dest, 1, (const void**)&d.dest);
   up(pk->len, 2, (const void**)&d.len);
+  up(pk->ct_mark, 1, (const void**)&d.ct_mark);
   void* dout = nullptr;
   void* dlb = nullptr;
   if (!rc && hip_ok(hipMalloc(&dout, n * 2 * sizeof(gpc_verdict)))) rc = -GPC_EDEV;
@@ -994,7 +1000,9 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   }
   if (ctx->comp_pending) ctx->dirty_hist.push_back({commit_no, dirty});
   const bool have_base = !ctx->last.blob.empty();
-  bool full = force_full || !have_base || ctx->last.any_noact || ctx->np.foreign() || ctx->journal.any_noact ||
+  const bool classifier_changed = (dirty.hard_tables & FeatureNP::kDirtyClassifier) != 0;
+  dirty.hard_tables &= uint8_t(~FeatureNP::kDirtyClassifier);
+  bool full = force_full || !have_base || classifier_changed || ctx->last.any_noact || ctx->np.foreign() || ctx->journal.any_noact ||
               ctx->journal.n_live > std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction) ||
               ctx->journal.pool.size() > kPoolWords * 7 / 8;
   int rc = GPC_OK;

@@ -76,7 +76,8 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
     bool live = true;
     if (kStage == 2) {  // packets the ingress launch settles without table work weigh nothing
       const uint32_t ea = out[i].y & 0xffu;
-      live = ea != RV_DROP && ea != RV_REJECT && ea != RV_ISO_DROP && !(pk.dest && pk.dest[i]);
+      live = ea != RV_DROP && ea != RV_REJECT && ea != RV_ISO_DROP &&
+             !ingress_bypass(ep.hdr->isc, pk.dest ? pk.dest[i] : 0u, pk.ct_mark ? pk.ct_mark[i] : 0u);
     }
     if (live) {
       const uint32_t src = pk.src[i], dst = pk.dst[i];
@@ -152,6 +153,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   uint32_t out_port = pk.out_port[i];
   uint32_t svc_group = pk.svc_group ? pk.svc_group[i] : 0u;
   uint32_t dest = pk.dest ? pk.dest[i] : 0u;
+  const uint32_t ct_mark = pk.ct_mark ? pk.ct_mark[i] : 0u;
   if (kSvc) {  // both launches derive the same Endpoint (the selection is a pure function of the packet)
     uint32_t lb[4];
     const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
@@ -169,8 +171,8 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
       if (kV6) out[i] = make_uint4(prev.x, prev.y, 0u, 0u);  // ingress NONE over the parked codes
       return;
     }
-    if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
-      out[i] = make_uint4(prev.x, prev.y, 0u, uint32_t(RV_BYPASS));
+    if (const uint32_t b = ingress_bypass(ep.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
+      out[i] = make_uint4(prev.x, prev.y, 0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
       return;
     }
   }
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
     im.n_img = 2u;
   }
-  PacketOut o = classify_packet<kDelta, kStage>(im, p, dest);
+  PacketOut o = classify_packet<kDelta, kStage>(im, p, dest, ct_mark);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
     unsigned long long* const copy = counters + size_t(blockIdx.x & ep.ctr_mask) * ep.ctr_stride;

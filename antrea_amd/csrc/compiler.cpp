@@ -664,6 +664,8 @@ void FeatureNP::note_flow(const Flow& f) {
     } else {
       dirty_.hard_tables |= uint8_t(1u << (f.table - 1));
     }
+  } else if (f.table == TB_INGRESS_CLASSIFIER) {
+    dirty_.hard_tables |= kDirtyClassifier;  // ImageHdr.isc changes: the next commit rebuilds
   } else if (f.table == TB_EGRESS_METRIC || f.table == TB_INGRESS_METRIC) {
     const Match& m = f.m;
     if (m.has_ct_label) dirty_.conj.insert(f.table == TB_INGRESS_METRIC ? uint32_t(m.label_v & 0xffffffffu) : uint32_t(m.label_v >> 32));

@@ -137,8 +137,9 @@ class FeatureNP {
   // added or removed (a shared context gaining rule B does not dirty rule A).
   struct Dirty {
     std::set<uint32_t> conj;
-    uint8_t hard_tables = 0;  // bit t-1 for rule table t
+    uint8_t hard_tables = 0;  // bit t-1 for rule table t; kDirtyClassifier: IngressSecurityClassifier
   };
+  static constexpr uint8_t kDirtyClassifier = 0x80;
   Dirty take_dirty() {
     Dirty d = std::move(dirty_);
     dirty_ = Dirty();

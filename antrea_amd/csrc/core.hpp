@@ -55,7 +55,8 @@ enum Axis : uint8_t {
 //   w2 flags byte (RecFlags) | off0 << 8 | off1 << 16 | off2 << 24   (word offsets of the clauses)
 //   w3 counter slot
 //   w4 tier | rid << 8                                               (rid: image-wide rule id)
-//   w5 clauses decided exactly by a passing driver entry: bits 0-2 (driver clause 0), 3-5 (1)
+//   w5 clauses decided exactly by a passing driver entry: bits 0-2 (driver clause 0), 3-5 (1);
+//      bit 8 (kRecPacketIn): the action flow sends the packet to the controller (GPC_VFLAG_PACKETIN)
 // clause k at word off_k: nseg, then nseg segments, each a tag word kind | axis << 4 | n << 8
 // followed by its data:
 //   SK_IVAL  2n words, sorted disjoint [lo,hi]     SK_XIVAL  1 word: offset of the 2n words
@@ -77,6 +78,7 @@ GPC_HD uint32_t rec_counted(uint32_t w2) { return (w2 >> 5) & 1u; }
 GPC_HD uint32_t rec_nclauses(uint32_t w2) { return (w2 >> 6) & 3u; }
 GPC_HD uint32_t rec_off(uint32_t w2, uint32_t k) { return (w2 >> (8 + 8 * k)) & 0xffu; }
 constexpr uint32_t kRecHdrWords = 6;
+constexpr uint32_t kRecPacketIn = 1u << 8;
 constexpr uint32_t kBoxWords = 7;
 
 constexpr int kMaxClauses = 3;
@@ -118,7 +120,20 @@ struct ImageHdr {
   uint32_t hash_log2;
   uint32_t n_slots;
   uint32_t v6_lpm;      // IPv6 image: word offset of its V6Lpm block (0 in IPv4 images)
+  uint32_t isc;         // IngressSecurityClassifier bypasses installed (kIsc* bits)
 };
+// IngressSecurityClassifier (pipeline.go:2144-2182), from the installed flows: bit d (gpc_dest d =
+// gateway 1, tunnel 2, uplink 3) -- packets to that destination skip to IngressMetric; kIscHairpin
+// -- ct_mark HairpinCTMark skips to ConntrackCommit. All at one priority, so a packet hitting two of
+// them is an overlap of different actions (TIE).
+constexpr uint32_t kIscGateway = 1u << GPC_DEST_GATEWAY, kIscTunnel = 1u << GPC_DEST_TUNNEL,
+                   kIscUplink = 1u << GPC_DEST_UPLINK, kIscHairpin = 1u << 4;
+// 0: the packet takes the ingress policy tables; else RV_BYPASS, | kHTie when two bypasses overlap.
+GPC_HD uint32_t ingress_bypass(uint32_t isc, uint32_t dest, uint32_t ct_mark) {
+  const bool d = dest != 0 && dest < 4 && ((isc >> dest) & 1u);
+  const bool h = (ct_mark & GPC_CT_MARK_HAIRPIN) && (isc & kIscHairpin);
+  return (d || h) ? (uint32_t(RV_BYPASS) | ((d && h) ? (1u << 8) : 0u)) : 0u;
+}
 
 struct Pkt {
   uint32_t ax[AX_N];
@@ -145,6 +160,7 @@ struct TableResult {
   uint8_t counted;
   uint32_t conj;
   uint32_t slot;
+  uint32_t pin;     // GPC_VFLAG_PACKETIN or 0
 };
 
 // ------------------------------------------------------------------------------ hashing / buckets
@@ -779,6 +795,7 @@ GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_bl
   res.counted = 0;
   res.conj = 0;
   res.slot = 0;
+  res.pin = 0;
   const bool hf = (q.h & kHFound) != 0, have = (q.s & kSHave) != 0;
   if (have && !(q.s & kSNoAct)) {
     const uint32_t* rec = ((q.s & kSImg) ? ovl_blob : base_blob) + q.win;
@@ -789,6 +806,7 @@ GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_bl
       res.tier = uint8_t(rec[4] & 0xffu);
       res.counted = uint8_t(rec_counted(w2));
       res.slot = rec[3];
+      res.pin = (rec[5] & kRecPacketIn) ? uint32_t(GPC_VFLAG_PACKETIN) : 0u;
       if (q.s & kSTie) res.tie = 1;
       return res;
     }
@@ -1004,7 +1022,7 @@ struct PacketOut {
 // kStage: 0 = both stages; 1 = egress only; 2 = ingress only (the caller has checked that the
 // egress verdict lets the packet reach the ingress tables).
 template <bool kJournal = true, int kStage = 0>
-GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
+GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, uint32_t ct_mark) {
   PacketOut o;
   o.e.conj = o.g.conj = 0;
   o.e.packed = o.g.packed = 0;
@@ -1016,6 +1034,7 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
     const TableResult r = eval_table<kJournal>(im, t, p);
     const uint32_t i = t <= 3 ? t - 1 : t - 4;  // position inside the stage
     if (r.tie) flags |= 2;
+    flags |= r.pin;
     uint32_t act = 0, slot = 0;
     int counted = 0;
     if (r.verdict == RV_PASS) {
@@ -1049,8 +1068,8 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest) {
     o.ecounted = counted;
     if (kStage == 1) break;
     if (act == RV_DROP || act == RV_REJECT || act == RV_ISO_DROP) break;  // ingress never reached (NONE)
-    if (dest != 0) {  // IngressSecurityClassifier: to gateway / tunnel / uplink (pipeline.go:2144-2182)
-      o.g.packed = RV_BYPASS;
+    if (const uint32_t b = ingress_bypass(im.base.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
+      o.g.packed = b & 0xffu ? pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u) : 0u;
       break;
     }
     flags = conj = tier = 0;

@@ -219,6 +219,28 @@ bool parse_action(const std::string& a, Action* out) {
     out->a = uint32_t(v);
     return true;
   }
+  if (a.compare(0, 6, "meter:") == 0) {
+    if (!num(a.substr(6), &v)) return false;
+    *out = Action{ACT_METER};
+    out->a = uint32_t(v);
+    return true;
+  }
+  if (a.compare(0, 11, "controller(") == 0 && a.back() == ')') {  // utils.go:800-838 (userdata kept, <= 4 bytes)
+    *out = Action{ACT_CONTROLLER};
+    for (auto& part : split_top(a.substr(11, a.size() - 12), ',')) {
+      if (part.compare(0, 9, "userdata=") != 0) continue;
+      uint32_t n = 0, packed = 0;
+      for (auto& b : split_top(part.substr(9), '.')) {
+        char* end = nullptr;
+        unsigned long x = std::strtoul(b.c_str(), &end, 16);
+        if (b.empty() || !end || *end || x > 255 || n >= 4) return false;
+        packed |= uint32_t(x) << (8 * n++);
+      }
+      out->a = n;
+      out->b = packed;
+    }
+    return true;
+  }
   return false;
 }
 
@@ -260,7 +282,9 @@ int parse_flow_text(const std::string& line_in, Flow* f, std::string* err) {
     bool hm;
     if (k == "table") {
       int t = table_id(v);
-      if (t < 0 || t > TB_INGRESS_METRIC) return 0;  // not a NetworkPolicy table
+      // the NetworkPolicy tables, plus IngressSecurityClassifier and the packet-in flows of Output
+      // (initFlows, network_policy.go:2126-2142); any other table is not on this path
+      if (t < 0 || (t > TB_INGRESS_METRIC && t != TB_INGRESS_CLASSIFIER && t != TB_OUTPUT)) return 0;
       f->table = uint8_t(t);
       have_table = true;
     } else if (k == "priority") {
@@ -296,6 +320,11 @@ int parse_flow_text(const std::string& line_in, Flow* f, std::string* err) {
         if (sign == '+') m.ct_data |= uint8_t(1u << bit);
         i = j;
       }
+    } else if (k == "ct_mark") {
+      if (!value_mask(v, &x, &y, &hm)) return bad_value(k, v, err);
+      m.has_ct_mark = true;
+      m.ct_mark_v = uint32_t(x);
+      m.ct_mark_m = hm ? uint32_t(y) : 0xffffffffu;
     } else if (k == "ct_label") {
       if (!value_mask(v, &x, &y, &hm)) return bad_value(k, v, err);
       m.has_ct_label = true;
@@ -350,6 +379,7 @@ int parse_flow_text(const std::string& line_in, Flow* f, std::string* err) {
     if (a.empty()) continue;
     Action act{ACT_DROP};
     if (!parse_action(a, &act)) {
+      if (f->table == TB_OUTPUT) return 0;  // an Output flow of another feature
       *err = "unsupported action '" + a + "'";
       return -GPC_EINVAL;
     }

@@ -70,6 +70,7 @@ struct RuleB {
   uint16_t act_prio = 0;
   bool counted = false;
   uint8_t tier = 0;
+  bool pin = false;  // the action flow sends the packet to the controller (DNS interception)
 };
 
 inline uint32_t prefix_mask(int plen) { return plen <= 0 ? 0u : plen >= 32 ? 0xffffffffu : ~((1u << (32 - plen)) - 1); }
@@ -815,10 +816,13 @@ struct Gather {
   std::map<uint32_t, RuleB> soft[7];
   std::map<std::pair<int, int>, RuleB> hard[7];  // key (-priority, verdict)
   std::set<uint32_t> counted_allow, counted_deny;
+  uint32_t isc = 0;  // ImageHdr.isc: the IngressSecurityClassifier bypasses the installed flows define
   uint32_t n_flows = 0;
   std::string error;
   // only_conj != 0: take only that conjunction's actions of a soft flow (delta builds gather per rule).
   int add(const Flow& f, uint32_t only_conj = 0);
+  int add_isc(const Flow& f);
+  uint16_t isc_prio = 0;
   uint16_t eth() const { return fam == 4 ? kEthIP : kEthIPv6; }
   // One conjunction(id, k/n) action of soft flow f (delta builds: the action comes from the
   // context's action map, not from a scan of the flow's possibly long action list).
@@ -863,6 +867,7 @@ int Gather::add(const Flow& f, uint32_t only_conj) {
     }
     return GPC_OK;
   }
+  if (f.table == TB_INGRESS_CLASSIFIER) return add_isc(f);
   if (f.table < TB_AP_EGRESS || f.table > TB_INGRESS_DEFAULT) return GPC_OK;
   if (f.m.has_conj) {  // conj action flow
     Match rest = f.m;
@@ -882,6 +887,8 @@ int Gather::add(const Flow& f, uint32_t only_conj) {
     RuleB& r = soft[f.table][f.m.conj_id];
     r.conj_id = f.m.conj_id;
     r.verdict = v;
+    for (auto& act : f.acts)
+      if (act.kind == ACT_CONTROLLER) r.pin = true;
     if (fam_ok) {
       if (!r.has_act || f.priority > r.act_prio) r.act_prio = f.priority;
       r.has_act = true;
@@ -915,6 +922,36 @@ int Gather::add(const Flow& f, uint32_t only_conj) {
     r.verdict = v;
     if (ar == 0) r.clause[0].push_back(a);
   }
+  return GPC_OK;
+}
+
+// IngressSecurityClassifier flows (pipeline.go:2144-2182) -> ImageHdr.isc. Supported: the shapes
+// ingressClassifierFlows installs, at one priority: reg0=<PktDestinationField mark>/0xf0 and
+// ct_mark=0x40/0x40 (HairpinCTMark), each going to IngressMetric or ConntrackCommit (out of the
+// policy tables). Anything else is rejected: the kernel could not honour it.
+int Gather::add_isc(const Flow& f) {
+  const Match& m = f.m;
+  const bool out = f.acts.size() == 1 && f.acts[0].kind == ACT_GOTO &&
+                   (f.acts[0].a == TB_INGRESS_METRIC || f.acts[0].a == TB_CONNTRACK_COMMIT);
+  const uint16_t only_reg0 = 1u;
+  uint32_t bit = 0;
+  if (out && m.reg_present == only_reg0 && m.reg_m[0] == 0xf0u && !m.has_ct_mark) {
+    switch (m.reg_v[0]) {
+      case kToGatewayMark: bit = kIscGateway; break;
+      case kToTunnelMark: bit = kIscTunnel; break;
+      case kToUplinkMark: bit = kIscUplink; break;
+    }
+  } else if (out && m.reg_present == 0 && m.has_ct_mark && m.ct_mark_v == kHairpinCTMark && m.ct_mark_m == kHairpinCTMark) {
+    bit = kIscHairpin;
+  }
+  const bool rest = !m.has_conj && !m.has_ct_state && !m.has_ct_label && !m.has_dl && !m.has_tun && !m.has_in_port &&
+                    !m.nw_src.set && !m.nw_dst.set && !m.ct_nw_src.set && !m.ct_nw_dst.set && !m.has_tp_src && !m.has_tp_dst;
+  if (!bit || !rest || (isc_prio && isc_prio != f.priority)) {
+    error = "unsupported IngressSecurityClassifier flow: " + f.str();
+    return -GPC_EINVAL;
+  }
+  isc_prio = f.priority;
+  isc |= bit;
   return GPC_OK;
 }
 
@@ -1240,7 +1277,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
                (uint32_t(r.n & 3) << 6) | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
       rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0u;
       rec[4] = uint32_t(r.tier) | (orid << 8);
-      rec[5] = 0u;
+      rec[5] = (!r.hard && r.pin) ? kRecPacketIn : 0u;
       const uint32_t off = append(rec.data(), rec.size(), 16);
       if (r.hard) {
         hard_orids_[t - 1].push_back(orid);
@@ -1419,7 +1456,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
       rec[2] = flags | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
       rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0;
       rec[4] = uint32_t(r.tier) | (rid << 8);
-      rec[5] = r.hard ? 0u : (skip_mask(r, 0, span) | (skip_mask(r, 1, span) << 3));
+      rec[5] = r.hard ? 0u : (skip_mask(r, 0, span) | (skip_mask(r, 1, span) << 3) | (r.pin ? kRecPacketIn : 0u));
       if (base >= (1u << 28)) {  // Ent.x holds record offset / 16 in 24 bits
         out->error = "rule records exceed 1 GiB";
         return -GPC_ENOMEM;
@@ -1553,6 +1590,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
   out->hdr.hash_off = B.put(tab.data(), tab.size(), 16);
   out->bytes_hash = 8ull * tab.size();
   out->hdr.n_slots = slots.size();
+  out->hdr.isc = G.isc;
   out->n_rids = next_rid;
   T_.lap(3);
   T_.report("emit");

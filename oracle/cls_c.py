@@ -11,13 +11,13 @@ import numpy as np
 from . import cbuild
 from .flowtext import parse_flow
 
-NF = 18
+NF = 19
 F = {"dl_type": 0, "nw_proto": 1, "nw_src": 2, "nw_dst": 3, "ct_nw_src": 4, "ct_nw_dst": 5, "in_port": 6, "reg0": 7,
      "reg1": 8, "reg3": 9, "reg7": 10, "tun_id": 11, "tp_src": 12, "tp_dst": 13, "icmp_type": 12, "icmp_code": 13,
-     "ct_state": 14, "conj_id": 15}
+     "ct_state": 14, "conj_id": 15, "ct_mark": 18}
 TABLE_IDS = {"AntreaPolicyEgressRule": 1, "EgressRule": 2, "EgressDefaultRule": 3, "AntreaPolicyIngressRule": 4,
              "IngressRule": 5, "IngressDefaultRule": 6, "EgressMetric": 7, "IngressMetric": 8, "L3Forwarding": 9,
-             "ConntrackCommit": 10, "Output": 11}
+             "ConntrackCommit": 10, "Output": 11, "IngressSecurityClassifier": 12}
 A_CONJ, A_SET_REG, A_CT_COMMIT, A_GOTO, A_GROUP, A_CONTROLLER = 1, 2, 3, 4, 5, 6
 
 # numpy twins of the C records (same layout as ocls_flow / ocls_action)
@@ -70,7 +70,7 @@ def _convert_lines(flow_lines: List[str]):
     for li, line in enumerate(flow_lines):
         f = parse_flow(line)
         t = TABLE_IDS.get(f["table"], 0)
-        if not (1 <= t <= 8):
+        if not (1 <= t <= 8 or t == 12):
             continue
         m = f["match"]
         if any(x.startswith("ipv6") or x.startswith("ct_ipv6") for x in m) or m.get("dl_type", (0x800, 0))[0] != 0x800:
@@ -164,7 +164,7 @@ class CPipeline:
         flows, acts, kept = _convert(flow_lines, procs)
         self._flows = np.ascontiguousarray(flows, dtype=FLOW_DT)
         self._acts = np.ascontiguousarray(acts, dtype=ACT_DT)
-        assert self._flows.dtype.itemsize == 168 and self._acts.dtype.itemsize == 32
+        assert self._flows.dtype.itemsize == 176 and self._acts.dtype.itemsize == 32
         tiers = tiers or {}
         keys = np.array(sorted(tiers), dtype=np.uint32)
         vals = np.array([max(0, min(255, tiers[int(k)])) for k in keys], dtype=np.uint8)
@@ -205,7 +205,7 @@ class CPipeline:
         return {k: int(v) for k, v in zip(STAT_NAMES, out)}
 
     def n_subtables(self) -> List[int]:
-        return [load().ocls_n_subtables(self.h, t) for t in range(1, 9)]
+        return [load().ocls_n_subtables(self.h, t) for t in (1, 2, 3, 4, 5, 6, 7, 8, 12)]
 
     def metric_dumps(self) -> Dict[str, List[str]]:
         """ovs-ofctl dump of the two Metric tables with the packet / byte counters accumulated by

@@ -42,8 +42,13 @@
 
 enum {
   F_DL_TYPE, F_NW_PROTO, F_NW_SRC, F_NW_DST, F_CT_NW_SRC, F_CT_NW_DST, F_IN_PORT, F_REG0, F_REG1, F_REG3, F_REG7,
-  F_TUN_ID, F_TP_SRC, F_TP_DST, F_CT_STATE, F_CONJ_ID, F_LABEL_LO, F_LABEL_HI, NF
+  F_TUN_ID, F_TP_SRC, F_TP_DST, F_CT_STATE, F_CONJ_ID, F_LABEL_LO, F_LABEL_HI, F_CT_MARK, NF
 };
+/* tables: 1..6 rule tables, 7 EgressMetric, 8 IngressMetric, 12 IngressSecurityClassifier */
+#define T_ISC 12
+#define N_TABLES 13
+static const int kTables[] = {1, 2, 3, 4, 5, 6, 7, 8, T_ISC};
+#define N_USED_TABLES (int)(sizeof kTables / sizeof kTables[0])
 
 /* flow action kinds (decoded by oracle/cls_c.py from the flow text) */
 enum { A_CONJ = 1, A_SET_REG = 2, A_CT_COMMIT = 3, A_GOTO = 4, A_GROUP = 5, A_CONTROLLER = 6 };
@@ -132,7 +137,7 @@ typedef struct ocls {
   int n_flows;
   ocls_action* acts;
   uint8_t* min_ncl;          /* per flow: min n_clauses of its conjunction actions (OVS min_n_clauses) */
-  table_t tables[9];
+  table_t tables[N_TABLES];
   uint32_t* tier_conj;       /* sorted conj ids */
   uint8_t* tier_val;
   int n_tier;
@@ -253,7 +258,8 @@ ocls* ocls_create(const ocls_flow* flows, int n_flows, const ocls_action* acts, 
   c->cnt = (uint64_t*)xcalloc(2 * (size_t)n_flows, 8);
   int* idx = (int*)xmalloc(sizeof(int) * (size_t)n_flows);
   int* owner = (int*)xmalloc(sizeof(int) * (size_t)n_flows);
-  for (int t = 1; t <= 8; t++) {
+  for (int ti = 0; ti < N_USED_TABLES; ti++) {
+    const int t = kTables[ti];
     int n = 0;
     for (int i = 0; i < n_flows; i++)
       if (c->flows[i].table == t) idx[n++] = i;
@@ -367,7 +373,8 @@ ocls* ocls_create(const ocls_flow* flows, int n_flows, const ocls_action* acts, 
 
 void ocls_destroy(ocls* c) {
   if (!c) return;
-  for (int t = 1; t <= 8; t++) {
+  for (int ti = 0; ti < N_USED_TABLES; ti++) {
+    const int t = kTables[ti];
     for (int s = 0; s < c->tables[t].n_st; s++) {
       subtable* st = &c->tables[t].st[s];
       free(st->head);
@@ -681,6 +688,29 @@ static void stage(const ocls* c, ws_t* w, int base, uint32_t* pv, uint32_t len, 
   *out_packed = action | (tindex << 8) | ((conj ? tier_of(c, conj) : 0u) << 16) | (flags << 24);
 }
 
+/* IngressSecurityClassifier as installed (pipeline.go:2144-2182): the destination class as its
+ * PktDestinationField mark in reg0[4..7] (fields.go:54-57: tunnel 1, gateway 2, uplink 4) and the
+ * packet's ct_mark; a flow out of the policy tables (IngressMetric / ConntrackCommit) makes the
+ * ingress verdict BYPASS (+TIE on an equal-priority overlap). Returns the packed verdict or 0. */
+static uint32_t ingress_classifier(const ocls* c, ws_t* w, uint32_t* pv, uint32_t dest, uint32_t ct_mark) {
+  static const uint32_t marks[4] = {0, 0x20, 0x10, 0x40}; /* gpc_dest: pod, gateway, tunnel, uplink */
+  if (!c->tables[T_ISC].n_st) return 0;
+  const uint32_t r0 = pv[F_REG0], cm = pv[F_CT_MARK];
+  pv[F_REG0] = dest < 4 ? marks[dest] : 0;
+  pv[F_CT_MARK] = ct_mark;
+  int tie = 0;
+  const int fi = lookup(c, w, T_ISC, pv, 0, &tie);
+  pv[F_REG0] = r0;
+  pv[F_CT_MARK] = cm;
+  if (fi < 0) return 0;
+  const ocls_flow* f = &c->flows[fi];
+  for (int a = 0; a < f->n_act; a++) {
+    const ocls_action* ac = &c->acts[f->act_off + a];
+    if (ac->kind == A_GOTO && (ac->a == 8 || ac->a == 10)) return ACT_BYPASS | ((tie ? 2u : 0u) << 24);
+  }
+  return 0;
+}
+
 static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo, size_t hi, uint32_t* out, uint64_t* cnt) {
   for (size_t i = lo; i < hi; i++) {
     uint32_t pv[NF];
@@ -701,15 +731,15 @@ static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo
     pv[F_TP_DST] = ported ? p->dport[i] : 0;
     pv[F_CT_STATE] = p->ct_state ? p->ct_state[i] : 0x21;
     uint32_t len = p->len ? p->len[i] : 0;
-    uint32_t ec, ep, gc, gp;
+    uint32_t ec, ep, gc, gp, isc;
     stage(c, w, 0, pv, len, cnt, &ec, &ep);
     uint32_t ea = ep & 0xff;
     if (ea == ACT_DROP || ea == ACT_REJECT || ea == ACT_ISO_DROP) {
       gc = 0;
       gp = ACT_NONE;
-    } else if ((p->dest && p->dest[i] != 0) || (p->ct_mark && (p->ct_mark[i] & 0x40))) {
+    } else if ((isc = ingress_classifier(c, w, pv, p->dest ? p->dest[i] : 0, p->ct_mark ? p->ct_mark[i] : 0)) != 0) {
       gc = 0;
-      gp = ACT_BYPASS;
+      gp = isc;
     } else {
       pv[F_REG0] = 0;
       pv[F_REG3] = 0;
@@ -782,4 +812,4 @@ const uint64_t* ocls_counters(const ocls* c) { return c->cnt; }
  * 1 subtables probed, 2 subtables skipped by the prefix tries, 3 soft matches collected, 4 soft-loop
  * levels, 5 conjunction actions hashed. */
 void ocls_stats(const ocls* c, uint64_t* out) { memcpy(out, c->stats, sizeof c->stats); }
-int ocls_n_subtables(const ocls* c, int table) { return (table >= 1 && table <= 8) ? c->tables[table].n_st : 0; }
+int ocls_n_subtables(const ocls* c, int table) { return (table >= 1 && table < N_TABLES) ? c->tables[table].n_st : 0; }

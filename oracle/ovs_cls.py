@@ -322,10 +322,15 @@ class Pipeline:
         if e[0] in (ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP):
             return ev, (ACT_NONE, 0, 0, 0, 0)
         st = {"regs": {}, "ct_label": st["ct_label"], "conj_id": 0}
-        if pkt.get("dest", DEST_POD) != DEST_POD or pkt.get("ct_mark", 0) & HAIRPIN_CT_MARK:
-            # IngressSecurityClassifier (pipeline.go:2144-2182): to gateway / tunnel / uplink ->
-            # IngressMetric; hairpin connections -> ConntrackCommit
-            return ev, (ACT_BYPASS, 0, 0, 0, 0)
+        isc = self.tables.get("IngressSecurityClassifier")
+        if isc:
+            # IngressSecurityClassifier (pipeline.go:2144-2182) as installed: PktDestinationField marks
+            # (fields.go:54-57) -> IngressMetric, HairpinCTMark -> ConntrackCommit; miss -> the policy tables
+            mark = {DEST_GATEWAY: 0x20, DEST_TUNNEL: 0x10, DEST_UPLINK: 0x40}.get(pkt.get("dest", DEST_POD), 0)
+            f, tie = classifier_lookup(isc, pkt, {"regs": {0: mark}, "ct_label": 0, "conj_id": 0}, allow_conj=False)
+            if f is not None and any(a[0] == "goto_table" and a[1] in ("IngressMetric", "ConntrackCommit")
+                                     for a in f["actions"]):
+                return ev, (ACT_BYPASS, 0, 0, 0, FLAG_TIE if tie else 0)
         i = self._stage(INGRESS, pkt, st)
         iv = (i[0], i[1], i[2], self.tiers.get(i[1], 0) if i[1] else 0, i[3])
         return ev, iv

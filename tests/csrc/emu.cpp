@@ -63,7 +63,7 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
     g_lines.clear();
     g_line_site.clear();
     const unsigned long long v0 = ::gpc_emu_stats[3], s0 = ::gpc_emu_stats[4];
-    PacketOut o = classify_packet(im, p, dest);
+    PacketOut o = classify_packet(im, p, dest, pk->ct_mark ? pk->ct_mark[i] : 0u);
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     std::sort(g_lines.begin(), g_lines.end());
@@ -111,7 +111,7 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pk
     make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
              pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst,
              pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
-    PacketOut o = classify_packet<false, 0>(im, p, dest);
+    PacketOut o = classify_packet<false, 0>(im, p, dest, pk->ct_mark ? pk->ct_mark[i] : 0u);
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;

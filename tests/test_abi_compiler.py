@@ -28,7 +28,7 @@ def test_exports_every_header_symbol():
     exported = set(re.findall(r"\bT (gpc_\w+)", syms))
     assert declared <= exported, declared - exported
     lib = gpc.load()
-    assert lib.gpc_abi_version() == 2  # 2: IPv6 columns in gpc_pkt_soa, gpc_classify6
+    assert lib.gpc_abi_version() == 3  # 3: ct_mark column, DNS conjunction trio, flow keys (2: IPv6 columns)
 
 
 @pytest.mark.parametrize("case", GOLD["cases"], ids=[c["name"] for c in GOLD["cases"]])
