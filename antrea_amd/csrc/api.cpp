@@ -132,6 +132,7 @@ struct gpc_ctx {
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
   uint64_t epoch = 0, n_full = 0, n_delta = 0, n_bg = 0;
+  std::map<hipStream_t, uint64_t> launch_epoch;  // epoch of the last classify launch per stream (data)
   uint64_t commit_no = 0;                // commits so far (COMMIT markers in the log)
   bool comp_pending = false;             // a background compaction was requested, not installed yet
   std::vector<std::pair<uint64_t, FeatureNP::Dirty>> dirty_hist;  // per commit since the request
@@ -721,6 +722,7 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   hipStream_t st = (hipStream_t)stream;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count, st);
   if (rc || n == 0) return rc;
+  ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained
   if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(ev, st));
@@ -743,6 +745,7 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   hipStream_t st = (hipStream_t)stream;
   int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, st);
   if (rc || n == 0) return rc;
+  ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];
   if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(ev, st));
@@ -938,6 +941,15 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
   std::lock_guard<std::mutex> g(ctx->ctl);
   if (blob) *blob = ctx->svc_blob.empty() ? nullptr : ctx->svc_blob.data();
   if (n_words) *n_words = ctx->svc_blob.size();
+  return GPC_OK;
+}
+
+int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch) {
+  if (!ctx || !epoch) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> d(ctx->data);
+  auto it = ctx->launch_epoch.find((hipStream_t)stream);
+  if (it == ctx->launch_epoch.end()) return -GPC_ENOTFOUND;
+  *epoch = it->second;
   return GPC_OK;
 }
 

@@ -33,6 +33,7 @@ VERDICT_DTYPE = np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"),
 LB_DTYPE = np.dtype([("endpoint_ip", "<u4"), ("endpoint_port", "<u2"), ("flags", "u1"), ("reserved", "u1"),
                      ("group_id", "<u4"), ("out_port", "<u4")])
 LB_HIT, LB_NO_ENDPOINT, LB_DNAT, LB_REMOTE = 1, 2, 4, 8
+VFLAG_PASS, VFLAG_TIE, VFLAG_PACKETIN = 1, 2, 4  # gpc_verdict.flags
 VTABLE_ENDPOINT_DNAT = 4
 
 
@@ -112,7 +113,7 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
            "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
-           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys"]
+           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch"]
 
 _lib = None
 
@@ -169,6 +170,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_del_dns_conj_addrs.argtypes = [vp, C.c_uint32, C.POINTER(gpc_addr), sz]
     lib.gpc_network_policy_flow_keys.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_uint8, C.c_char_p, sz, C.POINTER(sz),
                                                  C.POINTER(sz)]
+    lib.gpc_stream_epoch.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -543,6 +545,12 @@ class Classifier:
     def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, lb_ptr: int = 0):
         _check(self.lib.gpc_classify_lb(self.h, C.byref(soa), n, out_ptr, lb_ptr or None, int(count), stream or None),
                "gpc_classify")
+
+    def stream_epoch(self, stream: int = 0) -> int:
+        """Epoch the last classify launch on `stream` was bound to (gpc_stream_epoch)."""
+        e = C.c_uint64()
+        _check(self.lib.gpc_stream_epoch(self.h, stream or None, C.byref(e)), "gpc_stream_epoch")
+        return e.value
 
     def counters(self):
         p = C.POINTER(C.c_uint64)()

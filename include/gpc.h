@@ -416,6 +416,9 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
 /* Host mirror of the journal pool and the current epoch's journal header offset (NULL / 0 when
  * the epoch is the base image alone). */
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
+/* The epoch (gpc_image_stats.epoch) the last gpc_classify* launch on `stream` was bound to: with
+ * classification concurrent to commits, every launch sees exactly this one committed epoch. */
+int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch);
 const char* gpc_strerror(int err);
 int gpc_abi_version(void);
 

@@ -94,3 +94,31 @@ def site_lines(reset=False):
         for i in range(2048):
             arr[i] = 0
     return v
+
+
+def snapshot(clf: "gpc.Classifier"):
+    """Owned copies of the committed epoch's host state (base image, header, journal pool and
+    header offset, Service image): classify_snapshot emulates exactly that epoch later, whatever
+    has been committed since. Call it from the thread that commits, right after gpc_commit."""
+    blob, nw, hdr, hb = clf.debug_image()
+    pool, pw, jhdr = clf.debug_epoch()
+    svc = clf.debug_service_image()
+    copy = lambda ptr, n, dt: np.ctypeslib.as_array(C.cast(ptr, C.POINTER(dt)), shape=(n,)).copy() if ptr and n else None
+    snap = {"blob": copy(blob, nw, C.c_uint32), "hdr": copy(hdr, hb, C.c_uint8),
+            "pool": copy(pool, pw, C.c_uint32), "jhdr": jhdr, "svc": None}
+    assert not svc, "epochs with a Service image are not snapshotted"
+    return snap
+
+
+def classify_snapshot(snap, cols, counters=None):
+    """Emulated verdicts (n, 2) of a snapshot() epoch."""
+    soa, keep, n = gpc.pkt_soa_host(cols)
+    out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
+    cptr = None
+    if counters is not None:
+        assert counters.dtype == np.uint64 and counters.flags.c_contiguous
+        cptr = counters.ctypes.data
+    pool = snap["pool"].ctypes.data if snap["pool"] is not None else None
+    load().emu_classify(snap["blob"].ctypes.data, snap["hdr"].ctypes.data, pool, snap["jhdr"], None, C.byref(soa), n,
+                        out.ctypes.data, None, cptr)
+    return out.reshape(n, 2)
