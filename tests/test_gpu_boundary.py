@@ -100,14 +100,17 @@ def test_gpu_lane_sort_delta_epochs(monkeypatch):
     c.batch_install_policy_rule_flows(copy.deepcopy(rules))
     c.commit()
     rng = np.random.default_rng(41)
+    live = list(rules)
     for step in range(10):
-        r = rules[int(rng.integers(len(rules)))]
+        r = live.pop(int(rng.integers(len(live))))
         side = "src" if r.get("from") else "dst"
         addrs = ["%d.%d.%d.%d" % tuple(int(x) for x in rng.integers(0, 256, 4)) for _ in range(6)]
         addrs += [emu_ip(int(cols[side][i])) for i in rng.choice(n, 6, replace=False)]
         c.add_policy_rule_address(r["flow_id"], side, addrs, r.get("priority"))
         if step % 3 == 2:
             c.uninstall_policy_rule_flows(r["flow_id"])
+        else:
+            live.append(r)
         c.commit()
     st = c.image_stats()
     assert st["n_delta_builds"] >= 8 and st["n_overlay_rules"] > 0
