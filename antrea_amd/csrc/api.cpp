@@ -306,7 +306,7 @@ static void compactor_main(gpc_ctx* ctx) {
     int rc = GPC_OK;
     try {
       (void)shadow.take_dirty();
-      rc = build_image(shadow, ctx->slots, base.get());
+      rc = build_image(shadow, ctx->slots, base.get(), /*alloc=*/false);
       jn->reset(base.get());
       for (int round = 0; rc == GPC_OK && round < 4; round++) {
         size_t n = 0;
@@ -324,7 +324,7 @@ static void compactor_main(gpc_ctx* ctx) {
           break;
         }
         std::string err;
-        if ((!d.conj.empty() || d.hard_tables) && jn->apply(shadow, ctx->slots, d.conj, d.hard_tables, &err) != GPC_OK)
+        if ((!d.conj.empty() || d.hard_tables) && jn->apply(shadow, ctx->slots, d.conj, d.hard_tables, &err, false) != GPC_OK)
           rc = -GPC_EINVAL;
         if (n < 256) break;
       }
@@ -972,6 +972,13 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   FeatureNP::Dirty dirty = ctx->np.take_dirty();
+  // counter slots of the rules with Metric flows, allocated here in conj-id order before the commit
+  // is logged: the compactor (which replays up to a commit marker) then only looks them up
+  for (uint32_t conj : dirty.conj) {
+    auto it = ctx->np.policies().find(conj);
+    uint32_t slot;
+    if (it != ctx->np.policies().end() && !it->second->metric_flows.empty()) (void)ctx->slots.lookup(conj, true, &slot);
+  }
   const uint64_t commit_no = ++ctx->commit_no;
   {
     Op m;
@@ -1148,14 +1155,6 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       RetiredEpoch{std::move(ne)}.release(us);
       return -GPC_EDEV;
     }
-    if (ctx->d_counters) {  // carry the totals over in copy 0
-      if ((rc = fold_counters(ctx))) {
-        RetiredEpoch{std::move(ne)}.release(us);
-        (void)hipFree(nc);
-        return rc;
-      }
-      (void)hipMemcpy(nc, ctx->d_counters, ctx->counter_cap * kCounterBytes, hipMemcpyDeviceToDevice);
-    }
   }
   if (hip_ok(hipStreamSynchronize(us))) {  // the new epoch is resident before it is published
     RetiredEpoch{std::move(ne)}.release(us);
@@ -1163,6 +1162,8 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   }
   DevEpoch old;
   unsigned long long* old_counters = nullptr;
+  const size_t old_cap = ctx->counter_cap;
+  const uint32_t old_copies = ctx->counter_copies;
   {
     std::lock_guard<std::mutex> d(ctx->data);
     old = std::move(ctx->cur);
@@ -1177,6 +1178,12 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   // the previous epoch is freed once every stream that launched on it has passed that launch
   ctx->retired.push_back(RetiredEpoch{std::move(old)});
   if (old_counters) {
+    // Every launch that could still add to the old array was queued before the swap: once the
+    // device has drained them, all its replicas are merged into the new copy 0 (atomically: new
+    // launches may already be adding to it), so no count is lost however the growth interleaves.
+    (void)hipDeviceSynchronize();
+    (void)launch_merge_counters(ctx->d_counters, old_counters, uint64_t(old_cap) * kCounterWords, old_copies,
+                                uint64_t(old_cap) * kCounterWords, nullptr);
     (void)hipDeviceSynchronize();
     (void)hipFree(old_counters);
   }

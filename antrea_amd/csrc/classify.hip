@@ -66,7 +66,7 @@ __device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_
 // the packet index this lane now owns (>= n: none).
 template <int kStage>
 __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n,
-                                                 const uint4* __restrict__ out, uint64_t i) {
+                                                 const uint4* __restrict__ out, uint64_t i, uint32_t* pkt_lds) {
   constexpr uint32_t kBins = 64;  // one wavefront scans the histogram
   __shared__ uint32_t hist[kBins];
   __shared__ uint16_t perm[kSortBlock];
@@ -81,7 +81,7 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
     }
     if (live) {
       const uint32_t src = pk.src[i], dst = pk.dst[i];
-      Pkt p;
+      Pkt p(pkt_lds + tid, kSortBlock);
       make_axes(p, src, dst, pk.sport[i], pk.dport[i], pk.proto[i], pk.out_port[i], pk.in_port ? pk.in_port[i] : 0u,
                 pk.svc_group ? pk.svc_group[i] : 0u, pk.tun_id ? pk.tun_id[i] : 0u, pk.ct_src ? pk.ct_src[i] : src,
                 pk.ct_dst ? pk.ct_dst[i] : dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
@@ -115,8 +115,10 @@ template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = fal
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count) {
+  // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
+  __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
   uint64_t i = uint64_t(blockIdx.x) * block_threads<kSort>() + threadIdx.x;
-  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, i);  // its own instantiation: the plain kernel has no barrier
+  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, i, pkt_lds);  // its own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
   uint4 prev = make_uint4(0u, 0u, 0u, 0u);
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
       return;
     }
   }
-  Pkt p;
+  Pkt p(pkt_lds + threadIdx.x, block_threads<kSort>());
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
            pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
   View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
@@ -236,11 +238,32 @@ int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
+__global__ void merge_counters_kernel(unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ src,
+                                      uint64_t src_stride, uint32_t copies, uint64_t n_words) {
+  const uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (w >= n_words) return;
+  unsigned long long sum = 0;
+  for (uint32_t r = 0; r < copies; r++) sum += src[r * src_stride + w];
+  if (sum) atomicAdd(&dst[w], sum);
+}
+
+int launch_merge_counters(unsigned long long* dst, const unsigned long long* src, uint64_t src_stride, uint32_t copies,
+                          uint64_t n_words, hipStream_t stream) {
+  if (!dst || !src || !copies || !n_words) return 0;
+  hipLaunchKernelGGL(merge_counters_kernel, dim3(uint32_t((n_words + 255) / 256)), dim3(256), 0, stream, dst, src, src_stride,
+                     copies, n_words);
+  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
+}
+
+// Launch size: the grid is limited in work-items (gridDim.x * blockDim.x < 2^32 on ROCm), and the
+// lane-regrouping kernels use 256-thread blocks.
+constexpr uint64_t kMaxPackets = (1ull << 32) - uint64_t(kSortBlock);
+
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
                      unsigned long long* counters, int count, hipStream_t stream) {
   if (n == 0) return 0;
+  if (n > kMaxPackets) return -GPC_EINVAL;
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
-  if (blocks > 0xffffffffull) return -GPC_EINVAL;
   hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
                      reinterpret_cast<uint4*>(out), nullptr, counters, count);
   hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
@@ -251,7 +274,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, hipStream_t stream) {
   if (n == 0) return 0;
-  if ((n + kBlock - 1) / kBlock > 0xffffffffull) return -GPC_EINVAL;
+  if (n > kMaxPackets) return -GPC_EINVAL;
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
   if (delta && svc) launch<true, true>(ep, pk, n, out, lb_out, counters, count, stream);
   else if (delta) launch<true, false>(ep, pk, n, out, lb_out, counters, count, stream);

@@ -135,10 +135,21 @@ GPC_HD uint32_t ingress_bypass(uint32_t isc, uint32_t dest, uint32_t ct_mark) {
   return (d || h) ? (uint32_t(RV_BYPASS) | ((d && h) ? (1u << 8) : 0u)) : 0u;
 }
 
+// Per-packet values the evaluation indexes at run time (axis numbers come from the image): the 11
+// axes and the Bloom filter bits of axes 0..7. They live in caller-provided storage, strided: the
+// kernel gives each lane a column of a block-wide LDS table laid out [word][lane] (conflict-free,
+// explicitly sized, no scratch), the host emulation a plain array (stride 1).
+constexpr uint32_t kPktWords = AX_N + 8;
+struct PktRef {
+  uint32_t* v;
+  uint32_t s;
+  GPC_HD uint32_t& operator[](uint32_t i) const { return v[size_t(i) * s]; }
+};
 struct Pkt {
-  uint32_t ax[AX_N];
-  uint32_t fm[8];  // filter bits of axes 0..7 (bits 0-19)
-  uint32_t l4m;    // filter bit of (proto class, tp_dst block) (bits 20-31)
+  PktRef ax;     // ax[a]: axis a
+  PktRef fm;     // fm[a]: filter bits of axis a < 8 (bits 0-19)
+  uint32_t l4m;  // filter bit of (proto class, tp_dst block) (bits 20-31)
+  GPC_HD Pkt(uint32_t* store, uint32_t stride) : ax{store, stride}, fm{store + AX_N * stride, stride}, l4m(0) {}
 };
 
 // Partial decision of one image for one table, packed (it is live across the table loop):

@@ -38,6 +38,18 @@ uint32_t SlotMap::get(uint32_t conj) {
   return s;
 }
 
+bool SlotMap::lookup(uint32_t conj, bool alloc, uint32_t* slot) {
+  if (alloc) {
+    *slot = get(conj);
+    return true;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = slot_.find(conj);
+  if (it == slot_.end()) return false;
+  *slot = it->second;
+  return true;
+}
+
 void SlotMap::release(uint32_t conj, std::vector<uint32_t>* freed) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = slot_.find(conj);
@@ -955,11 +967,11 @@ int Gather::add_isc(const Flow& f) {
   return GPC_OK;
 }
 
-int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out);
+int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc);
 
 }  // namespace
 
-int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
+int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc) {
   *out = HostImage();
   Gather G;
   for (auto& kv : np.installed()) {
@@ -969,12 +981,12 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       return rc;
     }
   }
-  return emit(G, np, slots, out);
+  return emit(G, np, slots, out, alloc);
 }
 
 // IPv6 image: the same build over the IPv6 half of the flows (addresses interned as codes), plus
 // the LPM table the kernel maps packet addresses through (appended to the blob, hdr.v6_lpm).
-int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out) {
+int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc) {
   *out = HostImage();
   V6Codes codes;
   int rc = codes.build(np, &out->error);
@@ -988,7 +1000,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out) {
       return rc;
     }
   }
-  if ((rc = emit(G, np, slots, out))) return rc;
+  if ((rc = emit(G, np, slots, out, alloc))) return rc;
   // LPM by binary search on prefix lengths (Waldvogel et al.): the table holds every tree node
   // (root excluded: a miss everywhere means code 0) plus, for each node, a marker at every shorter
   // length its binary search passes through, carrying the best matching prefix's code there.
@@ -1180,7 +1192,7 @@ uint32_t Journal::append(const uint32_t* w, size_t n, size_t align) {
 }
 
 int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables,
-                   std::string* err) {
+                   std::string* err, bool alloc) {
   // 1. tombstones: every earlier copy of a changed rule (base or journal)
   for (uint32_t c : conj) {
     auto it = live_.find(c);
@@ -1273,9 +1285,11 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       for (auto& pt : patches) rec[pt.first] = base_off + ext_at + pt.second;
       rec[0] = r.hard ? 0u : r.conj_id;
       rec[1] = uint32_t(r.prio) | (uint32_t(r.act_prio) << 16);
-      rec[2] = (r.verdict & 7u) | ((r.hard ? 1u : 0u) << 3) | ((r.has_act ? 1u : 0u) << 4) | ((r.counted ? 1u : 0u) << 5) |
+      uint32_t slot = 0;
+      const bool counted = !r.hard && r.counted && slots.lookup(r.conj_id, alloc, &slot);
+      rec[2] = (r.verdict & 7u) | ((r.hard ? 1u : 0u) << 3) | ((r.has_act ? 1u : 0u) << 4) | ((counted ? 1u : 0u) << 5) |
                (uint32_t(r.n & 3) << 6) | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
-      rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0u;
+      rec[3] = slot;
       rec[4] = uint32_t(r.tier) | (orid << 8);
       rec[5] = (!r.hard && r.pin) ? kRecPacketIn : 0u;
       const uint32_t off = append(rec.data(), rec.size(), 16);
@@ -1355,7 +1369,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
 
 namespace {
 
-int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
+int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc) {
   PhaseTimer T_;
   auto& soft = G.soft;
   auto& hard = G.hard;
@@ -1451,10 +1465,12 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out) {
       }
       rec[0] = r.hard ? 0 : r.conj_id;
       rec[1] = uint32_t(r.prio) | (uint32_t(r.act_prio) << 16);
-      uint32_t flags = (r.verdict & 7u) | ((r.hard ? 1u : 0u) << 3) | ((r.has_act ? 1u : 0u) << 4) | ((r.counted ? 1u : 0u) << 5) |
+      uint32_t slot = 0;
+      const bool counted = !r.hard && r.counted && slots.lookup(r.conj_id, alloc, &slot);
+      uint32_t flags = (r.verdict & 7u) | ((r.hard ? 1u : 0u) << 3) | ((r.has_act ? 1u : 0u) << 4) | ((counted ? 1u : 0u) << 5) |
                        (uint32_t(r.n & 3) << 6);
       rec[2] = flags | (offs[0] << 8) | (offs[1] << 16) | (offs[2] << 24);
-      rec[3] = (!r.hard && r.counted) ? slots.get(r.conj_id) : 0;
+      rec[3] = slot;
       rec[4] = uint32_t(r.tier) | (rid << 8);
       rec[5] = r.hard ? 0u : (skip_mask(r, 0, span) | (skip_mask(r, 1, span) << 3) | (r.pin ? kRecPacketIn : 0u));
       if (base >= (1u << 28)) {  // Ent.x holds record offset / 16 in 24 bits

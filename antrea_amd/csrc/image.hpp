@@ -30,10 +30,15 @@ struct HostImage {
 
 // Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
 // rank that applies the same control-plane calls, so slots line up for the RCCL all-reduce).
-// Thread-safe: the background compactor assigns slots too.
+// Slots are allocated only by the control thread (gpc_commit, in conj-id order, before the commit
+// is logged for the compactor); the background compactor only looks them up (lookup with
+// alloc = false), so numbering never depends on thread timing and a conjunction uninstalled while
+// the compactor worked is built uncounted instead of re-acquiring a slot nothing would release.
 class SlotMap {
  public:
   uint32_t get(uint32_t conj);
+  // The slot of conj; a new one when absent and alloc, else false.
+  bool lookup(uint32_t conj, bool alloc, uint32_t* slot);
   void release(uint32_t conj, std::vector<uint32_t>* freed);
   uint32_t size() const {
     std::lock_guard<std::mutex> g(mu_);
@@ -51,9 +56,10 @@ class SlotMap {
   std::vector<uint32_t> free_;
 };
 
-int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out);
+// alloc = false (background compactor): counter slots are looked up, never allocated.
+int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true);
 // The IPv6 image (core.hpp "IPv6 interning"): full build, no journal.
-int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out);
+int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true);
 // Append-only delta store over one base image (core.hpp "journal"). apply() appends the current
 // versions of the changed rules (records, driver-bucket entries, copied-on-write head pages) and a
 // new epoch header with the cumulative tombstones; nothing published earlier is rewritten, so the
@@ -62,7 +68,8 @@ class Journal {
  public:
   void reset(const HostImage* base, uint32_t lg = 16);
   void set_base(const HostImage* base) { base_ = base; }  // the base image object moved
-  int apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, std::string* err);
+  int apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, std::string* err,
+            bool alloc = true);
   bool active() const { return hdr_off != 0; }
   uint32_t n_tombstones() const;
   std::vector<uint32_t> pool;  // host mirror of the device pool

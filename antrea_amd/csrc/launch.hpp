@@ -21,6 +21,10 @@ struct EpochArgs {
 };
 // Sums counter copies 1..copies-1 into copy 0 and zeroes them (stride words per copy).
 int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t copies, hipStream_t stream);
+// dst[w] += sum over r < copies of src[r * src_stride + w], w < n_words (device-scope atomics: launches
+// on other streams may be adding to dst concurrently). Used when the counter array grows.
+int launch_merge_counters(unsigned long long* dst, const unsigned long long* src, uint64_t src_stride, uint32_t copies,
+                          uint64_t n_words, hipStream_t stream);
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, hipStream_t stream);
 // IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).

@@ -192,8 +192,12 @@ def _roofline(pmc, kern_ms, n, b_in, b_out, lbar):
                          "gbs_if_uncached": round(pps_kernel * b_alg / 1e9, 1),
                          "compulsory_bytes_per_packet": b_in + b_out,
                          "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
-    rl["pmc_by_kernel"] = {k: {c: round(v, 1) for c, v in cs.items()} for p in pmc.get("_passes", [])
-                           for k, cs in (p or {}).get("by_kernel", {}).items()} or None
+    by_kernel = {}
+    for p in pmc.get("_passes", []):
+        for k, cs in (p or {}).get("by_kernel", {}).items():
+            short = k.split("(")[0].replace("void gpc::", "")
+            by_kernel.setdefault(short, {}).update({c: round(v, 1) for c, v in cs.items()})
+    rl["pmc_by_kernel"] = by_kernel or None
     return rl
 
 

@@ -57,7 +57,8 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
       w[2] = w[3] = 0;
       continue;
     }
-    Pkt p;
+    uint32_t pst[kPktWords];
+    Pkt p(pst, 1);
     make_pkt(p, src, dst, sport, dport, proto, out_port, pk->in_port ? pk->in_port[i] : 0u, svc_group,
              pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
     g_lines.clear();
@@ -107,7 +108,8 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pk
     const uint32_t src = sd[0], dst = sd[1];
     const uint32_t ct_src = pk->ct_src6 ? code(pk->ct_src6, i) : src, ct_dst = pk->ct_dst6 ? code(pk->ct_dst6, i) : dst;
     const uint32_t dest = pk->dest ? pk->dest[i] : 0u;
-    Pkt p;
+    uint32_t pst[kPktWords];
+    Pkt p(pst, 1);
     make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
              pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst,
              pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));

@@ -177,3 +177,42 @@ def test_background_compaction(delay_ms, monkeypatch):
     st = a.image_stats()
     assert st["n_background_builds"] >= 1, st
     assert st["n_full_builds"] == 1, st  # only the initial build ran in the foreground
+
+
+def test_compaction_uninstall_releases_slot(monkeypatch):
+    """a rule uninstalled while the background compactor builds from an older state must
+    not get a counter slot back from the compactor. Slots are allocated only by the control thread
+    (gpc_commit), so after the background result is installed the uninstalled conj id is in neither
+    slot_conj nor the metrics, and slot numbering equals a context that never compacts (the
+    'identical on every rank' promise the RCCL all-reduce relies on)."""
+    import time
+    monkeypatch.setenv("GPC_TEST_COMPACT_DELAY_MS", "400")
+    wl = workload.config3(seed=26, n_policies_per_dir=8, rules_per_policy=20)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=26)
+    rng = np.random.default_rng(26)
+    a, b = gpc.Classifier(compact_after=4), gpc.Classifier(compact_after=-1)
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    by_id = {r["flow_id"]: r for r in rules if r.get("from") and r.get("action", "Allow") != "Pass"}
+    ids = sorted(by_id)
+    for step in range(8):  # past compact_after live journal rules: the compactor starts (and sleeps)
+        rid = int(ids[step])
+        addrs = [_ip(int(cols["src"][i])) for i in rng.choice(N_PKTS, size=2, replace=False)]
+        for c in (a, b):
+            c.add_policy_rule_address(rid, "src", addrs, by_id[rid].get("priority"))
+        _compare(a, b, cols, "add %d" % step)
+    victim = int(ids[0])  # in the compactor's snapshot, uninstalled before its result is installed
+    for c in (a, b):
+        c.uninstall_policy_rule_flows(victim)
+    _compare(a, b, cols, "uninstall")
+    time.sleep(0.8)
+    _compare(a, b, cols, "install background result")
+    st = a.image_stats()
+    assert st["n_background_builds"] >= 1, st
+    _, slots_a = a.counters()
+    _, slots_b = b.counters()
+    assert victim not in slots_a and victim not in a.network_policy_metrics()
+    assert slots_a == slots_b

@@ -1,14 +1,26 @@
 #!/bin/bash
-# Per-kernel VGPRs / spills / occupancy of classify.hip (compile-time resource report, CPU only).
+# Per-kernel resources of classify.hip (compile-time report, CPU only): VGPRs, spills, scratch
+# bytes per lane, LDS bytes, occupancy. Extra hipcc flags (e.g. -DGPC_WAVES_PER_EU=5) pass through.
 cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I/root/repo/include -I/root/repo/antrea_amd/csrc \
   "$@" -c /root/repo/antrea_amd/csrc/classify.hip -o /tmp/kres.o -Rpass-analysis=kernel-resource-usage 2>&1 |
   python3 -c '
-import re,sys
-cur=None
+import re, sys
+rows, cur = [], None
 for l in sys.stdin:
-    m=re.search(r"Function Name: (\S+)",l)
-    if m: cur=m.group(1); print(); print(re.sub(r"EEEvNS.*","",cur.replace("_ZN3gpc15classify_kernelI","")),end=" ")
-    for k in ("VGPRs","VGPRs Spill","SGPRs Spill","Occupancy \\[waves/SIMD\\]"):
-        m=re.search(r"\s"+k+r": (\d+)",l)
-        if m: print(k.split()[0]+("S" if "Spill" in k else "")+"="+m.group(1),end=" ")
-print()'
+    m = re.search(r"Function Name: (\S+)", l)
+    if m:
+        name = m.group(1)
+        t = re.search(r"classify_kernelIL(b\d)EL(b\d)ELi(\d)EL(b\d)EL(b\d)E", name)
+        cur = {"kernel": "classify<delta=%s,svc=%s,stage=%s,v6=%s,sort=%s>" % (t.group(1)[1], t.group(2)[1], t.group(3),
+               t.group(4)[1], t.group(5)[1]) if t else re.sub(r"^_ZN3gpc\d+", "", name)[:40]}
+        rows.append(cur)
+        continue
+    for key, pat in (("vgpr", r"\sVGPRs: (\d+)"), ("vgpr_spill", r"VGPRs Spill: (\d+)"), ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
+                     ("lds", r"LDS Size \[bytes/block\]: (\d+)"), ("occ", r"Occupancy \[waves/SIMD\]: (\d+)")):
+        m = re.search(pat, l)
+        if m and cur is not None:
+            cur[key] = int(m.group(1))
+print("%-48s %5s %6s %8s %6s %4s" % ("kernel", "VGPR", "spill", "scratch", "LDS", "occ"))
+for r in rows:
+    print("%-48s %5s %6s %8s %6s %4s" % (r["kernel"], r.get("vgpr"), r.get("vgpr_spill"), r.get("scratch"), r.get("lds"), r.get("occ")))
+'
