@@ -101,6 +101,7 @@ struct Compactor {
   bool enabled = true, stop = false, busy = false;
   uint64_t want_commit = 0;  // compact once the shadow reaches this commit (0: not requested)
   bool ready = false;        // a result is waiting to be installed
+  bool discard = false;      // gpc_replay ran while the result was being built: its device buffers are stale
   int rc = 0;
   std::unique_ptr<HostImage> base;
   std::unique_ptr<Journal> journal;
@@ -702,6 +703,80 @@ int gpc_dump_flows(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed) {
 }
 
 int gpc_commit(gpc_ctx* ctx) { return commit_impl(ctx, false); }
+
+// ReplayFlows (client.go:1130-1152; NP part network_policy.go:1626-1657) for the device: after a
+// device reset (or to move a context's data path to a freshly initialised device) every device
+// buffer is rebuilt from the host shadow state -- base image, journal pool, IPv6 and Service
+// images -- without compiler work; the realized flows, conj ids and counter slots are unchanged.
+// Device counters restart from zero, as OVS flow counters do after the flows are replayed.
+int gpc_replay(gpc_ctx* ctx) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  (void)hipDeviceSynchronize();  // may fail after a reset: the old buffers are dropped regardless
+  (void)hipGetLastError();
+  {  // a background compaction result built on the old device state is dropped
+    std::lock_guard<std::mutex> c(ctx->comp.mu);
+    if (ctx->comp.busy) ctx->comp.discard = true;
+    ctx->comp.dbase.reset();
+    ctx->comp.dpool.reset();
+    if (ctx->comp.ready) ctx->comp.discard = true;
+  }
+  DevEpoch old;
+  unsigned long long* old_counters = nullptr;
+  {
+    std::lock_guard<std::mutex> d(ctx->data);
+    old = std::move(ctx->cur);
+    ctx->cur = DevEpoch();
+    old_counters = ctx->d_counters;
+    ctx->d_counters = nullptr;
+    ctx->launch_epoch.clear();
+  }
+  ctx->retired.push_back(RetiredEpoch{std::move(old)});
+  collect_retired(ctx, true);
+  if (old_counters) (void)hipFree(old_counters);
+  (void)hipGetLastError();
+  if (ctx->last.blob.empty()) return GPC_OK;  // nothing committed yet
+  if (!ctx->ustream && hip_ok(hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking))) return -GPC_EDEV;
+  hipStream_t us = ctx->ustream;
+  DevEpoch ne;
+  int rc = upload_image(ctx->last, us, &ne.base);
+  Journal& jn = ctx->journal;
+  if (!rc && jn.active()) {
+    auto pool = std::make_shared<DevImage>();
+    pool->s = us;
+    pool->bytes = kPoolWords * 4;
+    if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, us)) ||
+        hip_ok(hipMemcpyAsync(pool->d_blob, jn.pool.data(), jn.pool.size() * 4, hipMemcpyHostToDevice, us)))
+      rc = -GPC_EDEV;
+    ne.pool = std::move(pool);
+    jn.uploaded = jn.pool.size();
+    ne.jhdr = jn.hdr_off;
+  }
+  if (!rc && !ctx->last6.blob.empty()) {
+    rc = upload_image(ctx->last6, us, &ne.v6);
+    ne.v6_lpm = ctx->last6.hdr.v6_lpm;
+  }
+  if (!rc && !ctx->svc_blob.empty()) rc = upload_words(ctx->svc_blob, us, &ne.svc);
+  const size_t cap = std::max<size_t>(1, ctx->slots.size());
+  const uint32_t copies = counter_copies_for(cap);
+  unsigned long long* nc = nullptr;
+  if (!rc && (hip_ok(hipMalloc(&nc, cap * kCounterBytes * copies)) || hip_ok(hipMemset(nc, 0, cap * kCounterBytes * copies))))
+    rc = -GPC_EDEV;
+  if (!rc) rc = hip_ok(hipStreamSynchronize(us));
+  if (rc) {
+    RetiredEpoch{std::move(ne)}.release(us);
+    if (nc) (void)hipFree(nc);
+    return rc;
+  }
+  ne.epoch = ++ctx->epoch;
+  std::lock_guard<std::mutex> d(ctx->data);
+  ctx->cur = std::move(ne);
+  ctx->d_counters = nc;
+  ctx->counter_cap = cap;
+  ctx->counter_copies = copies;
+  return GPC_OK;
+}
 int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
 
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
@@ -726,6 +801,64 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained
   if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(ev, st));
+}
+
+int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pk, gpc_verdict* out, gpc_lb_result* lb_out, gpc_trace_step* steps,
+              size_t cap, size_t* n_steps) {
+  static_assert(sizeof(gpc_trace_step) == sizeof(TraceStep), "gpc_trace_step mirrors core.hpp TraceStep");
+  if (!ctx || !pk || !out || !pk->src || !pk->dst || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)
+    return -GPC_EINVAL;
+  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  // one packet: every present column's element 0 goes into one small device buffer
+  struct Col {
+    const void* h;
+    size_t elem;
+    const void** d;
+  };
+  gpc_pkt_soa d{};
+  Col cols[] = {{pk->src, 4, (const void**)&d.src},           {pk->dst, 4, (const void**)&d.dst},
+                {pk->sport, 2, (const void**)&d.sport},       {pk->dport, 2, (const void**)&d.dport},
+                {pk->proto, 1, (const void**)&d.proto},       {pk->out_port, 4, (const void**)&d.out_port},
+                {pk->in_port, 4, (const void**)&d.in_port},   {pk->svc_group, 4, (const void**)&d.svc_group},
+                {pk->tun_id, 4, (const void**)&d.tun_id},     {pk->ct_src, 4, (const void**)&d.ct_src},
+                {pk->ct_dst, 4, (const void**)&d.ct_dst},     {pk->ct_state, 1, (const void**)&d.ct_state},
+                {pk->dest, 1, (const void**)&d.dest},         {pk->len, 2, (const void**)&d.len},
+                {pk->ct_mark, 1, (const void**)&d.ct_mark}};
+  constexpr size_t kSlot = 16, kOut = 512;  // column slots, then verdicts / LB result / steps / count
+  const size_t ncol = sizeof cols / sizeof cols[0];
+  std::vector<uint8_t> h(kOut + ncol * kSlot, 0);
+  for (size_t c = 0; c < ncol; c++)
+    if (cols[c].h) std::memcpy(h.data() + kOut + c * kSlot, cols[c].h, cols[c].elem);
+  uint8_t* buf = nullptr;
+  if (hip_ok(hipMalloc(&buf, h.size()))) return -GPC_EDEV;
+  for (size_t c = 0; c < ncol; c++)
+    if (cols[c].h) *cols[c].d = buf + kOut + c * kSlot;
+  int rc = hip_ok(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+  uint4* dout = reinterpret_cast<uint4*>(buf);
+  uint4* dlb = reinterpret_cast<uint4*>(buf + 16);
+  TraceStep* dsteps = reinterpret_cast<TraceStep*>(buf + 64);
+  uint32_t* dn = reinterpret_cast<uint32_t*>(buf + 64 + kMaxTraceSteps * sizeof(TraceStep));
+  if (!rc) {
+    std::lock_guard<std::mutex> g(ctx->data);
+    if (!ctx->cur.base) {
+      rc = -GPC_EINVAL;  // nothing committed yet
+    } else {
+      EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.jhdr ? ctx->cur.pool->d_blob : nullptr,
+                   ctx->cur.jhdr, ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr, 0u, {0, 0}, 0u, 0u};
+      rc = launch_trace(ep, d, dout, dlb, dsteps, dn, nullptr);
+      if (!rc) rc = hip_ok(hipDeviceSynchronize());  // the epoch stays alive while it is current
+    }
+  }
+  if (!rc) rc = hip_ok(hipMemcpy(h.data(), buf, kOut, hipMemcpyDeviceToHost));
+  (void)hipFree(buf);
+  if (rc) return rc;
+  std::memcpy(out, h.data(), 2 * sizeof(gpc_verdict));
+  if (lb_out) std::memcpy(lb_out, h.data() + 16, sizeof(gpc_lb_result));
+  uint32_t n = 0;
+  std::memcpy(&n, h.data() + 64 + kMaxTraceSteps * sizeof(TraceStep), 4);
+  if (n_steps) *n_steps = n;
+  if (steps) std::memcpy(steps, h.data() + 64, std::min<size_t>(n, cap) * sizeof(TraceStep));
+  return n > cap && steps ? -GPC_ERANGE : GPC_OK;
 }
 
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count) {
@@ -995,7 +1128,9 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (ctx->comp.ready) {
       ctx->comp.ready = false;
       ctx->comp_pending = false;
-      if (ctx->comp.rc == GPC_OK && !force_full && !ctx->np.foreign()) {
+      const bool discard = ctx->comp.discard;
+      ctx->comp.discard = false;
+      if (ctx->comp.rc == GPC_OK && !force_full && !ctx->np.foreign() && !discard) {
         ctx->last = std::move(*ctx->comp.base);
         ctx->journal = std::move(*ctx->comp.journal);
         ctx->journal.set_base(&ctx->last);

@@ -223,6 +223,48 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
                        reinterpret_cast<uint4*>(out), lb_out, counters, count);
 }
 
+// gpc_trace: one packet through the same table walk as classify_kernel (Service stage and journal
+// included), recording every rule table it evaluates. One lane; debug path, not the data path.
+__global__ void trace_kernel(EpochArgs ep, gpc_pkt_soa pk, uint4* __restrict__ out, uint4* __restrict__ lb_out,
+                             TraceStep* __restrict__ steps, uint32_t* __restrict__ n_steps) {
+  __shared__ uint32_t pkt_lds[kPktWords];
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t src = pk.src[0], dst = pk.dst[0], dport = pk.dport[0];
+  const uint32_t sport = pk.sport[0], proto = pk.proto[0];
+  const uint32_t ct_src = pk.ct_src ? pk.ct_src[0] : src;
+  const uint32_t ct_dst = pk.ct_dst ? pk.ct_dst[0] : dst;
+  uint32_t out_port = pk.out_port[0], svc_group = pk.svc_group ? pk.svc_group[0] : 0u, dest = pk.dest ? pk.dest[0] : 0u;
+  const uint32_t ct_mark = pk.ct_mark ? pk.ct_mark[0] : 0u;
+  uint32_t lb[4] = {0u, 0u, 0u, 0u};
+  *n_steps = 0;
+  if (ep.svc) {
+    const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
+    if (f & GPC_LB_NO_ENDPOINT) {
+      out[0] = make_uint4(0u, pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0), 0u, 0u);
+      lb_out[0] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+      return;
+    }
+  }
+  lb_out[0] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+  Pkt p(pkt_lds, 1);
+  make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[0] : 0u, svc_group,
+           pk.tun_id ? pk.tun_id[0] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+  View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
+  if (ep.pool) {
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
+    if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
+    im.n_img = 2u;
+  }
+  const PacketOut o = classify_packet<true, 0, true>(im, p, dest, ct_mark, steps, n_steps);
+  out[0] = make_uint4(o.e.conj, o.e.packed, o.g.conj, o.g.packed);
+}
+
+int launch_trace(const EpochArgs& ep, const gpc_pkt_soa& pk, uint4* out, uint4* lb_out, TraceStep* steps, uint32_t* n_steps,
+                 hipStream_t stream) {
+  hipLaunchKernelGGL(trace_kernel, dim3(1), dim3(64), 0, stream, ep, pk, out, lb_out, steps, n_steps);
+  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
+}
+
 __global__ void fold_counters_kernel(unsigned long long* __restrict__ c, uint64_t stride, uint32_t copies) {
   const uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (w >= stride) return;

@@ -90,7 +90,7 @@ struct Conjunction {  // policyRuleConjunction (network_policy.go:664-677)
 using ConjPtr = std::shared_ptr<Conjunction>;
 
 struct FlowChange {
-  enum Type { INSERT, MODIFY, DELETE } type;
+  enum Type { INSERT, MODIFY, DELETE } type = MODIFY;
   std::unique_ptr<Flow> flow;  // null: DENY-ALL bookkeeping only
 };
 

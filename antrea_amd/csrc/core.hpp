@@ -172,6 +172,7 @@ struct TableResult {
   uint32_t conj;
   uint32_t slot;
   uint32_t pin;     // GPC_VFLAG_PACKETIN or 0
+  uint32_t prio;    // priority of the deciding flow (action flow of a soft winner, the hard flow; 0: miss)
 };
 
 // ------------------------------------------------------------------------------ hashing / buckets
@@ -590,11 +591,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     }
   }
   const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
-#ifdef GPC_ABL_NOSOFT  // timing experiment only: skip the soft-rule evaluation
-  if (true) {
-#else
   if (n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
-#endif
     if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
     return res;
   }
@@ -624,12 +621,6 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     }
   }
   const bool d1 = cnt1 < cnt0;
-#ifdef GPC_ABL_NOMERGE  // timing experiment only: stop after the bucket lookups
-  if (cnt0 + cnt1 != 0xffffffffu) {
-    res.s = (cnt0 + cnt1) & 1u;
-    return res;
-  }
-#endif
   const uint32_t d = d1 ? 1u : 0u;
   GPC_STAT(0, 1);
   GPC_STAT(1, d1 ? cnt1 : cnt0);
@@ -727,9 +718,6 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
         level_done = 0;
       }
       GPC_STAT(3, 1);
-#ifdef GPC_ABL_NOVERIFY  // timing experiment only: read the record header, skip the clauses
-      if (w2 != 0xffffffffu) continue;
-#endif
       const uint32_t rid = rec[4] >> 8;
       if (rule_dead(im, rid) || !rule_match(im, rec, w2, d, (rec[5] >> (3 * d)) & 7u, p)) {
         GPC_STAT(5, 1);
@@ -807,6 +795,7 @@ GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_bl
   res.conj = 0;
   res.slot = 0;
   res.pin = 0;
+  res.prio = 0;
   const bool hf = (q.h & kHFound) != 0, have = (q.s & kSHave) != 0;
   if (have && !(q.s & kSNoAct)) {
     const uint32_t* rec = ((q.s & kSImg) ? ovl_blob : base_blob) + q.win;
@@ -818,12 +807,14 @@ GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_bl
       res.counted = uint8_t(rec_counted(w2));
       res.slot = rec[3];
       res.pin = (rec[5] & kRecPacketIn) ? uint32_t(GPC_VFLAG_PACKETIN) : 0u;
+      res.prio = rec[1] >> 16;
       if (q.s & kSTie) res.tie = 1;
       return res;
     }
   }
   if (hf) {
     res.verdict = uint8_t((q.h >> 16) & 0xffu);
+    res.prio = q.h & 0xffffu;
     if (have && (q.s & kSTie)) res.tie = 1;
   }
   return res;
@@ -1030,10 +1021,23 @@ struct PacketOut {
   int ecounted, gcounted;
 };
 
+// gpc_trace (Traceflow readback, traceflow/packetin.go:211-270): one record per rule table the
+// packet's walk evaluated, in walk order.
+struct TraceStep {
+  uint32_t table;       // 1..6
+  uint32_t verdict;     // RVerdict of the table (RV_MISS: table-miss -> next table)
+  uint32_t flags;       // GPC_VFLAG_TIE / GPC_VFLAG_PACKETIN of this table's decision
+  uint32_t conj;        // deciding conjunction (0: hard flow or miss)
+  uint32_t priority;    // priority of the deciding flow (0: miss)
+  uint32_t candidates;  // driver-list entries the table's scan had to consider (scan_estimate)
+};
+constexpr uint32_t kMaxTraceSteps = 8;
+
 // kStage: 0 = both stages; 1 = egress only; 2 = ingress only (the caller has checked that the
 // egress verdict lets the packet reach the ingress tables).
-template <bool kJournal = true, int kStage = 0>
-GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, uint32_t ct_mark) {
+template <bool kJournal = true, int kStage = 0, bool kTrace = false>
+GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, uint32_t ct_mark,
+                                 TraceStep* trace = nullptr, uint32_t* n_trace = nullptr) {
   PacketOut o;
   o.e.conj = o.g.conj = 0;
   o.e.packed = o.g.packed = 0;
@@ -1043,6 +1047,15 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, ui
   uint32_t t = kStage == 2 ? 4u : 1u;
   while (true) {
     const TableResult r = eval_table<kJournal>(im, t, p);
+    if (kTrace && *n_trace < kMaxTraceSteps) {
+      TraceStep& st = trace[(*n_trace)++];
+      st.table = t;
+      st.verdict = r.verdict;
+      st.flags = (r.tie ? 2u : 0u) | r.pin;
+      st.conj = r.conj;  // the soft winner's conjunction (0 for hard flows and misses)
+      st.priority = r.prio;
+      st.candidates = scan_estimate(im.base, t, p);
+    }
     const uint32_t i = t <= 3 ? t - 1 : t - 4;  // position inside the stage
     if (r.tie) flags |= 2;
     flags |= r.pin;

@@ -19,6 +19,9 @@ struct EpochArgs {
   uint32_t ctr_stride;    // per-rule counters: words per copy (counter_cap * kCounterWords)
   uint32_t ctr_mask;      // number of striped copies - 1 (a block updates copy blockIdx & mask)
 };
+// One packet (index 0 of the device columns) through the table walk with a per-table trace.
+int launch_trace(const EpochArgs& ep, const gpc_pkt_soa& pk, uint4* out, uint4* lb_out, TraceStep* steps, uint32_t* n_steps,
+                 hipStream_t stream);
 // Sums counter copies 1..copies-1 into copy 0 and zeroes them (stride words per copy).
 int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t copies, hipStream_t stream);
 // dst[w] += sum over r < copies of src[r * src_stride + w], w < n_words (device-scope atomics: launches

@@ -73,6 +73,10 @@ class gpc_pkt_soa(C.Structure):
                                           "src6", "dst6", "ct_src6", "ct_dst6", "ct_mark")]
 
 
+class gpc_trace_step(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("table", "verdict", "flags", "conj_id", "priority", "candidates")]
+
+
 class gpc_policy_info(C.Structure):
     _fields_ = [("found", C.c_int32), ("policy_type", C.c_uint8), ("of_priority", C.c_uint16),
                 ("policy_namespace", C.c_char * 64), ("policy_name", C.c_char * 128), ("policy_uid", C.c_char * 64),
@@ -113,7 +117,7 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
            "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
-           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch"]
+           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay"]
 
 _lib = None
 
@@ -140,6 +144,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_metrics.argtypes = [vp, C.POINTER(gpc_rule_metric), sz, C.POINTER(sz)]
     lib.gpc_commit.argtypes = [vp]
     lib.gpc_compact.argtypes = [vp]
+    lib.gpc_replay.argtypes = [vp]
     lib.gpc_classify.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32, vp]
     lib.gpc_classify_host.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, i32]
     lib.gpc_counters.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz)]
@@ -171,6 +176,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_network_policy_flow_keys.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_uint8, C.c_char_p, sz, C.POINTER(sz),
                                                  C.POINTER(sz)]
     lib.gpc_stream_epoch.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
+    lib.gpc_trace.argtypes = [vp, C.POINTER(gpc_pkt_soa), vp, vp, C.POINTER(gpc_trace_step), sz, C.POINTER(sz)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -510,6 +516,10 @@ class Classifier:
         """Publish pending changes (a delta epoch when few rules changed, else a full rebuild)."""
         _check(self.lib.gpc_commit(self.h), "gpc_commit")
 
+    def replay(self):
+        """ReplayFlows for the device (gpc_replay): rebuild the device state from the host shadow."""
+        _check(self.lib.gpc_replay(self.h), "gpc_replay")
+
     def compact(self):
         """Publish with a full image rebuild (empties the overlay)."""
         _check(self.lib.gpc_compact(self.h), "gpc_compact")
@@ -545,6 +555,19 @@ class Classifier:
     def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, lb_ptr: int = 0):
         _check(self.lib.gpc_classify_lb(self.h, C.byref(soa), n, out_ptr, lb_ptr or None, int(count), stream or None),
                "gpc_classify")
+
+    def trace(self, pkt: Dict[str, int]):
+        """gpc_trace of one packet (dict of column values): (verdicts (2,), [step dicts], lb result)."""
+        cols = {k: np.array([v], dtype=PKT_COLUMNS[k]) for k, v in pkt.items()}
+        soa, keep, n = pkt_soa_host(cols)
+        out = np.zeros(2, dtype=VERDICT_DTYPE)
+        lb = np.zeros(1, dtype=LB_DTYPE)
+        steps = (gpc_trace_step * 8)()
+        ns = C.c_size_t()
+        _check(self.lib.gpc_trace(self.h, C.byref(soa), out.ctypes.data, lb.ctypes.data, steps, 8, C.byref(ns)),
+               "gpc_trace")
+        names = ("table", "verdict", "flags", "conj_id", "priority", "candidates")
+        return out, [{k: getattr(steps[i], k) for k in names} for i in range(ns.value)], lb[0]
 
     def stream_epoch(self, stream: int = 0) -> int:
         """Epoch the last classify launch on `stream` was bound to (gpc_stream_epoch)."""

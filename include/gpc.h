@@ -261,6 +261,16 @@ typedef struct gpc_policy_info { /* GetPolicyInfoFromConjunction result */
   char log_label[64];
 } gpc_policy_info;
 
+typedef struct gpc_trace_step { /* one rule table of a traced packet's walk (gpc_trace) */
+  uint32_t table;                /* gpc_table 1..6                                              */
+  uint32_t verdict;              /* table decision: 1 miss (-> next table), 2 allow, 3 drop, 4 reject,
+                                    5 isolation drop, 6 bypass (to Metric), 7 pass (-> *Rule)   */
+  uint32_t flags;                /* GPC_VFLAG_TIE / GPC_VFLAG_PACKETIN of this decision          */
+  uint32_t conj_id;              /* deciding conjunction (0: a non-conjunctive flow, or a miss)  */
+  uint32_t priority;             /* OpenFlow priority of the deciding flow (0: miss)             */
+  uint32_t candidates;           /* driver-index entries the table's lookup had to consider      */
+} gpc_trace_step;
+
 typedef struct gpc_rule_metric { /* types.RuleMetric keyed by conjunction id */
   uint32_t conj_id;
   uint32_t reserved;
@@ -370,6 +380,10 @@ int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed);
 int gpc_commit(gpc_ctx* ctx);
 /* Same, but always rebuilds the whole image (compaction: empties the overlay). */
 int gpc_compact(gpc_ctx* ctx);
+/* ReplayFlows (client.go:1130-1152) for the device: rebuilds every device buffer of the current
+ * epoch from the host shadow state (after a device reset); flows, conj ids and counter slots are
+ * unchanged, device counters restart from zero. */
+int gpc_replay(gpc_ctx* ctx);
 /* Classify n packets whose columns are DEVICE pointers; writes 2*n verdicts (device pointer).
  * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t. */
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
@@ -381,6 +395,12 @@ int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* o
  * runs the same stage (it just does not write lb_out). */
 int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
                     int32_t count, void* stream);
+/* Traceflow-style readback (traceflow/packetin.go:211-270 reads the verdict registers
+ * back, ovsctl.go:91-183 wraps ofproto/trace): packet 0 of the HOST columns `pkt` through the
+ * current epoch on the device, Service stage included; out[2] = its verdicts (as gpc_classify),
+ * steps[0..*n_steps) = each rule table the walk evaluated, in order. Synchronous; debug path. */
+int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pkt, gpc_verdict* out, gpc_lb_result* lb_out, gpc_trace_step* steps,
+              size_t cap, size_t* n_steps);
 /* IPv6 packets (pkts->src6 / dst6 columns) against the IPv6 half of the rule set (the ipv6_* /
  * tcp6 / udp6 / icmp6 flows and the family-less ones), as OVS classifies an IPv6 packet in the
  * same tables. Needs gpc_config.ipv6_enabled; every commit that changes rules rebuilds the IPv6

@@ -234,13 +234,19 @@ class Pipeline:
         res["out_port"] = p["out_port"]
         return p, flags, res
 
-    def _stage(self, tables, pkt, st):
+    def _stage(self, tables, pkt, st, trace=None):
+        """One policy stage. `trace` (a list) receives one (table 1..6, table verdict, flags, conj id,
+        priority) per rule table evaluated -- table verdicts 1 miss, 2 allow, 3 drop, 4 reject,
+        5 isolation drop, 6 bypass, 7 pass (the gpc_trace_step encoding)."""
         t1, t2, t3, metric = tables
         order = [t1, t2, t3, metric]
+        base = 0 if tables is EGRESS else 3
         t, flags, action, conj, tindex = t1, 0, ACT_NO_MATCH, 0, 0
         while t != metric:
             f, tie = classifier_lookup(self.tables.get(t, []), pkt, st)
             if f is None:
+                if trace is not None:
+                    trace.append((base + order.index(t) + 1, 1, 0, 0, 0))
                 t = order[order.index(t) + 1]
                 continue
             goto = None
@@ -271,6 +277,14 @@ class Pipeline:
             if tie:
                 flags |= FLAG_TIE
             tindex = order.index(t) + 1
+            if trace is not None:
+                if cid:
+                    tv = (3 + int(reject)) if deny else 7 if (goto in (t2,) or (goto == "group" and
+                          st["regs"].get(0, 0) & 0x1800 == 0x1800)) else 2 if commit else 6
+                else:
+                    tv = 5 if (goto is None or goto == "Output") else 6
+                tf = (FLAG_TIE if tie else 0) | (FLAG_PACKETIN if any(a[0] == "controller" for a in f["actions"]) else 0)
+                trace.append((base + tindex, tv, tf, cid, f["priority"]))
             if cid:
                 if deny:
                     conj = cid
@@ -307,9 +321,10 @@ class Pipeline:
             tindex = 0
         return action, conj, tindex, flags, mf
 
-    def classify(self, pkt: dict, lb: Optional[list] = None):
+    def classify(self, pkt: dict, lb: Optional[list] = None, trace: Optional[list] = None):
         """Returns ((e_act, e_conj, e_table, e_tier, e_flags), (i_act, ...)). `lb`: optional list that
-        receives (flags, result dict) of the Service stage."""
+        receives (flags, result dict) of the Service stage; `trace`: optional list receiving the
+        per-table steps of both stages (see _stage)."""
         pkt, lbf, lbr = self.service_stage(pkt)
         if lb is not None:
             lb.append((lbf, lbr))
@@ -317,7 +332,7 @@ class Pipeline:
             return (ACT_REJECT, 0, TABLE_ENDPOINT_DNAT, 0, 0), (ACT_NONE, 0, 0, 0, 0)
         st = {"regs": {}, "ct_label": 0, "conj_id": 0}
         ct = pkt.get("ct_state", CT_NEW | CT_TRK)
-        e = self._stage(EGRESS, pkt, st)
+        e = self._stage(EGRESS, pkt, st, trace)
         ev = (e[0], e[1], e[2], self.tiers.get(e[1], 0) if e[1] else 0, e[3])
         if e[0] in (ACT_DROP, ACT_REJECT, ACT_ISOLATION_DROP):
             return ev, (ACT_NONE, 0, 0, 0, 0)
@@ -331,7 +346,7 @@ class Pipeline:
             if f is not None and any(a[0] == "goto_table" and a[1] in ("IngressMetric", "ConntrackCommit")
                                      for a in f["actions"]):
                 return ev, (ACT_BYPASS, 0, 0, 0, FLAG_TIE if tie else 0)
-        i = self._stage(INGRESS, pkt, st)
+        i = self._stage(INGRESS, pkt, st, trace)
         iv = (i[0], i[1], i[2], self.tiers.get(i[1], 0) if i[1] else 0, i[3])
         return ev, iv
 

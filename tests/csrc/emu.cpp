@@ -84,6 +84,32 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
   return 0;
 }
 
+// gpc_trace's walk (core.hpp classify_packet<..., kTrace>) for packet 0 of the columns (no Service stage).
+extern "C" int emu_trace(const uint32_t* blob, const void* hdr, const uint32_t* pool, uint32_t jhdr, const gpc_pkt_soa* pk,
+                         gpc_verdict* out, TraceStep* steps, uint32_t* n_steps) {
+  View im{{blob, static_cast<const ImageHdr*>(hdr), nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr};
+  if (pool) {
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + jhdr);
+    if (jh->bdead_off) im.base.dead = pool + jh->bdead_off;
+    im.n_img = 2u;
+  }
+  const uint32_t src = pk->src[0], dst = pk->dst[0];
+  uint32_t pst[kPktWords];
+  Pkt p(pst, 1);
+  make_pkt(p, src, dst, pk->sport[0], pk->dport[0], pk->proto[0], pk->out_port[0], pk->in_port ? pk->in_port[0] : 0u,
+           pk->svc_group ? pk->svc_group[0] : 0u, pk->tun_id ? pk->tun_id[0] : 0u, pk->ct_src ? pk->ct_src[0] : src,
+           pk->ct_dst ? pk->ct_dst[0] : dst, pk->ct_state ? pk->ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+  *n_steps = 0;
+  PacketOut o = classify_packet<true, 0, true>(im, p, pk->dest ? pk->dest[0] : 0u, pk->ct_mark ? pk->ct_mark[0] : 0u, steps,
+                                               n_steps);
+  uint32_t* w = reinterpret_cast<uint32_t*>(out);
+  w[0] = o.e.conj;
+  w[1] = o.e.packed;
+  w[2] = o.g.conj;
+  w[3] = o.g.packed;
+  return 0;
+}
+
 // IPv6 batch over the IPv6 image (gpc_debug_image6): addresses mapped to codes as the kernel does.
 extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
                              unsigned long long* counters) {

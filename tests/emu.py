@@ -29,6 +29,8 @@ def load():
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
     _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                   C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
+    _lib.emu_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(gpc.gpc_pkt_soa), C.c_void_p,
+                               C.POINTER(gpc.gpc_trace_step), C.POINTER(C.c_uint32)]
     _lib.emu_classify6.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p,
                                    C.c_void_p]
     return _lib
@@ -122,3 +124,17 @@ def classify_snapshot(snap, cols, counters=None):
     load().emu_classify(snap["blob"].ctypes.data, snap["hdr"].ctypes.data, pool, snap["jhdr"], None, C.byref(soa), n,
                         out.ctypes.data, None, cptr)
     return out.reshape(n, 2)
+
+
+def trace(clf: "gpc.Classifier", pkt):
+    """Emulated gpc_trace of one packet (dict of column values): (verdicts (2,), [step dicts])."""
+    blob, nw, hdr, _ = clf.debug_image()
+    pool, _, jhdr = clf.debug_epoch()
+    cols = {k: np.array([v], dtype=gpc.PKT_COLUMNS[k]) for k, v in pkt.items()}
+    soa, keep, n = gpc.pkt_soa_host(cols)
+    out = np.zeros(2, dtype=gpc.VERDICT_DTYPE)
+    steps = (gpc.gpc_trace_step * 8)()
+    ns = C.c_uint32()
+    load().emu_trace(blob, hdr, pool, jhdr, C.byref(soa), out.ctypes.data, steps, C.byref(ns))
+    names = ("table", "verdict", "flags", "conj_id", "priority", "candidates")
+    return out, [{k: getattr(steps[i], k) for k in names} for i in range(ns.value)]

@@ -229,3 +229,33 @@ def test_gpu_rccl_counter_allreduce_world1():
         assert got and got == {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)}
     finally:
         tdist.destroy_process_group()
+
+
+def test_gpu_replay_rebuilds_device_state():
+    """gpc_replay (ReplayFlows for the device, client.go:1130-1152): every device buffer of the
+    current epoch -- base image, journal pool (a delta epoch), IPv6 image -- is rebuilt from the
+    host shadow state; verdicts are unchanged and counters restart from zero, as OVS's do when the
+    agent replays its flows."""
+    wl = workload.config1(seed=71)
+    c = gpc.Classifier(ipv6=True)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(workload.to_ipv6(wl, dual=True).rules))
+    c.commit()
+    c.add_policy_rule_address(wl.rules[0]["flow_id"], "src", ["10.10.0.77", "fd00:10::10.10.0.77"],
+                              wl.rules[0].get("priority"))
+    c.commit()
+    assert c.image_stats()["n_overlay_rules"] > 0  # a delta epoch: the journal pool must travel too
+    cols = workload.gen_packets(wl, 20000, seed=71)
+    v4 = c.classify_host(cols, count=True)
+    v6 = c.classify6_host(workload.packets_to_v6(cols))
+    m1 = {k: v for k, v in c.network_policy_metrics().items() if any(v)}
+    e0 = c.image_stats()["epoch"]
+    c.replay()
+    assert c.image_stats()["epoch"] == e0 + 1
+    assert not any(any(v) for v in c.network_policy_metrics().values())  # counters restart from zero
+    assert (c.classify_host(cols, count=True) == v4).all()
+    assert (c.classify6_host(workload.packets_to_v6(cols)) == v6).all()
+    assert {k: v for k, v in c.network_policy_metrics().items() if any(v)} == m1
+    c.add_policy_rule_address(wl.rules[1]["flow_id"], "src", ["10.10.0.78"], wl.rules[1].get("priority"))
+    c.commit()  # delta commits continue on the replayed journal
+    _cmp(c.classify_host(cols), emu.classify(c, cols), cols)

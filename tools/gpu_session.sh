@@ -7,7 +7,8 @@
 #   bench   python bench.py (default C3 line: PMC passes, parity stamp, CPU baseline)
 #   cfg:X   bench.py --config X (C1, C2, C4, C5) ; v6 = C3 in IPv6
 #   kt      rocprofv3 --kernel-trace --stats over a short bench run
-#   sq      rocprofv3 SQ counters ; tcc  TCC hit / miss ; fetch / write  FETCH_SIZE / WRITE_SIZE
+#   sq[:X]  rocprofv3 SQ counters (config X, default C3) ; tcc[:X] TCC hit / miss / EA read requests
+#   fetch / write  FETCH_SIZE / WRITE_SIZE of C3
 # Outputs under gpurun_out/TAG/. Every GPU step has its own time limit; the script stops at the
 # first failure (no retries).
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
@@ -19,11 +20,11 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 step() { echo "== $1 ($(date +%T))"; }
 KT_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-traffic --no-parity"
-pmc() {  # name, counters...
-  local name=$1; shift
-  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex classify -d "$O/pmc_$name" -o pmc \
+pmc() {  # name, config, counters...
+  local name=$1 cfg=$2; shift 2
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex classify -d "$O/pmc_${name}_$cfg" -o pmc \
     --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-traffic --no-parity \
-    ${PMC_CFG:+--config $PMC_CFG} > "$O/pmc_$name.log" 2>&1
+    --config $cfg > "$O/pmc_${name}_$cfg.log" 2>&1
 }
 for s in $STEPS; do
   case $s in
@@ -48,18 +49,19 @@ for s in $STEPS; do
     kt)
       step "rocprof kernel trace"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- \
-        python3 bench.py $KT_ARGS ${PMC_CFG:+--config $PMC_CFG} > "$O/kt.log" 2>&1 || exit $?
+        python3 bench.py $KT_ARGS > "$O/kt.log" 2>&1 || exit $?
       tail -1 "$O/kt.log" ;;
-    sq)
-      step "rocprof SQ"
-      pmc sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
+    sq|sq:*)
+      c=${s#sq}; c=${c#:}; c=${c:-C3}; step "rocprof SQ $c"
+      pmc sq $c SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
         SQ_INSTS_VMEM_RD SQ_WAVES || exit $? ;;
-    tcc)
-      step "rocprof TCC"; pmc tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum || exit $? ;;
+    tcc|tcc:*)
+      c=${s#tcc}; c=${c#:}; c=${c:-C3}; step "rocprof TCC $c"
+      pmc tcc $c TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum || exit $? ;;
     fetch)
-      step "rocprof FETCH_SIZE"; pmc fetch FETCH_SIZE || exit $? ;;
+      step "rocprof FETCH_SIZE"; pmc fetch C3 FETCH_SIZE || exit $? ;;
     write)
-      step "rocprof WRITE_SIZE"; pmc write WRITE_SIZE || exit $? ;;
+      step "rocprof WRITE_SIZE"; pmc write C3 WRITE_SIZE || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
