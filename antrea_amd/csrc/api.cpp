@@ -42,6 +42,15 @@ static void dev_free(void* p, hipStream_t s) {
   }
 }
 
+// Tuning knobs read once per context (documented in DESIGN.md §4); out-of-range values: default.
+static uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const unsigned long x = std::strtoul(v, &end, 10);
+  return (*end || x < lo || x > hi) ? dflt : uint32_t(x);
+}
+
 struct DevImage {  // one uploaded image (freed when the last epoch using it retires)
   ImageHdr* d_hdr = nullptr;
   uint32_t* d_blob = nullptr;
@@ -125,6 +134,8 @@ struct gpc_ctx {
   DevEpoch cur;
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
+  bool pool_kept = false;                // default mem pool release threshold raised (first classify)
+  uint32_t group_shift = env_u32("GPC_GROUP_SHIFT", 24, 0, 31);  // packet grouping key (classify.hip)
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;
   unsigned long long* d_counters = nullptr;
@@ -779,6 +790,9 @@ int gpc_replay(gpc_ctx* ctx) {
 }
 int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
 
+// Batches from this size on are grouped by nw_src before the table walk (gpc_config.group_packets = 0).
+constexpr size_t kGroupMinPackets = size_t(1) << 18;
+
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
   return gpc_classify_lb(ctx, pk, n, out, nullptr, count, stream);
 }
@@ -795,7 +809,24 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
                {ctx->cur.base->sort_table[0], ctx->cur.base->sort_table[1]},
                uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count, st);
+  // packet grouping (classify.hip group_*): scratch allocated and freed stream-ordered on the
+  // caller's stream, so concurrent callers on other streams never share it
+  const int gm = ctx->cfg.group_packets;
+  if (!ctx->pool_kept) {  // freed stream-ordered allocations (grouping scratch, epochs) stay pooled for reuse
+    hipMemPool_t pool;
+    uint64_t keep = UINT64_MAX;
+    if (hipDeviceGetDefaultMemPool(&pool, ctx->cfg.device) == hipSuccess)
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    (void)hipGetLastError();
+    ctx->pool_kept = true;
+  }
+  GroupArgs ga{nullptr, ctx->group_shift};
+  if (n && (gm > 0 || (gm == 0 && n >= kGroupMinPackets)) &&
+      hip_ok(dev_alloc((void**)&ga.scratch, group_scratch_bytes(*pk, n), st)))
+    return -GPC_ENOMEM;
+  int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
+                           ga.scratch ? &ga : nullptr, st);
+  if (ga.scratch) dev_free(ga.scratch, st);
   if (rc || n == 0) return rc;
   ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained

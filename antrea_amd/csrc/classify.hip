@@ -66,16 +66,18 @@ __device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_
 // the packet index this lane now owns (>= n: none).
 template <int kStage>
 __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n,
-                                                 const uint4* __restrict__ out, uint64_t i, uint32_t* pkt_lds) {
+                                                 const uint4* __restrict__ out, const uint2* __restrict__ mid, uint64_t i,
+                                                 uint32_t* pkt_lds) {
   constexpr uint32_t kBins = 64;  // one wavefront scans the histogram
   __shared__ uint32_t hist[kBins];
   __shared__ uint16_t perm[kSortBlock];
+  __shared__ uint32_t lane_pkt[kSortBlock];  // packet of each lane before the regrouping (< 2^32: kMaxPackets)
   const uint32_t tid = threadIdx.x;
   uint32_t est = 0;
   if (i < n) {
     bool live = true;
     if (kStage == 2) {  // packets the ingress launch settles without table work weigh nothing
-      const uint32_t ea = out[i].y & 0xffu;
+      const uint32_t ea = (mid ? mid[i].y : out[i].y) & 0xffu;
       live = ea != RV_DROP && ea != RV_REJECT && ea != RV_ISO_DROP &&
              !ingress_bypass(ep.hdr->isc, pk.dest ? pk.dest[i] : 0u, pk.ct_mark ? pk.ct_mark[i] : 0u);
     }
@@ -90,6 +92,7 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
     }
   }
   const uint32_t bin = est >> 1 < kBins - 1 ? est >> 1 : kBins - 1;
+  lane_pkt[tid] = i < n ? uint32_t(i) : 0xffffffffu;
   if (tid < kBins) hist[tid] = 0;
   __syncthreads();
   const uint32_t r = atomicAdd(&hist[bin], 1u);
@@ -107,22 +110,122 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
   __syncthreads();
   perm[hist[bin] + r] = uint16_t(tid);
   __syncthreads();
-  return uint64_t(blockIdx.x) * kSortBlock + perm[tid];
+  const uint32_t q = lane_pkt[perm[tid]];
+  return q == 0xffffffffu ? n : uint64_t(q);
+}
+
+// Packet grouping. Lanes of a wavefront that classify packets of one address
+// region share driver buckets, candidate lists and rule records, so their loads coalesce and their
+// scans run the same length. For a grouped batch a first launch rewrites every tile of kGroupTile
+// packets in the order of (nw_src >> shift) & 255 (a counting sort in LDS, then every present
+// column staged through LDS: coalesced reads and writes) and records each grouped packet's caller
+// index. The egress launch leaves its verdict in mid[] (grouped order); the ingress launch (or the
+// single Service launch) stores the verdict pair / LB result at the caller index. The blocks of
+// one tile run on one XCD (block_xcd_order), so those scattered stores stay inside one tile's
+// window of one L2 and leave it as whole lines. Packets are independent and counters are sums:
+// the grouping never shows in the results.
+constexpr uint32_t kGroupThreads = 1024, kGroupBins = 256, kGroupTile = 16384;
+
+template <typename T>
+__device__ __forceinline__ void group_column(const T* __restrict__ in, T* __restrict__ outc, uint64_t base, uint32_t m,
+                                             const uint16_t* from, void* stage) {
+  T* buf = reinterpret_cast<T*>(stage);
+  __syncthreads();  // the previous column's reads of `stage` are done
+  for (uint32_t j = threadIdx.x; j < m; j += kGroupThreads) buf[j] = in[base + j];
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < m; k += kGroupThreads) outc[base + k] = buf[from[k]];
+}
+
+__global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa in, uint64_t n, uint32_t shift,
+                                                                    gpc_pkt_soa g, uint32_t* __restrict__ orig) {
+  __shared__ uint32_t stage[kGroupTile];  // one column of the tile
+  __shared__ uint16_t from[kGroupTile];   // grouped position -> tile position
+  __shared__ uint32_t cur[kGroupBins];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
+  const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
+  if (tid < kGroupBins) cur[tid] = 0;
+  for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = in.src[base + j];
+  __syncthreads();
+  for (uint32_t j = tid; j < m; j += kGroupThreads) atomicAdd(&cur[(stage[j] >> shift) & (kGroupBins - 1)], 1u);
+  __syncthreads();
+  if (tid < 64) {  // exclusive prefix over the 256 bins: one wavefront, 4 bins per lane
+    const uint32_t c0 = cur[4 * tid], c1 = cur[4 * tid + 1], c2 = cur[4 * tid + 2], c3 = cur[4 * tid + 3];
+    const uint32_t v = c0 + c1 + c2 + c3;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (tid >= d) x += y;
+    }
+    const uint32_t e = x - v;
+    cur[4 * tid] = e;
+    cur[4 * tid + 1] = e + c0;
+    cur[4 * tid + 2] = e + c0 + c1;
+    cur[4 * tid + 3] = e + c0 + c1 + c2;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < m; j += kGroupThreads)
+    from[atomicAdd(&cur[(stage[j] >> shift) & (kGroupBins - 1)], 1u)] = uint16_t(j);
+  __syncthreads();
+  uint32_t* gsrc = const_cast<uint32_t*>(g.src);
+  for (uint32_t k = tid; k < m; k += kGroupThreads) {
+    const uint32_t j = from[k];
+    gsrc[base + k] = stage[j];
+    orig[base + k] = uint32_t(base + j);
+  }
+#define GPC_GROUP_COL(c, T) \
+  if (in.c) group_column<T>(in.c, const_cast<T*>(g.c), base, m, from, stage)
+  GPC_GROUP_COL(dst, uint32_t);
+  GPC_GROUP_COL(sport, uint16_t);
+  GPC_GROUP_COL(dport, uint16_t);
+  GPC_GROUP_COL(proto, uint8_t);
+  GPC_GROUP_COL(out_port, uint32_t);
+  GPC_GROUP_COL(in_port, uint32_t);
+  GPC_GROUP_COL(svc_group, uint32_t);
+  GPC_GROUP_COL(tun_id, uint32_t);
+  GPC_GROUP_COL(ct_src, uint32_t);
+  GPC_GROUP_COL(ct_dst, uint32_t);
+  GPC_GROUP_COL(ct_state, uint8_t);
+  GPC_GROUP_COL(dest, uint8_t);
+  GPC_GROUP_COL(len, uint16_t);
+  GPC_GROUP_COL(ct_mark, uint8_t);
+#undef GPC_GROUP_COL
+}
+
+// Logical block of this workgroup for a grouped batch: workgroups are dispatched round-robin over
+// the 8 XCDs, so XCD x (blocks b with b % 8 == x) gets the contiguous logical range
+// [x*q + min(x, r), ...) of the G = 8q + r blocks. A bijection whatever the dispatch order.
+__device__ __forceinline__ uint64_t block_xcd_order() {
+  const uint32_t b = blockIdx.x, G = gridDim.x, q = G >> 3, r = G & 7u, x = b & 7u;
+  return uint64_t(x) * q + (x < r ? x : r) + (b >> 3);
 }
 
 // kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
+// orig != null: a grouped batch (group_tiles_kernel): pk holds the grouped columns, lane i of the
+// logical block order classifies grouped packet i, whose caller index is orig[i].
 template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = false>
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
-    unsigned long long* __restrict__ counters, int count) {
+    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid) {
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
-  uint64_t i = uint64_t(blockIdx.x) * block_threads<kSort>() + threadIdx.x;
-  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, i, pkt_lds);  // its own instantiation: the plain kernel has no barrier
+  uint64_t i = (orig ? block_xcd_order() : uint64_t(blockIdx.x)) * block_threads<kSort>() + threadIdx.x;
+  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, i, pkt_lds);  // its own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
   uint4 prev = make_uint4(0u, 0u, 0u, 0u);
-  if (kStage == 2) prev = out[i];
+  if (kStage == 2) {
+    if (orig) {
+      const uint2 v = mid[i];
+      prev.x = v.x;
+      prev.y = v.y;
+    } else {
+      prev = out[i];
+    }
+  }
+  // caller index of this packet (loaded where a result is stored: no register held over the walk)
+  auto at = [&]() -> uint64_t { return orig ? uint64_t(orig[i]) : i; };
   if (kV6) {
     // The egress launch computes the src / dst codes (both LPMs in lock step) and parks them in the
     // still empty ingress half of the verdict pair; the ingress launch takes them from there.
@@ -159,22 +262,22 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if (kSvc) {  // both launches derive the same Endpoint (the selection is a pure function of the packet)
     uint32_t lb[4];
     const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
-    if (kStage != 2 && lb_out) lb_out[i] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+    if (kStage != 2 && lb_out) lb_out[at()] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
     if (f & GPC_LB_NO_ENDPOINT) {  // EndpointDNAT serviceNoEndpointFlow: rejected before the policy stages
-      if (kStage != 2) out[i] = make_uint4(0u, pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0), 0u, 0u);
+      if (kStage != 2) out[at()] = make_uint4(0u, pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0), 0u, 0u);
       return;
     }
   } else if (kStage != 2 && lb_out) {
-    lb_out[i] = make_uint4(0u, 0u, 0u, 0u);
+    lb_out[at()] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
     const uint32_t ea = prev.y & 0xffu;
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
-      if (kV6) out[i] = make_uint4(prev.x, prev.y, 0u, 0u);  // ingress NONE over the parked codes
+      if (kV6 || orig) out[at()] = make_uint4(prev.x, prev.y, 0u, 0u);  // ingress NONE (over the parked codes)
       return;
     }
     if (const uint32_t b = ingress_bypass(ep.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
-      out[i] = make_uint4(prev.x, prev.y, 0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
+      out[at()] = make_uint4(prev.x, prev.y, 0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
       return;
     }
   }
@@ -194,33 +297,35 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&copy[w], v); });
   }
   const VerdictOut e = o.e, g = o.g;
-  if (kStage == 2) out[i] = make_uint4(prev.x, prev.y, g.conj, g.packed);
+  if (kStage == 2) out[at()] = make_uint4(prev.x, prev.y, g.conj, g.packed);
   else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
-  else out[i] = make_uint4(e.conj, e.packed, g.conj, g.packed);  // ingress NONE until the second launch
+  else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
+  else out[at()] = make_uint4(e.conj, e.packed, g.conj, g.packed);  // ingress NONE until the second launch
 }
 
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                   unsigned long long* counters, int count, hipStream_t stream) {
+                   unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, hipStream_t stream) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  uint4* const o = reinterpret_cast<uint4*>(out);
   if (kSvc) {
-    hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                       reinterpret_cast<uint4*>(out), lb_out, counters, count);
+    hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
+                       lb_out, counters, count, orig, mid);
     return;
   }
   const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
   if (ep.sort_table[0])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
-                       ep, pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
+                       ep, pk, n, o, lb_out, counters, count, orig, mid);
   else
-    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                       reinterpret_cast<uint4*>(out), lb_out, counters, count);
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
+                       lb_out, counters, count, orig, mid);
   if (ep.sort_table[1])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
-                       ep, pk, n, reinterpret_cast<uint4*>(out), lb_out, counters, count);
+                       ep, pk, n, o, lb_out, counters, count, orig, mid);
   else
-    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                       reinterpret_cast<uint4*>(out), lb_out, counters, count);
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
+                       lb_out, counters, count, orig, mid);
 }
 
 // gpc_trace: one packet through the same table walk as classify_kernel (Service stage and journal
@@ -307,21 +412,61 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   if (n > kMaxPackets) return -GPC_EINVAL;
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count);
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr);
   hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count);
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n) {
+  uint64_t per = 4 /*src*/ + 4 /*orig*/ + 8 /*mid*/ + 4 + 2 + 2 + 1 + 4;  // + dst sport dport proto out_port
+  per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0) +
+         (pk.ct_state ? 1 : 0) + (pk.dest ? 1 : 0) + (pk.len ? 2 : 0) + (pk.ct_mark ? 1 : 0);
+  return per * n + 16 * 256;  // every region 256-B aligned
+}
+
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                    unsigned long long* counters, int count, hipStream_t stream) {
+                    unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream) {
   if (n == 0) return 0;
   if (n > kMaxPackets) return -GPC_EINVAL;
+  gpc_pkt_soa g{};
+  const gpc_pkt_soa* p = &pk;
+  uint32_t* orig = nullptr;
+  uint2* mid = nullptr;
+  if (group) {
+    if (!group->scratch || group->shift > 31) return -GPC_EINVAL;
+    uint8_t* q = group->scratch;
+    auto take = [&](uint64_t bytes) {
+      uint8_t* r = q;
+      q += (bytes + 255) & ~uint64_t(255);
+      return r;
+    };
+    mid = reinterpret_cast<uint2*>(take(8 * n));
+    orig = reinterpret_cast<uint32_t*>(take(4 * n));
+    g.src = reinterpret_cast<const uint32_t*>(take(4 * n));
+    g.dst = reinterpret_cast<const uint32_t*>(take(4 * n));
+    g.sport = reinterpret_cast<const uint16_t*>(take(2 * n));
+    g.dport = reinterpret_cast<const uint16_t*>(take(2 * n));
+    g.proto = take(n);
+    g.out_port = reinterpret_cast<const uint32_t*>(take(4 * n));
+    if (pk.in_port) g.in_port = reinterpret_cast<const uint32_t*>(take(4 * n));
+    if (pk.svc_group) g.svc_group = reinterpret_cast<const uint32_t*>(take(4 * n));
+    if (pk.tun_id) g.tun_id = reinterpret_cast<const uint32_t*>(take(4 * n));
+    if (pk.ct_src) g.ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
+    if (pk.ct_dst) g.ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
+    if (pk.ct_state) g.ct_state = take(n);
+    if (pk.dest) g.dest = take(n);
+    if (pk.len) g.len = reinterpret_cast<const uint16_t*>(take(2 * n));
+    if (pk.ct_mark) g.ct_mark = take(n);
+    const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
+    hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, pk, n, group->shift, g, orig);
+    p = &g;
+  }
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
-  if (delta && svc) launch<true, true>(ep, pk, n, out, lb_out, counters, count, stream);
-  else if (delta) launch<true, false>(ep, pk, n, out, lb_out, counters, count, stream);
-  else if (svc) launch<false, true>(ep, pk, n, out, lb_out, counters, count, stream);
-  else launch<false, false>(ep, pk, n, out, lb_out, counters, count, stream);
+  if (delta && svc) launch<true, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
+  else if (delta) launch<true, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
+  else if (svc) launch<false, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
+  else launch<false, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

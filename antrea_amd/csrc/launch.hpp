@@ -28,8 +28,17 @@ int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t
 // on other streams may be adding to dst concurrently). Used when the counter array grows.
 int launch_merge_counters(unsigned long long* dst, const unsigned long long* src, uint64_t src_stride, uint32_t copies,
                           uint64_t n_words, hipStream_t stream);
+// Packet grouping of a batch (classify.hip group_tiles_kernel): the batch is classified in the
+// order of (nw_src >> shift) & 255 within every tile of 16384 packets, from a grouped copy in
+// `scratch` (group_scratch_bytes(pk, n) bytes of device memory, live until the launches have run:
+// stream-ordered).
+struct GroupArgs {
+  uint8_t* scratch;
+  uint32_t shift;
+};
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n);
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                    unsigned long long* counters, int count, hipStream_t stream);
+                    unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream);
 // IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
                      unsigned long long* counters, int count, hipStream_t stream);

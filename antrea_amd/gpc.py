@@ -41,7 +41,7 @@ class gpc_config(C.Structure):
     _fields_ = [("ipv4_enabled", C.c_int32), ("ipv6_enabled", C.c_int32), ("enable_antrea_policy", C.c_int32),
                 ("enable_deny_tracking", C.c_int32), ("cookie", C.c_uint64), ("device", C.c_int32),
                 ("compact_after", C.c_int32), ("ovs_meters", C.c_int32), ("external_node", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("group_packets", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class gpc_addr(C.Structure):
@@ -344,13 +344,13 @@ class Classifier:
     """One gpc context (one GPU)."""
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
-                 cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True):
+                 cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True, group_packets=0):
         self.lib = load()
         cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
                          enable_antrea_policy=int(enable_antrea_policy),
                          enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device,
                          compact_after=int(compact_after), ovs_meters=int(ovs_meters),
-                         external_node=int(not k8s_node))
+                         external_node=int(not k8s_node), group_packets=int(group_packets))
         h = C.c_void_p()
         _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
         self.h = h

@@ -215,6 +215,8 @@ def main():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
+    ap.add_argument("--group", type=int, default=0,
+                    help="gpc_config.group_packets: 0 = auto (batches >= 2^18 grouped by nw_src), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),
                     help="6: the workload's addresses embedded in fd00:10::/96, IPv6 packets (gpc_classify6)")
     args = ap.parse_args()
@@ -270,7 +272,7 @@ def main():
     t0 = time.time()
     wl = workload.CONFIGS["C3" if churn else args.config]()
     v6 = args.family == 6
-    clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6)
+    clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6, group_packets=args.group)
     clf.initialize()
     clf.batch_install_policy_rule_flows(workload.to_ipv6(wl).rules if v6 else wl.rules)
     if getattr(wl, "services", None):
@@ -404,7 +406,9 @@ def main():
                    "flows": st["n_flows"],
                    "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
-                   "verdict_mix": mix, "build_s": round(t_build, 1)},
+                   "verdict_mix": mix, "build_s": round(t_build, 1),
+                   "packet_grouping": ("nw_src >> %s in 16384-packet tiles" % os.environ.get("GPC_GROUP_SHIFT", "24"))
+                   if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18)) else "off"},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)
         "launches_per_step": 1 if getattr(wl, "services", None) else 2,
         "roofline": roofline,

@@ -128,7 +128,9 @@ typedef struct gpc_config {
                                     (0: max(2048, rules / 32); < 0: never in the background)   */
   int32_t ovs_meters;            /* OVS meters supported: packet-in flows carry meter:256/258    */
   int32_t external_node;         /* config.ExternalNode: no IngressSecurityClassifier flows      */
-  int32_t reserved[4];
+  int32_t group_packets;         /* gpc_classify groups a batch by nw_src before the table walk:
+                                    0 = for batches of >= 2^18 packets, > 0 = always, < 0 = never  */
+  int32_t reserved[3];
 } gpc_config;
 
 typedef struct gpc_addr {        /* 24 bytes */

@@ -27,8 +27,8 @@ def _built():
     assert torch.cuda.is_available(), "GPU tier needs a HIP device"
 
 
-def _classifier(wl, ipv6=False, rules=None):
-    c = gpc.Classifier(ipv4=not ipv6, ipv6=ipv6)
+def _classifier(wl, ipv6=False, rules=None, group=0):
+    c = gpc.Classifier(ipv4=not ipv6, ipv6=ipv6, group_packets=group)
     c.initialize()
     c.batch_install_policy_rule_flows(copy.deepcopy(rules if rules is not None else wl.rules))
     if getattr(wl, "services", None):
@@ -49,15 +49,17 @@ def _nonzero(m):
     return {int(k): tuple(int(x) for x in v) for k, v in m.items() if any(v)}
 
 
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
 @pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4"])
-def test_device_vs_oracle_fullscale(config):
+def test_device_vs_oracle_fullscale(config, group):
     """Verdicts (conj id, action, table, tier, flags) and NetworkPolicyMetrics of 100k packets at
     full scale equal the C oracle's exactly (C4: the packets that hit no Service, with the Service
-    stage live in the kernel)."""
+    stage live in the kernel), with the packet grouping pre-pass off and on (the bench's 64M-packet
+    batches are grouped)."""
     f, wl, cols = _inputs(config)
     mask = f["mask"].astype(bool)
     sub = cols if mask.all() else {k: v[mask] for k, v in cols.items()}
-    c = _classifier(wl)
+    c = _classifier(wl, group=group)
     got = c.classify_host(sub, count=True)
     res = parity.compare(got, f["verdicts"][mask])
     assert res["mismatches"] == 0, res

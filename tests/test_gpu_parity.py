@@ -131,17 +131,19 @@ def _ip(v):
     return "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
 
 
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
 @pytest.mark.parametrize("name", ["C1", "C3"])
-def test_gpu_delta_epochs(name):
+def test_gpu_delta_epochs(name, group):
     """Delta epochs on the device (overlay image + tombstones): after address churn, uninstall and
     reinstall, each published through gpc_commit, the device verdicts and counters equal the host
-    emulation of the same epoch, and a compaction gives the same verdicts again."""
+    emulation of the same epoch, and a compaction gives the same verdicts again; with and without
+    the packet grouping pre-pass."""
     wl = workload.config1(seed=31) if name == "C1" else workload.config3()
     n = 20000 if name == "C1" else 200_000
     cols = workload.gen_packets(wl, n, seed=31)
     rng = np.random.default_rng(31)
     rules = copy.deepcopy(wl.rules)
-    c = gpc.Classifier()
+    c = gpc.Classifier(group_packets=group)
     c.initialize()
     c.batch_install_policy_rule_flows(copy.deepcopy(rules))
     c.commit()
@@ -183,16 +185,18 @@ def test_gpu_delta_epochs(name):
     _cmp(again, want, cols)
 
 
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
 @pytest.mark.parametrize("name", ["C1", "C4"])
-def test_gpu_service_stage(name):
+def test_gpu_service_stage(name, group):
     """AntreaProxy stage on the device: verdicts and per-packet LB results equal the host emulation of
     the same epoch (small: C1 + 60 Services; full: C4 = C3 + 10k Services x 10 Endpoints); the small
-    case also against the oracle."""
+    case also against the oracle; with and without the packet grouping pre-pass (LB results are
+    scattered back to caller order)."""
     from tests.test_service import _oracle, _svc_workload
     wl = _svc_workload("C1", 61) if name == "C1" else workload.config4()
     n = 3000 if name == "C1" else 200_000
     cols = workload.gen_packets(wl, n, seed=61)
-    c = gpc.Classifier()
+    c = gpc.Classifier(group_packets=group)
     c.initialize()
     c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
     workload.install_services(c, wl)
