@@ -66,12 +66,12 @@ __device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_
 // the packet index this lane now owns (>= n: none).
 template <int kStage>
 __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n,
-                                                 const uint4* __restrict__ out, const uint2* __restrict__ mid, uint64_t i,
-                                                 uint32_t* pkt_lds) {
+                                                 const uint4* __restrict__ out, const uint2* __restrict__ mid,
+                                                 uint64_t block_base, uint32_t* pkt_lds) {
   constexpr uint32_t kBins = 64;  // one wavefront scans the histogram
   __shared__ uint32_t hist[kBins];
   __shared__ uint16_t perm[kSortBlock];
-  __shared__ uint32_t lane_pkt[kSortBlock];  // packet of each lane before the regrouping (< 2^32: kMaxPackets)
+  const uint64_t i = block_base + threadIdx.x;
   const uint32_t tid = threadIdx.x;
   uint32_t est = 0;
   if (i < n) {
@@ -92,7 +92,6 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
     }
   }
   const uint32_t bin = est >> 1 < kBins - 1 ? est >> 1 : kBins - 1;
-  lane_pkt[tid] = i < n ? uint32_t(i) : 0xffffffffu;
   if (tid < kBins) hist[tid] = 0;
   __syncthreads();
   const uint32_t r = atomicAdd(&hist[bin], 1u);
@@ -110,8 +109,7 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
   __syncthreads();
   perm[hist[bin] + r] = uint16_t(tid);
   __syncthreads();
-  const uint32_t q = lane_pkt[perm[tid]];
-  return q == 0xffffffffu ? n : uint64_t(q);
+  return block_base + perm[tid];
 }
 
 // Packet grouping. Lanes of a wavefront that classify packets of one address
@@ -207,11 +205,13 @@ __device__ __forceinline__ uint64_t block_xcd_order() {
 template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = false>
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
-    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid) {
+    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
+    uint32_t xcd_order) {
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
-  uint64_t i = (orig ? block_xcd_order() : uint64_t(blockIdx.x)) * block_threads<kSort>() + threadIdx.x;
-  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, i, pkt_lds);  // its own instantiation: the plain kernel has no barrier
+  const uint64_t block_base = (xcd_order ? block_xcd_order() : uint64_t(blockIdx.x)) * block_threads<kSort>();
+  uint64_t i = block_base + threadIdx.x;
+  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // its own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
   uint4 prev = make_uint4(0u, 0u, 0u, 0u);
@@ -305,27 +305,28 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
 
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                   unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, hipStream_t stream) {
+                   unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, uint32_t xo,
+                   hipStream_t stream) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   uint4* const o = reinterpret_cast<uint4*>(out);
   if (kSvc) {
     hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid);
+                       lb_out, counters, count, orig, mid, xo);
     return;
   }
   const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
   if (ep.sort_table[0])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
-                       ep, pk, n, o, lb_out, counters, count, orig, mid);
+                       ep, pk, n, o, lb_out, counters, count, orig, mid, xo);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid);
+                       lb_out, counters, count, orig, mid, xo);
   if (ep.sort_table[1])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
-                       ep, pk, n, o, lb_out, counters, count, orig, mid);
+                       ep, pk, n, o, lb_out, counters, count, orig, mid, xo);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid);
+                       lb_out, counters, count, orig, mid, xo);
 }
 
 // gpc_trace: one packet through the same table walk as classify_kernel (Service stage and journal
@@ -412,9 +413,9 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   if (n > kMaxPackets) return -GPC_EINVAL;
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr);
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr, 0u);
   hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr);
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr, 0u);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
@@ -433,7 +434,9 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   const gpc_pkt_soa* p = &pk;
   uint32_t* orig = nullptr;
   uint2* mid = nullptr;
+  uint32_t xo = 0;
   if (group) {
+    xo = group->xcd_order;
     if (!group->scratch || group->shift > 31) return -GPC_EINVAL;
     uint8_t* q = group->scratch;
     auto take = [&](uint64_t bytes) {
@@ -463,10 +466,10 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
     p = &g;
   }
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
-  if (delta && svc) launch<true, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
-  else if (delta) launch<true, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
-  else if (svc) launch<false, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
-  else launch<false, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, stream);
+  if (delta && svc) launch<true, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  else if (delta) launch<true, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  else if (svc) launch<false, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  else launch<false, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

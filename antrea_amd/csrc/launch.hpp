@@ -35,6 +35,7 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
 struct GroupArgs {
   uint8_t* scratch;
   uint32_t shift;
+  uint32_t xcd_order;  // 1: the blocks of one tile run on one XCD (classify.hip block_xcd_order)
 };
 uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n);
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,

@@ -408,7 +408,8 @@ def main():
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
                    "verdict_mix": mix, "build_s": round(t_build, 1),
                    "packet_grouping": ("nw_src >> %s in 16384-packet tiles" % os.environ.get("GPC_GROUP_SHIFT", "24"))
-                   if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18)) else "off"},
+                   if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18 and st["device_bytes"] >= 4 << 20))
+                   else "off"},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)
         "launches_per_step": 1 if getattr(wl, "services", None) else 2,
         "roofline": roofline,

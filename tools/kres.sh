@@ -1,8 +1,9 @@
 #!/bin/bash
 # Per-kernel resources of classify.hip (compile-time report, CPU only): VGPRs, spills, scratch
 # bytes per lane, LDS bytes, occupancy. Extra hipcc flags (e.g. -DGPC_WAVES_PER_EU=5) pass through.
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I/root/repo/include -I/root/repo/antrea_amd/csrc \
-  "$@" -c /root/repo/antrea_amd/csrc/classify.hip -o /tmp/kres.o -Rpass-analysis=kernel-resource-usage 2>&1 |
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include -I$ROOT/antrea_amd/csrc \
+  "$@" -c $ROOT/antrea_amd/csrc/classify.hip -o /tmp/kres.o -Rpass-analysis=kernel-resource-usage 2>&1 |
   python3 -c '
 import re, sys
 rows, cur = [], None
