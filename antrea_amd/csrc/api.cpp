@@ -51,6 +51,11 @@ static uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t h
   return (*end || x < lo || x > hi) ? dflt : uint32_t(x);
 }
 
+struct StreamScratch {  // device scratch of the packet grouping pre-pass on one stream
+  uint8_t* p = nullptr;
+  size_t bytes = 0;
+};
+
 struct DevImage {  // one uploaded image (freed when the last epoch using it retires)
   ImageHdr* d_hdr = nullptr;
   uint32_t* d_blob = nullptr;
@@ -134,7 +139,7 @@ struct gpc_ctx {
   DevEpoch cur;
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
-  bool pool_kept = false;                // default mem pool release threshold raised (first classify)
+  std::map<hipStream_t, StreamScratch> scratch;  // packet grouping buffers per stream (data)
   uint32_t group_shift = env_u32("GPC_GROUP_SHIFT", 24, 0, 31);  // packet grouping key (classify.hip)
   uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 1, 0, 1);         // XCD-contiguous tiles
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
@@ -429,6 +434,7 @@ void gpc_destroy(gpc_ctx* ctx) {
     ctx->retired.push_back(RetiredEpoch{std::move(ctx->cur)});
     collect_retired(ctx, true);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    for (auto& kv : ctx->scratch) (void)hipFree(kv.second.p);
     if (ctx->ustream) {
       (void)hipStreamSynchronize(ctx->ustream);
       (void)hipStreamDestroy(ctx->ustream);
@@ -736,6 +742,7 @@ int gpc_replay(gpc_ctx* ctx) {
   }
   DevEpoch old;
   unsigned long long* old_counters = nullptr;
+  std::map<hipStream_t, StreamScratch> old_scratch;
   {
     std::lock_guard<std::mutex> d(ctx->data);
     old = std::move(ctx->cur);
@@ -743,7 +750,9 @@ int gpc_replay(gpc_ctx* ctx) {
     old_counters = ctx->d_counters;
     ctx->d_counters = nullptr;
     ctx->launch_epoch.clear();
+    old_scratch.swap(ctx->scratch);
   }
+  for (auto& kv : old_scratch) (void)hipFree(kv.second.p);
   ctx->retired.push_back(RetiredEpoch{std::move(old)});
   collect_retired(ctx, true);
   if (old_counters) (void)hipFree(old_counters);
@@ -813,25 +822,26 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
                {ctx->cur.base->sort_table[0], ctx->cur.base->sort_table[1]},
                uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  // packet grouping (classify.hip group_*): scratch allocated and freed stream-ordered on the
-  // caller's stream, so concurrent callers on other streams never share it
+  // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
+  // the next batch on that stream (launches of one stream run in order), so callers on different
+  // streams never share one and the data path does no allocation once warm
   const int gm = ctx->cfg.group_packets;
-  if (!ctx->pool_kept) {  // freed stream-ordered allocations (grouping scratch, epochs) stay pooled for reuse
-    hipMemPool_t pool;
-    uint64_t keep = UINT64_MAX;
-    if (hipDeviceGetDefaultMemPool(&pool, ctx->cfg.device) == hipSuccess)
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    (void)hipGetLastError();
-    ctx->pool_kept = true;
-  }
   GroupArgs ga{nullptr, ctx->group_shift, ctx->group_xcd};
   const bool auto_group = n >= kGroupMinPackets && ctx->cur.base->bytes >= kGroupMinImageBytes;
-  if (n && (gm > 0 || (gm == 0 && auto_group)) &&
-      hip_ok(dev_alloc((void**)&ga.scratch, group_scratch_bytes(*pk, n), st)))
-    return -GPC_ENOMEM;
+  if (n && (gm > 0 || (gm == 0 && auto_group))) {
+    const size_t need = group_scratch_bytes(*pk, n);
+    StreamScratch& sc = ctx->scratch[st];
+    if (sc.bytes < need) {
+      dev_free(sc.p, st);  // after the launches already queued on st
+      sc.p = nullptr;
+      sc.bytes = 0;
+      if (hip_ok(hipMalloc((void**)&sc.p, need))) return -GPC_ENOMEM;
+      sc.bytes = need;
+    }
+    ga.scratch = sc.p;
+  }
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
                            ga.scratch ? &ga : nullptr, st);
-  if (ga.scratch) dev_free(ga.scratch, st);
   if (rc || n == 0) return rc;
   ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained

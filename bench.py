@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -117,7 +118,7 @@ def _pmc_pass(counters, args):
     if not shutil.which("rocprofv3"):
         return None
     d = tempfile.mkdtemp(prefix="gpc_pmc_")
-    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel", "-d", d, "-o", "pmc",
+    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel|group_tiles", "-d", d, "-o", "pmc",
                                                        "--output-format", "csv", "--", sys.executable,
                                                        os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
                                                        "--no-cpu-baseline", "--no-traffic", "--no-parity", "--config",
@@ -130,14 +131,17 @@ def _pmc_pass(counters, args):
         rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
-                rows += [r for r in csv.DictReader(fh) if "classify_kernel" in r.get("Kernel_Name", "")]
-        # one step = two launches without Services (egress stage, ingress stage), one with them
-        per_step = 1.0 if args.config == "C4" else 2.0
+                rows += [r for r in csv.DictReader(fh)
+                         if "classify_kernel" in r.get("Kernel_Name", "") or "group_tiles" in r.get("Kernel_Name", "")]
+        # one step = the grouping launch (if grouped) + two classify launches without Services
+        # (egress stage, ingress stage) or one with them: steps = dispatches of the first classify stage
+        first = [r for r in rows if re.search(r"classify_kernel<\w+, \w+, [01],", r.get("Kernel_Name", ""))]
+        steps = len({r.get("Dispatch_Id") for r in first}) or 1
         out, by_kernel = {}, {}
         for c in counters:
             vals = [float(r["Counter_Value"]) for r in rows if r.get("Counter_Name") == c]
             if vals:
-                out[c] = sum(vals) / (len(vals) / per_step)
+                out[c] = sum(vals) / steps
             for r in rows:
                 if r.get("Counter_Name") != c:
                     continue
@@ -174,7 +178,7 @@ def _roofline(pmc, kern_ms, n, b_in, b_out, lbar):
     pps_kernel = n / (kern_ms / 1e3)
     b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
     rl = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-          "basis": "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per step (2 launches w/o Services) / HIP-event kernel time"}
+          "basis": "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per step (grouping + classify launches) / HIP-event kernel time"}
     f, w = pmc.get("FETCH_SIZE"), pmc.get("WRITE_SIZE")
     if f is not None and w is not None:
         traffic = (2.0 * f + w) * 1024.0  # counters are in KB
