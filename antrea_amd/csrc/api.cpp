@@ -140,7 +140,7 @@ struct gpc_ctx {
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
   std::map<hipStream_t, StreamScratch> scratch;  // packet grouping buffers per stream (data)
-  uint32_t group_shift = env_u32("GPC_GROUP_SHIFT", 24, 0, 31);  // packet grouping key (classify.hip)
+  uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // packet grouping key (classify.hip)
   uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 1, 0, 1);         // XCD-contiguous tiles
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;
@@ -826,7 +826,7 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   // the next batch on that stream (launches of one stream run in order), so callers on different
   // streams never share one and the data path does no allocation once warm
   const int gm = ctx->cfg.group_packets;
-  GroupArgs ga{nullptr, ctx->group_shift, ctx->group_xcd};
+  GroupArgs ga{nullptr, ctx->group_src_bits, ctx->group_xcd};
   const bool auto_group = n >= kGroupMinPackets && ctx->cur.base->bytes >= kGroupMinImageBytes;
   if (n && (gm > 0 || (gm == 0 && auto_group))) {
     const size_t need = group_scratch_bytes(*pk, n);

@@ -115,7 +115,7 @@ __device__ __forceinline__ uint64_t sorted_index(const EpochArgs& ep, const gpc_
 // Packet grouping. Lanes of a wavefront that classify packets of one address
 // region share driver buckets, candidate lists and rule records, so their loads coalesce and their
 // scans run the same length. For a grouped batch a first launch rewrites every tile of kGroupTile
-// packets in the order of (nw_src >> shift) & 255 (a counting sort in LDS, then every present
+// packets in the order of group_key (top bits of nw_src, then of nw_dst; a counting sort in LDS, then every present
 // column staged through LDS: coalesced reads and writes) and records each grouped packet's caller
 // index. The egress launch leaves its verdict in mid[] (grouped order); the ingress launch (or the
 // single Service launch) stores the verdict pair / LB result at the caller index. The blocks of
@@ -134,18 +134,29 @@ __device__ __forceinline__ void group_column(const T* __restrict__ in, T* __rest
   for (uint32_t k = threadIdx.x; k < m; k += kGroupThreads) outc[base + k] = buf[from[k]];
 }
 
-__global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa in, uint64_t n, uint32_t shift,
+// Grouping key of a packet: the top src_bits of nw_src followed by the top 8 - src_bits of nw_dst.
+__device__ __forceinline__ uint32_t group_key(uint32_t src, uint32_t dst, uint32_t src_bits) {
+  const uint32_t db = 8u - src_bits;
+  const uint32_t hi = src_bits ? (src >> (32u - src_bits)) << db : 0u;
+  return hi | (db ? dst >> (32u - db) : 0u);
+}
+
+__global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa in, uint64_t n, uint32_t src_bits,
                                                                     gpc_pkt_soa g, uint32_t* __restrict__ orig) {
-  __shared__ uint32_t stage[kGroupTile];  // one column of the tile
+  __shared__ uint32_t stage[kGroupTile];  // the tile's keys, then one column of the tile
   __shared__ uint16_t from[kGroupTile];   // grouped position -> tile position
   __shared__ uint32_t cur[kGroupBins];
   const uint32_t tid = threadIdx.x;
   const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
   const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
   if (tid < kGroupBins) cur[tid] = 0;
-  for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = in.src[base + j];
+  if (src_bits == 8u) {
+    for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = in.src[base + j] >> 24;
+  } else {
+    for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = group_key(in.src[base + j], in.dst[base + j], src_bits);
+  }
   __syncthreads();
-  for (uint32_t j = tid; j < m; j += kGroupThreads) atomicAdd(&cur[(stage[j] >> shift) & (kGroupBins - 1)], 1u);
+  for (uint32_t j = tid; j < m; j += kGroupThreads) atomicAdd(&cur[stage[j]], 1u);
   __syncthreads();
   if (tid < 64) {  // exclusive prefix over the 256 bins: one wavefront, 4 bins per lane
     const uint32_t c0 = cur[4 * tid], c1 = cur[4 * tid + 1], c2 = cur[4 * tid + 2], c3 = cur[4 * tid + 3];
@@ -163,17 +174,12 @@ __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa 
     cur[4 * tid + 3] = e + c0 + c1 + c2;
   }
   __syncthreads();
-  for (uint32_t j = tid; j < m; j += kGroupThreads)
-    from[atomicAdd(&cur[(stage[j] >> shift) & (kGroupBins - 1)], 1u)] = uint16_t(j);
+  for (uint32_t j = tid; j < m; j += kGroupThreads) from[atomicAdd(&cur[stage[j]], 1u)] = uint16_t(j);
   __syncthreads();
-  uint32_t* gsrc = const_cast<uint32_t*>(g.src);
-  for (uint32_t k = tid; k < m; k += kGroupThreads) {
-    const uint32_t j = from[k];
-    gsrc[base + k] = stage[j];
-    orig[base + k] = uint32_t(base + j);
-  }
+  for (uint32_t k = tid; k < m; k += kGroupThreads) orig[base + k] = uint32_t(base + from[k]);
 #define GPC_GROUP_COL(c, T) \
   if (in.c) group_column<T>(in.c, const_cast<T*>(g.c), base, m, from, stage)
+  GPC_GROUP_COL(src, uint32_t);
   GPC_GROUP_COL(dst, uint32_t);
   GPC_GROUP_COL(sport, uint16_t);
   GPC_GROUP_COL(dport, uint16_t);
@@ -437,7 +443,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   uint32_t xo = 0;
   if (group) {
     xo = group->xcd_order;
-    if (!group->scratch || group->shift > 31) return -GPC_EINVAL;
+    if (!group->scratch || group->src_bits > 8) return -GPC_EINVAL;
     uint8_t* q = group->scratch;
     auto take = [&](uint64_t bytes) {
       uint8_t* r = q;
@@ -462,7 +468,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
     if (pk.len) g.len = reinterpret_cast<const uint16_t*>(take(2 * n));
     if (pk.ct_mark) g.ct_mark = take(n);
     const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
-    hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, pk, n, group->shift, g, orig);
+    hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, pk, n, group->src_bits, g, orig);
     p = &g;
   }
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;

@@ -411,7 +411,8 @@ def main():
                    "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
                    "verdict_mix": mix, "build_s": round(t_build, 1),
-                   "packet_grouping": ("nw_src >> %s in 16384-packet tiles" % os.environ.get("GPC_GROUP_SHIFT", "24"))
+                   "packet_grouping": ("key: top %s bits of nw_src + %d of nw_dst, 16384-packet tiles" % (
+                       os.environ.get("GPC_GROUP_SRC_BITS", "8"), 8 - int(os.environ.get("GPC_GROUP_SRC_BITS", "8"))))
                    if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18 and st["device_bytes"] >= 4 << 20))
                    else "off"},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)

@@ -65,10 +65,17 @@ def main():
         elif name.startswith("sort_"):  # sort_src / sort_dst, or sort_src16: stable sort on the top 16 bits
             col, bits = name[5:8], int(name[8:] or 32)
             perm = torch.argsort((base[col].to(torch.int64) & 0xFFFFFFFF) >> (32 - bits), stable=True)
-        elif name.startswith("tile"):  # tile<T>_src<bits>: stable sort inside tiles of T packets
+        elif name.startswith("tile"):  # tile<T>_<key>: stable sort inside tiles of T packets
             t, rest = name[4:].split("_")
-            col, bits = rest[:3], int(rest[3:])
-            key = (base[col].to(torch.int64) & 0xFFFFFFFF) >> (32 - bits)
+            u = lambda c: base[c].to(torch.int64) & 0xFFFFFFFF
+            keys = {"out": lambda: u("out_port") & 255, "s4o4": lambda: ((u("src") >> 28) << 4) | (u("out_port") & 15),
+                    "s4d4": lambda: ((u("src") >> 28) << 4) | (u("dst") >> 28),
+                    "proto": lambda: (u("proto") & 255), "s6p2": lambda: ((u("src") >> 26) << 2) | (u("proto") & 3)}
+            if rest in keys:
+                key, bits = keys[rest](), 8
+            else:
+                col, bits = rest[:3], int(rest[3:])
+                key = u(col) >> (32 - bits)
             tile_id = torch.arange(len(key), device=key.device) // int(t)
             perm = torch.argsort((tile_id << bits) | key, stable=True)
         elif name.startswith("xcd_"):
