@@ -812,7 +812,7 @@ int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out
 
 int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, gpc_lb_result* lb_out, int32_t count,
                     void* stream) {
-  if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
+  if (!ctx || !pk || (!out && n) || n > GPC_MAX_BATCH) return -GPC_EINVAL;
   if (n && (!pk->src || !pk->dst || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
   if (!ctx->cur.base) return -GPC_EINVAL;  // nothing committed yet

@@ -412,6 +412,7 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
 // Launch size: the grid is limited in work-items (gridDim.x * blockDim.x < 2^32 on ROCm), and the
 // lane-regrouping kernels use 256-thread blocks.
 constexpr uint64_t kMaxPackets = (1ull << 32) - uint64_t(kSortBlock);
+static_assert(kMaxPackets == GPC_MAX_BATCH, "gpc.h GPC_MAX_BATCH mirrors the launch limit");
 
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
                      unsigned long long* counters, int count, hipStream_t stream) {

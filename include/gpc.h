@@ -387,7 +387,10 @@ int gpc_compact(gpc_ctx* ctx);
  * epoch from the host shadow state (after a device reset); flows, conj ids and counter slots are
  * unchanged, device counters restart from zero. */
 int gpc_replay(gpc_ctx* ctx);
+/* Largest batch of one gpc_classify* call (the launch grid is limited to 2^32 work-items). */
+#define GPC_MAX_BATCH (4294967296ull - 256ull)
 /* Classify n packets whose columns are DEVICE pointers; writes 2*n verdicts (device pointer).
+ * n > GPC_MAX_BATCH: -GPC_EINVAL, nothing launched.
  * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t. */
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
 /* gpc_classify plus the AntreaProxy stage in front of the policy tables: packets to a Service

@@ -109,3 +109,23 @@ def test_grouped_device_stream_batch():
         outs.append((out.cpu(), _metrics(c)))
     assert torch.equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
+
+
+def test_batch_over_launch_limit_is_einval():
+    """n > GPC_MAX_BATCH (2^32 - 256) is rejected with -GPC_EINVAL before any allocation or launch
+    (the grouping scratch for such a batch would not be allocated either)."""
+    import ctypes as C
+    import torch
+    wl = workload.config3(n_policies_per_dir=5, rules_per_policy=10)
+    c = gpc.Classifier(group_packets=1)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    c.commit()
+    cols = workload.gen_packets_torch(wl, 256, device="cuda")
+    out = torch.zeros(2 * 256 * 8, dtype=torch.uint8, device="cuda")
+    soa = gpc.pkt_soa_device(cols)
+    for n in ((1 << 32) - 255, 1 << 32, (1 << 40)):
+        rc = c.lib.gpc_classify(c.h, C.byref(soa), C.c_size_t(n), C.c_void_p(out.data_ptr()), 0, None)
+        assert rc == -gpc.GPC_EINVAL, (n, rc)
+    c.classify_device(soa, 256, out.data_ptr(), count=False, stream=0)
+    torch.cuda.synchronize()
