@@ -54,7 +54,9 @@ static uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t h
 struct StreamScratch {  // device scratch of the packet grouping pre-pass on one stream
   uint8_t* p = nullptr;
   size_t bytes = 0;
+  hipEvent_t done = nullptr;  // recorded after the last launch that used it
 };
+constexpr size_t kScratchStreams = 8;  // idle buffers of other streams are released past this many
 
 struct DevImage {  // one uploaded image (freed when the last epoch using it retires)
   ImageHdr* d_hdr = nullptr;
@@ -434,7 +436,10 @@ void gpc_destroy(gpc_ctx* ctx) {
     ctx->retired.push_back(RetiredEpoch{std::move(ctx->cur)});
     collect_retired(ctx, true);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
-    for (auto& kv : ctx->scratch) (void)hipFree(kv.second.p);
+    for (auto& kv : ctx->scratch) {
+      (void)hipFree(kv.second.p);
+      if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+    }
     if (ctx->ustream) {
       (void)hipStreamSynchronize(ctx->ustream);
       (void)hipStreamDestroy(ctx->ustream);
@@ -752,7 +757,10 @@ int gpc_replay(gpc_ctx* ctx) {
     ctx->launch_epoch.clear();
     old_scratch.swap(ctx->scratch);
   }
-  for (auto& kv : old_scratch) (void)hipFree(kv.second.p);
+  for (auto& kv : old_scratch) {
+    (void)hipFree(kv.second.p);
+    if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+  }
   ctx->retired.push_back(RetiredEpoch{std::move(old)});
   collect_retired(ctx, true);
   if (old_counters) (void)hipFree(old_counters);
@@ -830,6 +838,18 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   const bool auto_group = n >= kGroupMinPackets && ctx->cur.base->bytes >= kGroupMinImageBytes;
   if (n && (gm > 0 || (gm == 0 && auto_group))) {
     const size_t need = group_scratch_bytes(*pk, n);
+    if (ctx->scratch.size() >= kScratchStreams && !ctx->scratch.count(st)) {
+      for (auto it = ctx->scratch.begin(); it != ctx->scratch.end();) {  // streams whose last batch is done
+        if (!it->second.done || hipEventQuery(it->second.done) == hipSuccess) {
+          (void)hipFree(it->second.p);
+          if (it->second.done) (void)hipEventDestroy(it->second.done);
+          it = ctx->scratch.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      (void)hipGetLastError();
+    }
     StreamScratch& sc = ctx->scratch[st];
     if (sc.bytes < need) {
       dev_free(sc.p, st);  // after the launches already queued on st
@@ -842,6 +862,11 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   }
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
                            ga.scratch ? &ga : nullptr, st);
+  if (!rc && ga.scratch) {
+    StreamScratch& sc = ctx->scratch[st];
+    if (!sc.done && hip_ok(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming))) return -GPC_EDEV;
+    rc = hip_ok(hipEventRecord(sc.done, st));
+  }
   if (rc || n == 0) return rc;
   ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained

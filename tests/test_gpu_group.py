@@ -129,3 +129,33 @@ def test_batch_over_launch_limit_is_einval():
         assert rc == -gpc.GPC_EINVAL, (n, rc)
     c.classify_device(soa, 256, out.data_ptr(), count=False, stream=0)
     torch.cuda.synchronize()
+
+
+def test_grouped_many_streams():
+    """Grouped batches on more streams than the scratch cache keeps (8): idle buffers of finished
+    streams are released, results stay identical to the plain launch."""
+    import torch
+    wl = workload.config1(seed=21)
+    n = 20_000
+    cols = workload.gen_packets_torch(wl, n, device="cuda")
+    soa = gpc.pkt_soa_device(cols)
+    ref = torch.zeros(2 * n * 8, dtype=torch.uint8, device="cuda")
+    plain = gpc.Classifier(group_packets=-1)
+    grouped = gpc.Classifier(group_packets=1)
+    for c in (plain, grouped):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+        c.commit()
+    plain.classify_device(soa, n, ref.data_ptr(), stream=0)
+    torch.cuda.synchronize()
+    outs = []
+    for k in range(12):
+        s = torch.cuda.Stream()
+        o = torch.zeros_like(ref)
+        grouped.classify_device(soa, n, o.data_ptr(), stream=s.cuda_stream)
+        outs.append((s, o))
+        if k % 3 == 2:
+            s.synchronize()
+    torch.cuda.synchronize()
+    for s, o in outs:
+        assert torch.equal(o, ref)
