@@ -29,18 +29,38 @@ sys.path.insert(0, ROOT)
 from antrea_amd import workload  # noqa: E402
 from oracle import parity  # noqa: E402
 
-SPECS = {  # config -> (packets, packet seed)
+SPECS = {  # config -> (packets, packet seed); "x": the workload with every optional packet column set
     "C1": (100_000, 0xF1C1),
     "C2": (100_000, 0xF1C2),
     "C3": (100_000, 0xF1C3),
     "C4": (100_000, 0xF1C4),
+    "C3x": (100_000, 0xF1C5),
 }
 COLS = ("src", "dst", "sport", "dport", "proto", "out_port", "len")
+OPT_COLS = ("in_port", "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "ct_mark", "svc_group")
+
+
+def optional_columns(cols, seed):
+    """Every optional column of gpc_pkt_soa, seeded: conntrack states (new / est / rel / reply, the
+    64990 skip flows and the DNS +rpl flow), pre-NAT addresses, IngressSecurityClassifier
+    destinations (Pod / gateway / tunnel / uplink) and the hairpin ct_mark, in_port, tun_id, reg7."""
+    rng = np.random.default_rng(seed)
+    n = len(cols["src"])
+    out = dict(cols)
+    out["in_port"] = rng.integers(0, 200, n).astype(np.uint32)
+    out["tun_id"] = rng.integers(0, 4, n).astype(np.uint32)
+    out["ct_src"] = np.where(rng.random(n) < 0.9, cols["src"], rng.integers(0, 1 << 32, n)).astype(np.uint32)
+    out["ct_dst"] = np.where(rng.random(n) < 0.9, cols["dst"], rng.integers(0, 1 << 32, n)).astype(np.uint32)
+    out["ct_state"] = rng.choice([0x21, 0x22, 0x24, 0x2a, 0x29], size=n, p=[0.75, 0.1, 0.05, 0.05, 0.05]).astype(np.uint8)
+    out["dest"] = rng.choice(4, size=n, p=[0.85, 0.05, 0.05, 0.05]).astype(np.uint8)
+    out["ct_mark"] = np.where(rng.random(n) < 0.05, 0x40, 0).astype(np.uint8)
+    out["svc_group"] = np.where(rng.random(n) < 0.1, rng.integers(1, 50, n), 0).astype(np.uint32)
+    return out
 
 
 def cols_digest(cols) -> str:
     h = hashlib.sha256()
-    for k in COLS:
+    for k in COLS + tuple(c for c in OPT_COLS if c in cols):
         h.update(k.encode())
         h.update(np.ascontiguousarray(cols[k]).tobytes())
     return h.hexdigest()
@@ -56,8 +76,9 @@ def path(config: str) -> str:
 
 def packets(config: str, wl=None):
     n, seed = SPECS[config]
-    wl = wl or workload.CONFIGS[config]()
-    return wl, workload.gen_packets(wl, n, seed=seed)
+    wl = wl or workload.CONFIGS[config.rstrip("x")]()
+    cols = workload.gen_packets(wl, n, seed=seed)
+    return wl, optional_columns(cols, seed) if config.endswith("x") else cols
 
 
 def make(config: str):

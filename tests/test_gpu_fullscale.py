@@ -50,12 +50,13 @@ def _nonzero(m):
 
 
 @pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
-@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4"])
+@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4", "C3x"])
 def test_device_vs_oracle_fullscale(config, group):
     """Verdicts (conj id, action, table, tier, flags) and NetworkPolicyMetrics of 100k packets at
     full scale equal the C oracle's exactly (C4: the packets that hit no Service, with the Service
-    stage live in the kernel), with the packet grouping pre-pass off and on (the bench's 64M-packet
-    batches are grouped)."""
+    stage live in the kernel; C3x: C3 with every optional column set -- conntrack states, pre-NAT
+    addresses, IngressSecurityClassifier destinations and hairpin mark, in_port, tun_id, reg7),
+    with the packet grouping pre-pass off and on (the bench's 64M-packet batches are grouped)."""
     f, wl, cols = _inputs(config)
     mask = f["mask"].astype(bool)
     sub = cols if mask.all() else {k: v[mask] for k, v in cols.items()}

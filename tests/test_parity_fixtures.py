@@ -18,7 +18,7 @@ from tests import emu
 from tests.golden import make_parity_fixtures as fx
 
 
-@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4"])
+@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4", "C3x"])
 def test_fixture_inputs_stable(config):
     f = fx.load(config)
     wl, cols = fx.packets(config)
@@ -27,7 +27,7 @@ def test_fixture_inputs_stable(config):
     assert f["verdicts"].shape == (len(cols["src"]), 2)
 
 
-@pytest.mark.parametrize("config", ["C2", "C3"])
+@pytest.mark.parametrize("config", ["C2", "C3", "C3x"])
 def test_emu_vs_oracle_fixture(config):
     f = fx.load(config)
     wl, cols = fx.packets(config)
