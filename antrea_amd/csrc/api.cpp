@@ -58,6 +58,17 @@ struct StreamScratch {  // device scratch of the packet grouping pre-pass on one
 };
 constexpr size_t kScratchStreams = 8;  // idle buffers of other streams are released past this many
 
+// IPv6 grouping key: the 8 address bits just above the shortest prefix length of the image's prefix
+// tree (the bits in which its shortest prefixes differ; fd00:10::/96 embedding: the embedded IPv4
+// address's top byte).
+static int32_t v6_group_bit(const HostImage& h) {
+  if (!h.hdr.v6_lpm || h.blob.size() * 4 < size_t(h.hdr.v6_lpm) * 4 + sizeof(V6Lpm)) return 0;
+  const V6Lpm* L = reinterpret_cast<const V6Lpm*>(h.blob.data() + h.hdr.v6_lpm);
+  const int32_t shortest = L->n_lens ? int32_t(L->lens[0]) : 8;
+  return std::min<int32_t>(120, std::max<int32_t>(0, shortest - 8));
+}
+
+
 struct DevImage {  // one uploaded image (freed when the last epoch using it retires)
   ImageHdr* d_hdr = nullptr;
   uint32_t* d_blob = nullptr;
@@ -77,6 +88,7 @@ struct DevEpoch {
   std::shared_ptr<DevImage> svc;        // Service image (d_hdr unused), shared until Services change
   std::shared_ptr<DevImage> v6;         // IPv6 image (ipv6_enabled), shared until rules change
   uint32_t v6_lpm = 0;                  // its ImageHdr.v6_lpm
+  int32_t v6_bit = 0;                   // grouping key of IPv6 batches (v6_group_bit)
   uint64_t epoch = 0;
   std::map<hipStream_t, hipEvent_t> last_use;  // last launch on each stream that used this epoch
 };
@@ -785,6 +797,7 @@ int gpc_replay(gpc_ctx* ctx) {
   if (!rc && !ctx->last6.blob.empty()) {
     rc = upload_image(ctx->last6, us, &ne.v6);
     ne.v6_lpm = ctx->last6.hdr.v6_lpm;
+    ne.v6_bit = v6_group_bit(ctx->last6);
   }
   if (!rc && !ctx->svc_blob.empty()) rc = upload_words(ctx->svc_blob, us, &ne.svc);
   const size_t cap = std::max<size_t>(1, ctx->slots.size());
@@ -814,6 +827,44 @@ int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
 constexpr size_t kGroupMinPackets = size_t(1) << 18;
 constexpr size_t kGroupMinImageBytes = size_t(4) << 20;
 
+// Grouping scratch of stream st with at least `need` bytes (ctx->data held).
+static int group_scratch(gpc_ctx* ctx, hipStream_t st, size_t need, uint8_t** out) {
+  if (ctx->scratch.size() >= kScratchStreams && !ctx->scratch.count(st)) {
+    for (auto it = ctx->scratch.begin(); it != ctx->scratch.end();) {  // streams whose last batch is done
+      if (!it->second.done || hipEventQuery(it->second.done) == hipSuccess) {
+        (void)hipFree(it->second.p);
+        if (it->second.done) (void)hipEventDestroy(it->second.done);
+        it = ctx->scratch.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    (void)hipGetLastError();
+  }
+  StreamScratch& sc = ctx->scratch[st];
+  if (sc.bytes < need) {
+    dev_free(sc.p, st);  // after the launches already queued on st
+    sc.p = nullptr;
+    sc.bytes = 0;
+    if (hip_ok(hipMalloc((void**)&sc.p, need))) return -GPC_ENOMEM;
+    sc.bytes = need;
+  }
+  *out = sc.p;
+  return GPC_OK;
+}
+
+// The grouping scratch of stream st is in use until the launches just queued there have run.
+static int group_scratch_used(gpc_ctx* ctx, hipStream_t st) {
+  StreamScratch& sc = ctx->scratch[st];
+  if (!sc.done && hip_ok(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming))) return -GPC_EDEV;
+  return hip_ok(hipEventRecord(sc.done, st));
+}
+
+static bool group_batch(const gpc_ctx* ctx, size_t n, size_t image_bytes) {
+  const int gm = ctx->cfg.group_packets;
+  return n && (gm > 0 || (gm == 0 && n >= kGroupMinPackets && image_bytes >= kGroupMinImageBytes));
+}
+
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
   return gpc_classify_lb(ctx, pk, n, out, nullptr, count, stream);
 }
@@ -833,40 +884,12 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
   // the next batch on that stream (launches of one stream run in order), so callers on different
   // streams never share one and the data path does no allocation once warm
-  const int gm = ctx->cfg.group_packets;
-  GroupArgs ga{nullptr, ctx->group_src_bits, ctx->group_xcd};
-  const bool auto_group = n >= kGroupMinPackets && ctx->cur.base->bytes >= kGroupMinImageBytes;
-  if (n && (gm > 0 || (gm == 0 && auto_group))) {
-    const size_t need = group_scratch_bytes(*pk, n);
-    if (ctx->scratch.size() >= kScratchStreams && !ctx->scratch.count(st)) {
-      for (auto it = ctx->scratch.begin(); it != ctx->scratch.end();) {  // streams whose last batch is done
-        if (!it->second.done || hipEventQuery(it->second.done) == hipSuccess) {
-          (void)hipFree(it->second.p);
-          if (it->second.done) (void)hipEventDestroy(it->second.done);
-          it = ctx->scratch.erase(it);
-        } else {
-          ++it;
-        }
-      }
-      (void)hipGetLastError();
-    }
-    StreamScratch& sc = ctx->scratch[st];
-    if (sc.bytes < need) {
-      dev_free(sc.p, st);  // after the launches already queued on st
-      sc.p = nullptr;
-      sc.bytes = 0;
-      if (hip_ok(hipMalloc((void**)&sc.p, need))) return -GPC_ENOMEM;
-      sc.bytes = need;
-    }
-    ga.scratch = sc.p;
-  }
+  GroupArgs ga{nullptr, ctx->group_src_bits, ctx->group_xcd, 0};
+  if (group_batch(ctx, n, ctx->cur.base->bytes))
+    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n), &ga.scratch)) return e;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
                            ga.scratch ? &ga : nullptr, st);
-  if (!rc && ga.scratch) {
-    StreamScratch& sc = ctx->scratch[st];
-    if (!sc.done && hip_ok(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming))) return -GPC_EDEV;
-    rc = hip_ok(hipEventRecord(sc.done, st));
-  }
+  if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
   if (rc || n == 0) return rc;
   ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained
@@ -937,7 +960,7 @@ int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict
 }
 
 int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
-  if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
+  if (!ctx || !pk || (!out && n) || n > GPC_MAX_BATCH) return -GPC_EINVAL;
   if (n && (!pk->src6 || !pk->dst6 || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
   for (const void* c : {(const void*)pk->src6, (const void*)pk->dst6, (const void*)pk->ct_src6, (const void*)pk->ct_dst6})
     if (reinterpret_cast<uintptr_t>(c) % 16) return -GPC_EINVAL;  // one 128-bit load per address
@@ -947,7 +970,11 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm, {0, 0},
                uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, st);
+  GroupArgs ga{nullptr, 8u, ctx->group_xcd, ctx->cur.v6_bit};
+  if (group_batch(ctx, n, ctx->cur.v6->bytes))
+    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n), &ga.scratch)) return e;
+  int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st);
+  if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
   if (rc || n == 0) return rc;
   ctx->launch_epoch[st] = ctx->cur.epoch;
   hipEvent_t& ev = ctx->cur.last_use[st];
@@ -1342,9 +1369,11 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   if (!v6_changed) {
     ne.v6 = ctx->cur.v6;
     ne.v6_lpm = ctx->cur.v6_lpm;
+    ne.v6_bit = ctx->cur.v6_bit;
   } else if (!ctx->last6.blob.empty()) {
     if ((rc = upload_image(ctx->last6, us, &ne.v6))) return rc;
     ne.v6_lpm = ctx->last6.hdr.v6_lpm;
+    ne.v6_bit = v6_group_bit(ctx->last6);
   }
   if (!svc_changed) ne.svc = ctx->cur.svc;
   else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, us, &ne.svc))) return rc;

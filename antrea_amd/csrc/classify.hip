@@ -134,6 +134,26 @@ __device__ __forceinline__ void group_column(const T* __restrict__ in, T* __rest
   for (uint32_t k = threadIdx.x; k < m; k += kGroupThreads) outc[base + k] = buf[from[k]];
 }
 
+// An IPv6 address column (16 network-order bytes per packet) as four word columns.
+__device__ __forceinline__ void group_column16(const uint8_t* __restrict__ in, const uint8_t* outc, uint64_t base, uint32_t m,
+                                               const uint16_t* from, void* stage) {
+  const uint32_t* iw = reinterpret_cast<const uint32_t*>(in);
+  uint32_t* ow = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(outc));
+  uint32_t* buf = reinterpret_cast<uint32_t*>(stage);
+  for (uint32_t w = 0; w < 4; w++) {
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < m; j += kGroupThreads) buf[j] = iw[(base + j) * 4 + w];
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < m; k += kGroupThreads) ow[(base + k) * 4 + w] = buf[from[k]];
+  }
+}
+
+// Grouping key of an IPv6 packet: the 8 bits of ipv6_src from bit `bit` (0 = most significant).
+__device__ __forceinline__ uint32_t group_key6(const uint8_t* a, uint32_t bit) {
+  const uint32_t b0 = a[bit >> 3], b1 = (bit >> 3) < 15u ? a[(bit >> 3) + 1] : 0u;
+  return (((b0 << 8) | b1) >> (8u - (bit & 7u))) & 0xffu;
+}
+
 // Grouping key of a packet: the top src_bits of nw_src followed by the top 8 - src_bits of nw_dst.
 __device__ __forceinline__ uint32_t group_key(uint32_t src, uint32_t dst, uint32_t src_bits) {
   const uint32_t db = 8u - src_bits;
@@ -141,8 +161,10 @@ __device__ __forceinline__ uint32_t group_key(uint32_t src, uint32_t dst, uint32
   return hi | (db ? dst >> (32u - db) : 0u);
 }
 
+// v6_bit >= 0: an IPv6 batch, keyed by 8 bits of ipv6_src from that bit (api.cpp picks the bits
+// just above the shortest prefix of the IPv6 image).
 __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa in, uint64_t n, uint32_t src_bits,
-                                                                    gpc_pkt_soa g, uint32_t* __restrict__ orig) {
+                                                                    int32_t v6_bit, gpc_pkt_soa g, uint32_t* __restrict__ orig) {
   __shared__ uint32_t stage[kGroupTile];  // the tile's keys, then one column of the tile
   __shared__ uint16_t from[kGroupTile];   // grouped position -> tile position
   __shared__ uint32_t cur[kGroupBins];
@@ -150,7 +172,9 @@ __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa 
   const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
   const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
   if (tid < kGroupBins) cur[tid] = 0;
-  if (src_bits == 8u) {
+  if (v6_bit >= 0) {
+    for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = group_key6(in.src6 + (base + j) * 16, uint32_t(v6_bit));
+  } else if (src_bits == 8u) {
     for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = in.src[base + j] >> 24;
   } else {
     for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = group_key(in.src[base + j], in.dst[base + j], src_bits);
@@ -195,6 +219,10 @@ __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa 
   GPC_GROUP_COL(len, uint16_t);
   GPC_GROUP_COL(ct_mark, uint8_t);
 #undef GPC_GROUP_COL
+  if (in.src6) group_column16(in.src6, g.src6, base, m, from, stage);
+  if (in.dst6) group_column16(in.dst6, g.dst6, base, m, from, stage);
+  if (in.ct_src6) group_column16(in.ct_src6, g.ct_src6, base, m, from, stage);
+  if (in.ct_dst6) group_column16(in.ct_dst6, g.ct_dst6, base, m, from, stage);
 }
 
 // Logical block of this workgroup for a grouped batch: workgroups are dispatched round-robin over
@@ -211,8 +239,11 @@ __device__ __forceinline__ uint64_t block_xcd_order() {
 template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = false>
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
-    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
+    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, void* __restrict__ midv,
     uint32_t xcd_order) {
+  // grouped batches: the egress launch's result in grouped order (IPv6: 16 B, the address codes too)
+  uint2* const mid = reinterpret_cast<uint2*>(midv);
+  uint4* const mid6 = reinterpret_cast<uint4*>(midv);
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
   const uint64_t block_base = (xcd_order ? block_xcd_order() : uint64_t(blockIdx.x)) * block_threads<kSort>();
@@ -222,7 +253,9 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   uint32_t src, dst, ct_src, ct_dst;
   uint4 prev = make_uint4(0u, 0u, 0u, 0u);
   if (kStage == 2) {
-    if (orig) {
+    if (orig && kV6) {
+      prev = mid6[i];
+    } else if (orig) {
       const uint2 v = mid[i];
       prev.x = v.x;
       prev.y = v.y;
@@ -304,14 +337,15 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   }
   const VerdictOut e = o.e, g = o.g;
   if (kStage == 2) out[at()] = make_uint4(prev.x, prev.y, g.conj, g.packed);
-  else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
+  else if (kV6 && kStage == 1 && orig) mid6[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
+  else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);
   else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
   else out[at()] = make_uint4(e.conj, e.packed, g.conj, g.packed);  // ingress NONE until the second launch
 }
 
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                   unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, uint32_t xo,
+                   unsigned long long* counters, int count, const uint32_t* orig, void* mid, uint32_t xo,
                    hipStream_t stream) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   uint4* const o = reinterpret_cast<uint4*>(out);
@@ -414,62 +448,91 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
 constexpr uint64_t kMaxPackets = (1ull << 32) - uint64_t(kSortBlock);
 static_assert(kMaxPackets == GPC_MAX_BATCH, "gpc.h GPC_MAX_BATCH mirrors the launch limit");
 
-int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
-                     unsigned long long* counters, int count, hipStream_t stream) {
-  if (n == 0) return 0;
-  if (n > kMaxPackets) return -GPC_EINVAL;
-  const uint64_t blocks = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr, 0u);
-  hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count, nullptr, nullptr, 0u);
-  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
-}
-
 uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n) {
-  uint64_t per = 4 /*src*/ + 4 /*orig*/ + 8 /*mid*/ + 4 + 2 + 2 + 1 + 4;  // + dst sport dport proto out_port
+  const bool v6 = pk.src6 != nullptr;
+  uint64_t per = 4 /*orig*/ + (v6 ? 16 : 8) /*mid*/ + 2 + 2 + 1 + 4;  // + sport dport proto out_port
+  per += v6 ? 32 + (pk.ct_src6 ? 16 : 0) + (pk.ct_dst6 ? 16 : 0) : 8;  // addresses
   per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0) +
          (pk.ct_state ? 1 : 0) + (pk.dest ? 1 : 0) + (pk.len ? 2 : 0) + (pk.ct_mark ? 1 : 0);
-  return per * n + 16 * 256;  // every region 256-B aligned
+  return per * n + 24 * 256;  // every region 256-B aligned
+}
+
+// Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
+static int launch_group(const gpc_pkt_soa& pk, uint64_t n, const GroupArgs& group, hipStream_t stream, gpc_pkt_soa* g,
+                        uint32_t** orig, void** mid) {
+  if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120) return -GPC_EINVAL;
+  const bool v6 = pk.src6 != nullptr;
+  uint8_t* q = group.scratch;
+  auto take = [&](uint64_t bytes) {
+    uint8_t* r = q;
+    q += (bytes + 255) & ~uint64_t(255);
+    return r;
+  };
+  *g = gpc_pkt_soa{};
+  *mid = take((v6 ? 16 : 8) * n);
+  *orig = reinterpret_cast<uint32_t*>(take(4 * n));
+  if (v6) {
+    g->src6 = take(16 * n);
+    g->dst6 = take(16 * n);
+    if (pk.ct_src6) g->ct_src6 = take(16 * n);
+    if (pk.ct_dst6) g->ct_dst6 = take(16 * n);
+  } else {
+    g->src = reinterpret_cast<const uint32_t*>(take(4 * n));
+    g->dst = reinterpret_cast<const uint32_t*>(take(4 * n));
+  }
+  g->sport = reinterpret_cast<const uint16_t*>(take(2 * n));
+  g->dport = reinterpret_cast<const uint16_t*>(take(2 * n));
+  g->proto = take(n);
+  g->out_port = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.in_port) g->in_port = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.svc_group) g->svc_group = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.tun_id) g->tun_id = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.ct_src) g->ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.ct_dst) g->ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.ct_state) g->ct_state = take(n);
+  if (pk.dest) g->dest = take(n);
+  if (pk.len) g->len = reinterpret_cast<const uint16_t*>(take(2 * n));
+  if (pk.ct_mark) g->ct_mark = take(n);
+  const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
+  hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, pk, n, group.src_bits,
+                     v6 ? group.v6_bit : -1, *g, *orig);
+  return 0;
+}
+
+int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
+                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (n > kMaxPackets) return -GPC_EINVAL;
+  gpc_pkt_soa g;
+  const gpc_pkt_soa* p = &pk;
+  uint32_t* orig = nullptr;
+  void* mid = nullptr;
+  uint32_t xo = 0;
+  if (group) {
+    if (const int rc = launch_group(pk, n, *group, stream, &g, &orig, &mid)) return rc;
+    xo = group->xcd_order;
+    p = &g;
+  }
+  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo);
+  hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
+                     reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo);
+  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream) {
   if (n == 0) return 0;
   if (n > kMaxPackets) return -GPC_EINVAL;
-  gpc_pkt_soa g{};
+  gpc_pkt_soa g;
   const gpc_pkt_soa* p = &pk;
   uint32_t* orig = nullptr;
-  uint2* mid = nullptr;
+  void* mid = nullptr;
   uint32_t xo = 0;
   if (group) {
+    if (const int rc = launch_group(pk, n, *group, stream, &g, &orig, &mid)) return rc;
     xo = group->xcd_order;
-    if (!group->scratch || group->src_bits > 8) return -GPC_EINVAL;
-    uint8_t* q = group->scratch;
-    auto take = [&](uint64_t bytes) {
-      uint8_t* r = q;
-      q += (bytes + 255) & ~uint64_t(255);
-      return r;
-    };
-    mid = reinterpret_cast<uint2*>(take(8 * n));
-    orig = reinterpret_cast<uint32_t*>(take(4 * n));
-    g.src = reinterpret_cast<const uint32_t*>(take(4 * n));
-    g.dst = reinterpret_cast<const uint32_t*>(take(4 * n));
-    g.sport = reinterpret_cast<const uint16_t*>(take(2 * n));
-    g.dport = reinterpret_cast<const uint16_t*>(take(2 * n));
-    g.proto = take(n);
-    g.out_port = reinterpret_cast<const uint32_t*>(take(4 * n));
-    if (pk.in_port) g.in_port = reinterpret_cast<const uint32_t*>(take(4 * n));
-    if (pk.svc_group) g.svc_group = reinterpret_cast<const uint32_t*>(take(4 * n));
-    if (pk.tun_id) g.tun_id = reinterpret_cast<const uint32_t*>(take(4 * n));
-    if (pk.ct_src) g.ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
-    if (pk.ct_dst) g.ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
-    if (pk.ct_state) g.ct_state = take(n);
-    if (pk.dest) g.dest = take(n);
-    if (pk.len) g.len = reinterpret_cast<const uint16_t*>(take(2 * n));
-    if (pk.ct_mark) g.ct_mark = take(n);
-    const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
-    hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, pk, n, group->src_bits, g, orig);
     p = &g;
   }
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;

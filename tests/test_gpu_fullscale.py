@@ -70,11 +70,13 @@ def test_device_vs_oracle_fullscale(config, group):
     assert {1, 2} <= acts and (3 in acts or 5 in acts), acts
 
 
-def test_device_ipv6_vs_oracle_fullscale_c3():
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
+def test_device_ipv6_vs_oracle_fullscale_c3(group):
     """gpc_classify6 on full C3 embedded in fd00:10::/96 (IPv6 image, device LPM) equals the C
-    oracle's IPv4 verdicts of the same packets (the embedding preserves every match)."""
+    oracle's IPv4 verdicts of the same packets (the embedding preserves every match), with the
+    grouping pre-pass off and on (IPv6 key: the 8 ipv6_src bits above the shortest prefix)."""
     f, wl, cols = _inputs("C3")
-    c = _classifier(wl, ipv6=True, rules=workload.to_ipv6(wl).rules)
+    c = _classifier(wl, ipv6=True, rules=workload.to_ipv6(wl).rules, group=group)
     got = c.classify6_host(workload.packets_to_v6(cols), count=True)
     res = parity.compare(got, f["verdicts"])
     assert res["mismatches"] == 0, res

@@ -159,3 +159,22 @@ def test_grouped_many_streams():
     torch.cuda.synchronize()
     for s, o in outs:
         assert torch.equal(o, ref)
+
+
+@pytest.mark.parametrize("n", [1, 8191, 8193, 3 * 8192 + 5])
+def test_grouped_ipv6_equals_plain(n):
+    """IPv6 batches (gpc_classify6): grouped == plain, verdicts and counters, with ct_*6 columns."""
+    wl = workload.config1(seed=9)
+    w6 = workload.to_ipv6(wl, dual=True)
+    rng = np.random.default_rng(n)
+    cols = workload.packets_to_v6(workload.gen_packets(wl, n, seed=9))
+    cols["ct_src6"] = np.ascontiguousarray(np.where((rng.random(n) < 0.9)[:, None], cols["src6"], cols["dst6"]))
+    res = []
+    for g in (-1, 1):
+        c = gpc.Classifier(ipv4=True, ipv6=True, group_packets=g)
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(w6.rules))
+        c.commit()
+        res.append((c.classify6_host(cols, count=True), _metrics(c)))
+    assert (res[0][0] == res[1][0]).all()
+    assert res[0][1] == res[1][1]
