@@ -886,7 +886,7 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   // streams never share one and the data path does no allocation once warm
   GroupArgs ga{nullptr, ctx->group_src_bits, ctx->group_xcd, 0};
   if (group_batch(ctx, n, ctx->cur.base->bytes))
-    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n), &ga.scratch)) return e;
+    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, false), &ga.scratch)) return e;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
                            ga.scratch ? &ga : nullptr, st);
   if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
@@ -972,7 +972,7 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   hipStream_t st = (hipStream_t)stream;
   GroupArgs ga{nullptr, 8u, ctx->group_xcd, ctx->cur.v6_bit};
   if (group_batch(ctx, n, ctx->cur.v6->bytes))
-    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n), &ga.scratch)) return e;
+    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
   int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st);
   if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
   if (rc || n == 0) return rc;

@@ -448,20 +448,18 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
 constexpr uint64_t kMaxPackets = (1ull << 32) - uint64_t(kSortBlock);
 static_assert(kMaxPackets == GPC_MAX_BATCH, "gpc.h GPC_MAX_BATCH mirrors the launch limit");
 
-uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n) {
-  const bool v6 = pk.src6 != nullptr;
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6) {
   uint64_t per = 4 /*orig*/ + (v6 ? 16 : 8) /*mid*/ + 2 + 2 + 1 + 4;  // + sport dport proto out_port
-  per += v6 ? 32 + (pk.ct_src6 ? 16 : 0) + (pk.ct_dst6 ? 16 : 0) : 8;  // addresses
-  per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0) +
+  per += v6 ? 32 + (pk.ct_src6 ? 16 : 0) + (pk.ct_dst6 ? 16 : 0) : 8 + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0);
+  per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) +
          (pk.ct_state ? 1 : 0) + (pk.dest ? 1 : 0) + (pk.len ? 2 : 0) + (pk.ct_mark ? 1 : 0);
   return per * n + 24 * 256;  // every region 256-B aligned
 }
 
 // Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
-static int launch_group(const gpc_pkt_soa& pk, uint64_t n, const GroupArgs& group, hipStream_t stream, gpc_pkt_soa* g,
-                        uint32_t** orig, void** mid) {
+static int launch_group(const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group, hipStream_t stream,
+                        gpc_pkt_soa* g, uint32_t** orig, void** mid) {
   if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120) return -GPC_EINVAL;
-  const bool v6 = pk.src6 != nullptr;
   uint8_t* q = group.scratch;
   auto take = [&](uint64_t bytes) {
     uint8_t* r = q;
@@ -487,14 +485,19 @@ static int launch_group(const gpc_pkt_soa& pk, uint64_t n, const GroupArgs& grou
   if (pk.in_port) g->in_port = reinterpret_cast<const uint32_t*>(take(4 * n));
   if (pk.svc_group) g->svc_group = reinterpret_cast<const uint32_t*>(take(4 * n));
   if (pk.tun_id) g->tun_id = reinterpret_cast<const uint32_t*>(take(4 * n));
-  if (pk.ct_src) g->ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
-  if (pk.ct_dst) g->ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (!v6 && pk.ct_src) g->ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (!v6 && pk.ct_dst) g->ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
   if (pk.ct_state) g->ct_state = take(n);
   if (pk.dest) g->dest = take(n);
   if (pk.len) g->len = reinterpret_cast<const uint16_t*>(take(2 * n));
   if (pk.ct_mark) g->ct_mark = take(n);
+  // the other family's address columns are ignored by the classification launches: never copied
+  // (their grouped regions do not exist)
+  gpc_pkt_soa in = pk;
+  if (v6) in.src = in.dst = in.ct_src = in.ct_dst = nullptr;
+  else in.src6 = in.dst6 = in.ct_src6 = in.ct_dst6 = nullptr;
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
-  hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, pk, n, group.src_bits,
+  hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, in, n, group.src_bits,
                      v6 ? group.v6_bit : -1, *g, *orig);
   return 0;
 }
@@ -509,7 +512,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   void* mid = nullptr;
   uint32_t xo = 0;
   if (group) {
-    if (const int rc = launch_group(pk, n, *group, stream, &g, &orig, &mid)) return rc;
+    if (const int rc = launch_group(pk, n, true, *group, stream, &g, &orig, &mid)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
@@ -531,7 +534,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   void* mid = nullptr;
   uint32_t xo = 0;
   if (group) {
-    if (const int rc = launch_group(pk, n, *group, stream, &g, &orig, &mid)) return rc;
+    if (const int rc = launch_group(pk, n, false, *group, stream, &g, &orig, &mid)) return rc;
     xo = group->xcd_order;
     p = &g;
   }

@@ -38,7 +38,7 @@ struct GroupArgs {
   uint32_t xcd_order;  // 1: the blocks of one tile run on one XCD (classify.hip block_xcd_order)
   int32_t v6_bit;      // IPv6 batches: key = 8 bits of ipv6_src from this bit (0 = most significant)
 };
-uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n);
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6);
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream);
 // IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).
