@@ -156,6 +156,8 @@ struct gpc_ctx {
   std::map<hipStream_t, StreamScratch> scratch;  // packet grouping buffers per stream (data)
   uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // packet grouping key (classify.hip)
   uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 1, 0, 1);         // XCD-contiguous tiles
+  // IPv6 grouping: implemented, not yet measured on the device -- opt in with GPC_GROUP_V6=1
+  uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;
   unsigned long long* d_counters = nullptr;
@@ -971,7 +973,7 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
                uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
   GroupArgs ga{nullptr, 8u, ctx->group_xcd, ctx->cur.v6_bit};
-  if (group_batch(ctx, n, ctx->cur.v6->bytes))
+  if (ctx->group_v6 && group_batch(ctx, n, ctx->cur.v6->bytes))
     if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
   int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st);
   if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);

@@ -130,7 +130,8 @@ typedef struct gpc_config {
   int32_t external_node;         /* config.ExternalNode: no IngressSecurityClassifier flows      */
   int32_t group_packets;         /* gpc_classify groups a batch by nw_src before the table walk:
                                     0 = batches of >= 2^18 packets against an image of >= 4 MB,
-                                    > 0 = always, < 0 = never                                    */
+                                    > 0 = always, < 0 = never (gpc_classify6: only with the
+                                    environment GPC_GROUP_V6=1, not yet measured)               */
   int32_t reserved[3];
 } gpc_config;
 

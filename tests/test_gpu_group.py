@@ -4,6 +4,7 @@ scattered back to caller order) is invisible in the results: verdicts, LB result
 counters equal the ungrouped launch's exactly, for ragged batch sizes around the 8192-packet tile
 and with every optional packet column present."""
 import copy
+import os
 
 import numpy as np
 import pytest
@@ -161,6 +162,7 @@ def test_grouped_many_streams():
         assert torch.equal(o, ref)
 
 
+@pytest.mark.skipif(os.environ.get("GPC_GROUP_V6") != "1", reason="IPv6 grouping is opt-in (GPC_GROUP_V6=1)")
 @pytest.mark.parametrize("n", [1, 8191, 8193, 3 * 8192 + 5])
 def test_grouped_ipv6_equals_plain(n):
     """IPv6 batches (gpc_classify6): grouped == plain, verdicts and counters, with ct_*6 columns."""
