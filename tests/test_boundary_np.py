@@ -215,3 +215,63 @@ def test_get_policy_info_from_conjunction():
         ok, ref, prio, name, label = side.get_policy_info_from_conjunction(102)
         assert ok and prio == "100" and name == "102" and label == "test-log-label"
         assert "%s:%s/%s" % (ref[0], ref[1], ref[2]) == "K8sNetworkPolicy:ns1/np1"  # NetworkPolicyReference.ToString
+
+
+def test_network_policy_flow_keys_dual_stack():
+    """TestInstallPolicyRuleFlowsInDualStackCluster (network_policy_test.go:671-810) through the
+    public API: with IPv4 and IPv6 enabled, K8s rule 102 (From two IPv4 + one IPv6 address, To
+    0.0.0.0/0) realizes 2 conj_id flows (ip, ipv6) + 4 conjunctive match flows + 3 drop flows = 9
+    keys, and rule 103 (TCP 8080 / 8081, matched as tcp and tcp6) brings np1 to 20. Rule 101 is the
+    DENY-ALL From-only rule, here of another policy (the reference applies its flows without
+    registering it). Product and oracle compilers give identical dumps and keys."""
+    r1 = _rule(101, ["192.168.1.30", "192.168.1.50", "fd12:ab:34:a001::4"], name="np0")
+    r2 = _rule(102, ["192.168.1.40", "192.168.1.50", "fd12:ab:34:a001::5"], to=["0.0.0.0/0"])
+    r3 = _rule(103, ["192.168.1.40", "192.168.1.60"], to=["192.168.2.0/24"],
+               svc=[{"protocol": "TCP", "port": 8080}, {"protocol": "TCP", "port": 8081}])
+    fnp, c = oc.FeatureNetworkPolicy(ipv4=True, ipv6=True), gpc.Classifier(ipv4=True, ipv6=True)
+    keys = lambda s: sorted(s.get_network_policy_flow_keys("np1", "ns1", "K8sNetworkPolicy"))
+    for side in (fnp, c):
+        side.install_policy_rule_flows(copy.deepcopy(r1))
+    # DENY-ALL: one drop flow per From address in EgressDefaultRule, no conjunction
+    drops = [f for f in c.dump_flows() if "table=EgressDefaultRule" in f]
+    assert len(drops) == 3 and any("ipv6_src=fd12:ab:34:a001::4" in f for f in drops)
+    for side in (fnp, c):
+        side.install_policy_rule_flows(copy.deepcopy(r2))
+    assert len(keys(c)) == 9 and keys(c) == keys(fnp)
+    assert "table=EgressRule,conj_id=102,ipv6" in keys(c)
+    for side in (fnp, c):
+        side.install_policy_rule_flows(copy.deepcopy(r3))
+    assert len(keys(c)) == 20 and keys(c) == keys(fnp)
+    assert "table=EgressRule,tcp6,tp_dst=0x1f90" in keys(c) or "table=EgressRule,tcp6,tp_dst=8080" in keys(c)
+    assert normalize_flows(c.dump_flows()) == normalize_flows(fnp.dump_flows())
+
+
+def test_get_match_flow_updates_reassign():
+    """TestGetMatchFlowUpdates (network_policy_test.go:1197-1273): ANNP rules 10 / 11 at priority 100
+    share the nw_src=192.168.1.40 conjunctive match flow, rule 12 at 200 has its own; after
+    ReassignFlowPriorities {100: 101, 200: 202} the shared flow carries both conjunctions at 101 and
+    rule 12's at 202 -- product and oracle dumps identical, no flow left at the old priorities."""
+    def annp(fid, frm, ports, prio, action, svc=None):
+        r = _rule(fid, frm, to=[{"ofport": p} for p in ports], svc=svc, name="np%d" % fid, prio=prio,
+                  table="AntreaPolicyEgressRule")
+        r.update(policy_type="AntreaNetworkPolicy", action=action)
+        return r
+    tcp8080 = [{"protocol": "TCP", "port": 8080}]
+    rules = [annp(10, ["192.168.1.40", "192.168.1.50"], [1, 2], 100, "Allow"),
+             annp(11, ["192.168.1.40", "192.168.1.51"], [1, 3], 100, "Drop", tcp8080),
+             annp(12, ["192.168.1.40"], [1], 200, "Drop", tcp8080)]
+    fnp, c = oc.FeatureNetworkPolicy(), gpc.Classifier()
+    for side in (fnp, c):
+        side.initialize()
+        side.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    before = [f for f in c.dump_flows() if "nw_src=192.168.1.40" in f]
+    assert any("priority=100" in f and "conjunction(10,1/2)" in f and "conjunction(11,1/3)" in f for f in before)
+    assert any("priority=200" in f and "conjunction(12,1/3)" in f for f in before)
+    for side in (fnp, c):
+        side.reassign_flow_priorities({100: 101, 200: 202}, "AntreaPolicyEgressRule")
+    got = c.dump_flows()
+    assert normalize_flows(got) == normalize_flows(fnp.dump_flows())
+    ap = [f for f in got if "table=AntreaPolicyEgressRule" in f]
+    assert not any("priority=100," in f or "priority=200," in f for f in ap)
+    assert any("priority=101" in f and "nw_src=192.168.1.40" in f and "conjunction(10,1/2)" in f for f in ap)
+    assert any("priority=202" in f and "conj_id=12" in f for f in ap)
