@@ -63,3 +63,20 @@ def test_errors_mirror_reference():
                                             ("dport", np.uint16), ("proto", np.uint8), ("out_port", np.uint32))}
     with pytest.raises(gpc.GpcError):
         c.classify_host(one)  # nothing committed (and no device on this host): fails loudly
+
+
+def test_batch_limit_checked_before_any_device_work():
+    """n > GPC_MAX_BATCH (2^32 - 256, the launch grid limit) is -GPC_EINVAL on both classify entry
+    points before the library touches the device (so also here, without one); the header constant
+    equals that limit."""
+    import ctypes as C
+    hdr = open(gpc.os.path.join(gpc.os.path.dirname(gpc.HERE), "include", "gpc.h")).read()
+    assert re.search(r"#define GPC_MAX_BATCH \(4294967296ull - 256ull\)", hdr)
+    c = gpc.Classifier(ipv4=True, ipv6=True)
+    soa = gpc.gpc_pkt_soa()
+    dummy = (C.c_uint8 * 64)()
+    for name in ("src", "dst", "sport", "dport", "proto", "out_port", "src6", "dst6"):
+        setattr(soa, name, C.addressof(dummy))
+    for n in ((1 << 32) - 255, 1 << 40):
+        assert c.lib.gpc_classify(c.h, C.byref(soa), C.c_size_t(n), C.addressof(dummy), 0, None) == -gpc.GPC_EINVAL
+        assert c.lib.gpc_classify6(c.h, C.byref(soa), C.c_size_t(n), C.addressof(dummy), 0, None) == -gpc.GPC_EINVAL

@@ -1,0 +1,45 @@
+"""CPU only: where one packet's image reads go, from the instrumented host build of the kernel body
+(tests/csrc/emu.cpp compiles core.hpp with GPC_TOUCH / GPC_STAT hooks). Prints distinct 64-B lines
+per packet by source line of core.hpp, plus table lookups, scanned entries and verifications per
+packet -- the proxy used to judge image-layout changes before they go to the GPU.
+
+    python tools/emu_lines.py [--config C3] [--packets 20000]
+"""
+import argparse
+import copy
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--packets", type=int, default=20000)
+    args = ap.parse_args()
+    from antrea_amd import gpc, workload
+    from tests import emu
+    wl = workload.CONFIGS[args.config]()
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    if getattr(wl, "services", None):
+        workload.install_services(c, wl)
+    emu.commit_host(c)
+    cols = workload.gen_packets(wl, args.packets, seed=5)
+    emu.stats(reset=True)
+    emu.site_lines(reset=True)
+    emu.classify(c, cols)
+    s, sites = emu.stats(), emu.site_lines()
+    n = s[7] or 1
+    src = open(os.path.join(os.path.dirname(gpc.HERE), "antrea_amd", "csrc", "core.hpp")).read().split("\n")
+    print("%s: %.2f distinct lines / packet; %.2f table lookups, %.2f entries scanned, %.3f verifications "
+          "(%.3f failed) per packet" % (args.config, s[6] / n, s[0] / n, s[4] / n, s[3] / n, s[5] / n))
+    for line, v in sorted(sites.items(), key=lambda kv: -kv[1]):
+        if v / n >= 0.01:
+            print("  core.hpp:%-5d %6.2f  %s" % (line, v / n, src[line - 1].strip()[:70]))
+
+
+if __name__ == "__main__":
+    main()
