@@ -248,7 +248,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
   const uint64_t block_base = (xcd_order ? block_xcd_order() : uint64_t(blockIdx.x)) * block_threads<kSort>();
   uint64_t i = block_base + threadIdx.x;
-  if (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // its own instantiation: the plain kernel has no barrier
+  if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
   uint4 prev = make_uint4(0u, 0u, 0u, 0u);
