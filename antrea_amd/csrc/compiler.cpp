@@ -584,7 +584,7 @@ Flow FeatureNP::conjunction_deny_flow(uint32_t id, uint8_t table, uint16_t prio,
     f.acts.push_back(set_reg(0, ops << 25, 0xfe000000u));
     f.acts.push_back(set_reg(2, table, 0xff));
     Action g{ACT_GROUP};
-    g.a = metric;  // logging-and-resubmit group keyed by the metric table (network_policy.go:2271-2311)
+    g.a = metric == TB_EGRESS_METRIC ? kLogGroupEgressMetric : kLogGroupIngressMetric;  // resubmits to the metric table
     f.acts.push_back(g);
   } else {
     f.acts.push_back(go(metric));
@@ -608,7 +608,7 @@ Flow FeatureNP::conjunction_pass_flow(uint32_t id, uint8_t table, uint16_t prio,
     f.acts.push_back(set_reg(0, 1u << 25, 0xfe000000u));
     f.acts.push_back(set_reg(2, table, 0xff));
     Action g{ACT_GROUP};
-    g.a = next;
+    g.a = next == TB_EGRESS ? kLogGroupEgressRule : kLogGroupIngressRule;  // resubmits to the K8s rule table
     f.acts.push_back(g);
   } else {
     f.acts.push_back(go(next));

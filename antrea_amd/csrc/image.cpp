@@ -324,9 +324,9 @@ uint8_t action_verdict(const Flow& f, bool* ok) {  // conj_id flows and hard flo
         else if (a.a == TB_OUTPUT) output = true;
         else *ok = false;
         break;
-      case ACT_GROUP:
-        if (a.a == t2) pass = true;
-        else metric = true;  // logging / reject group resubmits to the metric table
+      case ACT_GROUP:  // logging-and-resubmit group (model.hpp kLogGroup*): to the K8s rule table = Pass
+        if (a.a == kLogGroupEgressRule || a.a == kLogGroupIngressRule) pass = true;
+        else metric = true;
         break;
       default: break;
     }

@@ -40,6 +40,10 @@ enum TableId : uint8_t {
   TB_COUNT = 17
 };
 const char* table_name(uint8_t t);
+// Logging-and-resubmit group IDs as initGroups allocates them (network_policy.go:2271-2300, Multicast
+// off; client_test.go:2762-2767): keyed by the table the group resubmits to.
+constexpr uint32_t kLogGroupEgressRule = 1, kLogGroupEgressMetric = 2, kLogGroupIngressRule = 3,
+                   kLogGroupIngressMetric = 4;
 inline bool is_egress_table(uint8_t t) { return t == TB_AP_EGRESS || t == TB_EGRESS || t == TB_EGRESS_DEFAULT || t == TB_EGRESS_METRIC; }
 uint8_t next_table(uint8_t t);
 

@@ -36,6 +36,14 @@ PRIORITY_NORMAL = 200
 PRIORITY_LOW = 190
 PRIORITY_TOP_ANTREA_POLICY = 64990
 PRIORITY_DNS_INTERCEPT = 64991
+# PacketInTableField (reg2[0..7]) carries the rule table's OpenFlow table ID, which depends on the
+# agent's realized pipeline; the restatement (like libgpc, model.hpp TB_*) numbers the six rule
+# tables 1-6. The logging-and-resubmit groups take the group IDs initGroups allocates in order
+# (network_policy.go:2271-2300, Multicast off): EgressRule 1, EgressMetric 2, IngressRule 3,
+# IngressMetric 4 (as in client_test.go:2762-2767).
+TABLE_NUM = {"AntreaPolicyEgressRule": 1, "EgressRule": 2, "EgressDefaultRule": 3, "AntreaPolicyIngressRule": 4,
+             "IngressRule": 5, "IngressDefaultRule": 6}
+LOGGING_GROUP = {"EgressRule": 1, "EgressMetric": 2, "IngressRule": 3, "IngressMetric": 4}
 DNS_PORT = 53
 PACKET_IN_METER_NP, PACKET_IN_METER_DNS = 256, 258          # client.go:851-858 meter ids
 PACKET_IN_CATEGORY_NP, PACKET_IN_CATEGORY_DNS = 1, 2       # packetin.go:44-52
@@ -671,7 +679,7 @@ class FeatureNetworkPolicy:
         if enable_logging or self.enable_deny_tracking:
             ops = (1 if enable_logging else 0) + (2 if self.enable_deny_tracking else 0)
             acts = [("set_reg", 0, DISPOSITION_DROP << 11, 0x1800), ("set_reg", 0, ops << 25, 0x1FE000000 & 0xFFFFFFFF),
-                    ("set_reg", 0, 2 << 21, 0x600000), ("set_reg", 2, 0, 0xFF), ("goto_table", "Output")]
+                    ("set_reg", 0, 2 << 21, 0x600000), ("set_reg", 2, TABLE_NUM[table], 0xFF), ("goto_table", "Output")]
             return Flow(table, PRIORITY_NORMAL, m, acts, self.cookie)
         return Flow(table, PRIORITY_NORMAL, m, [("drop",)], self.cookie)
 
@@ -697,7 +705,8 @@ class FeatureNetworkPolicy:
             acts = [("set_reg", reg, cid, None), ("ct_commit", next_table, zone, [label])]
             if enable_logging:
                 acts += [("set_reg", 0, 0, 0x1800), ("set_reg", 0, 2 << 21, 0x600000),
-                         ("set_reg", 0, 1 << 25, 0x1FE000000 & 0xFFFFFFFF), ("goto_table", "Output")]
+                         ("set_reg", 0, 1 << 25, 0x1FE000000 & 0xFFFFFFFF), ("set_reg", 2, TABLE_NUM[table], 0xFF),
+                         ("goto_table", "Output")]
             flows.append(Flow(table, p, m, acts, self.cookie))
         return flows
 
@@ -716,8 +725,8 @@ class FeatureNetworkPolicy:
         if disposition == DISPOSITION_REJ:
             ops += 4
         if enable_logging or self.enable_deny_tracking or disposition == DISPOSITION_REJ:
-            acts += [("set_reg", 0, ops << 25, 0x1FE000000 & 0xFFFFFFFF), ("set_reg", 2, 0, 0xFF),
-                     ("group", 0)]
+            acts += [("set_reg", 0, ops << 25, 0x1FE000000 & 0xFFFFFFFF), ("set_reg", 2, TABLE_NUM[table], 0xFF),
+                     ("group", LOGGING_GROUP[metric])]
         else:
             acts.append(("goto_table", metric))
         return Flow(table, priority, m, acts, self.cookie)
@@ -730,7 +739,8 @@ class FeatureNetworkPolicy:
         m = {"conj_id": (cid,)}
         acts = [("set_reg", reg, cid, None)]
         if enable_logging:
-            acts += [("set_reg", 0, DISPOSITION_PASS << 11, 0x1800), ("group", 0)]
+            acts += [("set_reg", 0, DISPOSITION_PASS << 11, 0x1800), ("set_reg", 0, 1 << 25, 0xFE000000),
+                     ("set_reg", 2, TABLE_NUM[table], 0xFF), ("group", LOGGING_GROUP[nxt])]
         else:
             acts.append(("goto_table", nxt))
         return Flow(table, priority, m, acts, self.cookie)

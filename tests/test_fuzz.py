@@ -1,0 +1,176 @@
+"""CPU tier, property-based: small random NetworkPolicy rule sets over a tiny address / port
+universe (so rules overlap, share conjunctive match flows, tie in priority and hit each other's
+packets), checked three ways -- the product compiler's flow dump equals the oracle compiler's,
+and the product image evaluated by the host emulation of the kernel body (tests/csrc/emu.cpp,
+same core.hpp as the device) gives the Python OVS oracle's verdict for every packet of a random
+batch drawn from the same universe. hypothesis shrinks a failure to a minimal rule set."""
+import copy
+
+import numpy as np
+import pytest
+
+hypothesis = pytest.importorskip("hypothesis")
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+from antrea_amd import gpc  # noqa: E402
+from tests.test_emu_parity import _cmp, oracle_verdicts, product_verdicts  # noqa: E402
+from tests.util import assign_tables, normalize_flows  # noqa: E402
+
+IPS = ["10.0.0.%d" % i for i in range(8)]
+CIDRS = ["10.0.0.0/29", "10.0.0.4/30", "10.0.0.0/24", "10.0.1.0/24", "0.0.0.0/0"]
+PORTS = [80, 81, 443, 1000, 5000]
+
+addr = st.one_of(st.sampled_from(IPS), st.sampled_from(CIDRS))
+ofport = st.builds(lambda p: {"ofport": p}, st.integers(1, 4))
+
+
+def _svc():
+    l4 = st.builds(lambda proto, port, width: {"protocol": proto, "port": port, **({"end_port": port + width}
+                                                                                  if width else {})},
+                   st.sampled_from(["TCP", "UDP"]), st.sampled_from(PORTS), st.sampled_from([0, 0, 1, 7]))
+    icmp = st.builds(lambda t: {"protocol": "ICMP", "icmp_type": t, "icmp_code": 0}, st.sampled_from([0, 8]))
+    proto_only = st.builds(lambda p: {"protocol": p}, st.sampled_from(["TCP", "UDP"]))
+    return st.one_of(st.none(), st.lists(st.one_of(l4, icmp, proto_only), min_size=0, max_size=2))
+
+
+@st.composite
+def rule(draw, fid):
+    k8s = draw(st.booleans())
+    direction = draw(st.sampled_from(["In", "Out"]))
+    peers = st.one_of(st.none(), st.lists(addr, min_size=0, max_size=3))
+    applied = st.lists(ofport if direction == "In" else st.sampled_from(IPS[:4]), min_size=1, max_size=2)
+    r = {"direction": direction, "flow_id": fid, "name": "r%d" % fid,
+         "policy_type": "K8sNetworkPolicy" if k8s else "AntreaClusterNetworkPolicy",
+         "policy_namespace": "" if not k8s else "ns", "policy_name": "p%d" % fid, "policy_uid": "u%d" % fid,
+         "service": draw(_svc()), "enable_logging": draw(st.sampled_from([False, False, True]))}
+    if direction == "In":
+        r["from"], r["to"] = draw(peers), draw(applied)
+    else:
+        r["from"], r["to"] = draw(applied), draw(peers)
+    if not k8s:
+        r["action"] = draw(st.sampled_from(["Allow", "Drop", "Reject", "Pass"]))
+        r["priority"] = draw(st.sampled_from([100, 100, 101, 200]))  # equal priorities: ties
+        r["tier_priority"] = draw(st.sampled_from([50, 250]))
+    return r
+
+
+@st.composite
+def rule_set(draw):
+    n = draw(st.integers(1, 6))
+    return assign_tables([draw(rule(100 + i)) for i in range(n)])
+
+
+@st.composite
+def packets(draw):
+    n = 48
+    ip_pool = [int.from_bytes(bytes(map(int, a.split("."))), "big") for a in IPS] + [0x0A000109, 0x0B000001]
+    pick = lambda: st.lists(st.sampled_from(ip_pool), min_size=n, max_size=n)
+    proto = draw(st.lists(st.sampled_from([6, 6, 17, 1]), min_size=n, max_size=n))
+    dport = draw(st.lists(st.sampled_from(PORTS + [1003, 1007, 1008]), min_size=n, max_size=n))
+    icmp_t = draw(st.lists(st.sampled_from([0, 8]), min_size=n, max_size=n))
+    return {"src": np.array(draw(pick()), np.uint32), "dst": np.array(draw(pick()), np.uint32),
+            "sport": np.array([t if p == 1 else 40000 for t, p in zip(icmp_t, proto)], np.uint16),
+            "dport": np.array([0 if p == 1 else d for d, p in zip(dport, proto)], np.uint16),
+            "proto": np.array(proto, np.uint8),
+            "out_port": np.array(draw(st.lists(st.integers(1, 4), min_size=n, max_size=n)), np.uint32),
+            "ct_state": np.array(draw(st.lists(st.sampled_from([0x21, 0x21, 0x21, 0x22]), min_size=n,
+                                               max_size=n)), np.uint8)}
+
+
+@settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")), deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(rules=rule_set(), cols=packets())
+def test_random_rule_sets_product_equals_oracle(rules, cols):
+    from oracle import compiler as oc
+    fnp = oc.FeatureNetworkPolicy()
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    got, c = product_verdicts(rules, cols)
+    assert normalize_flows(c.dump_flows()) == normalize_flows(fnp.dump_flows())
+    want, _ = oracle_verdicts(rules, cols, len(cols["src"]))
+    _cmp(got, want, cols)
+
+
+@st.composite
+def churn(draw):
+    """A rule set, then 1-8 control-plane operations on it (the agent's churn path, network_policy.go
+    1570-1710, 1873), each published with gpc_commit (delta epochs on the product side)."""
+    rules = draw(rule_set())
+    ops = []
+    for _ in range(draw(st.integers(1, 8))):
+        i = draw(st.integers(0, len(rules) - 1))
+        r = rules[i]
+        kind = draw(st.sampled_from(["add", "add", "del", "uninstall", "reinstall", "reassign"]))
+        side = draw(st.sampled_from(["src", "dst"]))
+        peer_side = "dst" if r["direction"] == "Out" else "src"
+        if side == peer_side:
+            addrs = draw(st.lists(addr, min_size=1, max_size=2))
+        elif r["direction"] == "In":
+            addrs = draw(st.lists(ofport, min_size=1, max_size=2))
+        else:
+            addrs = draw(st.lists(st.sampled_from(IPS[:6]), min_size=1, max_size=2))
+        ops.append((kind, i, side, addrs))
+    return rules, ops
+
+
+def _both(fnp, c, fn):
+    """Apply one operation to the oracle and the product: both succeed or both fail."""
+    errs = []
+    for side in (fnp, c):
+        try:
+            fn(side)
+            errs.append(None)
+        except Exception as e:  # noqa: BLE001 -- the error class differs, the outcome must not
+            errs.append(e)
+    assert (errs[0] is None) == (errs[1] is None), errs
+    return errs[1] is None
+
+
+@settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")), deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(case=churn(), cols=packets())
+def test_random_churn_product_equals_oracle(case, cols):
+    """Random churn in lock step: after every operation the realized flows are identical, and at the
+    end the product's committed image (base + journal delta epochs, host emulation of the kernel
+    body) gives the Python oracle's verdicts."""
+    from oracle import compiler as oc
+    from oracle import ovs_cls
+    from tests import emu
+    rules, ops = case
+    rules = copy.deepcopy(rules)
+    fnp, c = oc.FeatureNetworkPolicy(), gpc.Classifier()
+    for side in (fnp, c):
+        side.initialize()
+        side.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    emu.commit_host(c, full=True)
+    installed = {r["flow_id"]: True for r in rules}
+    for kind, i, side, addrs in ops:
+        r = rules[i]
+        fid, prio = r["flow_id"], r.get("priority")
+        if kind == "add":
+            _both(fnp, c, lambda s: s.add_policy_rule_address(fid, side, copy.deepcopy(addrs), prio))
+        elif kind == "del":
+            _both(fnp, c, lambda s: s.delete_policy_rule_address(fid, side, copy.deepcopy(addrs), prio))
+        elif kind == "uninstall" and installed[fid]:
+            if _both(fnp, c, lambda s: s.uninstall_policy_rule_flows(fid)):
+                installed[fid] = False
+        elif kind == "reinstall" and not installed[fid]:
+            if _both(fnp, c, lambda s: s.install_policy_rule_flows(copy.deepcopy(r))):
+                installed[fid] = True
+        elif kind == "reassign" and prio is not None:
+            upd = {prio: prio + 1000}
+            if _both(fnp, c, lambda s: s.reassign_flow_priorities(upd, r["table"])):
+                for q in rules:
+                    if q.get("priority") == prio and q["table"] == r["table"]:
+                        q["priority"] = prio + 1000
+        assert normalize_flows(c.dump_flows()) == normalize_flows(fnp.dump_flows()), (kind, fid, side, addrs)
+        emu.commit_host(c)
+    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in rules}
+    pipe = ovs_cls.Pipeline(fnp.dump_flows(), tiers)
+    n = len(cols["src"])
+    want = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
+    for k in range(n):
+        e, g = pipe.classify({key: int(v[k]) for key, v in cols.items()})
+        for j, v in enumerate((e, g)):
+            want[k, j] = (v[1], v[0], v[2], v[3], v[4])
+    _cmp(emu.classify(c, cols), want, cols)
