@@ -174,3 +174,87 @@ def test_random_churn_product_equals_oracle(case, cols):
         for j, v in enumerate((e, g)):
             want[k, j] = (v[1], v[0], v[2], v[3], v[4])
     _cmp(emu.classify(c, cols), want, cols)
+
+
+IPS6 = ["fd00::%x" % i for i in range(1, 4)] + ["fd00::/126", "fd00::/64"]
+
+
+@st.composite
+def rich_rule(draw, fid):
+    """rule() plus IPv6 peers (dual-stack flows), ANNP / BANP (baseline tier: *DefaultRule tables),
+    logging, source-port ranges."""
+    r = draw(rule(fid))
+    kind = draw(st.sampled_from(["K8sNetworkPolicy", "AntreaClusterNetworkPolicy", "AntreaNetworkPolicy",
+                                 "BaselineAdminNetworkPolicy"]))
+    r["policy_type"] = kind
+    if kind == "K8sNetworkPolicy":
+        for k in ("action", "priority", "tier_priority"):
+            r.pop(k, None)
+    else:
+        r.setdefault("action", draw(st.sampled_from(["Allow", "Drop", "Reject"])))
+        r.setdefault("priority", draw(st.sampled_from([100, 101])))
+        if kind == "BaselineAdminNetworkPolicy":
+            r["action"] = draw(st.sampled_from(["Allow", "Drop"]))
+            r["priority"] = draw(st.sampled_from([10, 11, 20]))
+            r["table"] = "EgressDefaultRule" if r["direction"] == "Out" else "IngressDefaultRule"
+    peer_key = "to" if r["direction"] == "Out" else "from"
+    if r[peer_key] is not None and draw(st.booleans()):
+        r[peer_key] = r[peer_key] + draw(st.lists(st.sampled_from(IPS6), min_size=1, max_size=2))
+    if r["service"] and draw(st.booleans()):
+        s = dict(r["service"][0])
+        if s.get("protocol") in ("TCP", "UDP"):
+            s.update(src_port=40000, src_end_port=40003)
+            r["service"] = [s] + r["service"][1:]
+    return r
+
+
+@st.composite
+def rich_packets(draw):
+    cols = draw(packets())
+    n = len(cols["src"])
+    cols["ct_state"] = np.array(draw(st.lists(st.sampled_from([0x21, 0x21, 0x22, 0x24, 0x2a]), min_size=n,
+                                              max_size=n)), np.uint8)
+    cols["dest"] = np.array(draw(st.lists(st.sampled_from([0, 0, 0, 1, 2, 3]), min_size=n, max_size=n)), np.uint8)
+    cols["ct_mark"] = np.array(draw(st.lists(st.sampled_from([0, 0, 0, 0x40]), min_size=n, max_size=n)), np.uint8)
+    cols["sport"] = np.where(cols["proto"] == 1, cols["sport"],
+                             np.array(draw(st.lists(st.sampled_from([40000, 40002, 40004]), min_size=n, max_size=n)),
+                                      np.uint16)).astype(np.uint16)
+    return cols
+
+
+@settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")), deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(rules=st.integers(1, 6).flatmap(lambda n: st.tuples(*[rich_rule(100 + i) for i in range(n)])),
+       cols=rich_packets(), dns=st.booleans())
+def test_random_dual_stack_rule_sets_product_equals_oracle(rules, cols, dns):
+    """Dual-stack contexts (IPv4 + IPv6 flows), all policy kinds incl. the baseline tier, logging,
+    source-port ranges, a DNS interception conjunction, and packets with conntrack states,
+    IngressSecurityClassifier destinations and the hairpin mark: product == oracle flows, and the
+    IPv4 verdicts of the emulated product image == the Python oracle's."""
+    from oracle import compiler as oc
+    from oracle import ovs_cls
+    from tests import emu
+    rules = assign_tables([copy.deepcopy(r) for r in rules])
+    fnp, c = oc.FeatureNetworkPolicy(ipv4=True, ipv6=True), gpc.Classifier(ipv4=True, ipv6=True)
+    for side in (fnp, c):
+        side.initialize()
+        if dns:
+            side.new_dns_packet_in_conjunction(7)
+            side.add_address_to_dns_conjunction(7, ["10.0.0.2", "fd00::2"])
+        side.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    assert normalize_flows(c.dump_flows()) == normalize_flows(fnp.dump_flows())
+    emu.commit_host(c)
+    tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in rules}
+    pipe = ovs_cls.Pipeline(fnp.dump_flows(), tiers)
+    n = len(cols["src"])
+    want = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
+    for k in range(n):
+        e, g = pipe.classify({key: int(v[k]) for key, v in cols.items()})
+        for j, v in enumerate((e, g)):
+            want[k, j] = (v[1], v[0], v[2], v[3], v[4])
+    _cmp(emu.classify(c, cols), want, cols)
+    # the C restatement (the full-scale checker and CPU baseline) agrees with the Python one
+    from oracle.cls_c import CPipeline
+    cp = CPipeline(fnp.dump_flows(), tiers, procs=1)
+    got_c = cp.classify(cols, threads=1)
+    _cmp(np.ascontiguousarray(got_c).view(gpc.VERDICT_DTYPE).reshape(-1, 2), want, cols)
