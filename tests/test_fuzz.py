@@ -269,3 +269,25 @@ def test_random_dual_stack_rule_sets_product_equals_oracle(rules, cols, dns):
     cp = CPipeline(fnp.dump_flows(), tiers, procs=1)
     got_c = cp.classify(cols, threads=1)
     _cmp(np.ascontiguousarray(got_c).view(gpc.VERDICT_DTYPE).reshape(-1, 2), want, cols)
+
+
+@settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_SVC_EXAMPLES", "15")), deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(seed=st.integers(1, 10_000), c1=st.booleans(), n_svc=st.integers(1, 40), eps=st.integers(1, 6))
+def test_random_services_product_equals_oracle(seed, c1, n_svc, eps):
+    """AntreaProxy stage on random Service sets (Endpoints local / remote, no-Endpoint
+    Services, Local traffic policy) in front of random policies: the emulated product's verdicts and
+    LB results equal the Python oracle's over the realized ServiceLB / EndpointDNAT flows and groups."""
+    from antrea_amd import workload
+    from tests import emu
+    from tests.test_service import _oracle, _product
+    base = workload.config1(seed=seed) if c1 else workload.config3(seed=seed, n_policies_per_dir=4, rules_per_policy=6)
+    wl = workload.add_services(base, n_svc, eps, seed=seed, noep_frac=0.15, local_policy_frac=0.25)
+    n = 300
+    cols = workload.gen_packets(wl, n, seed=seed)
+    c = _product(wl)
+    lb = np.zeros(n, dtype=gpc.LB_DTYPE)
+    got = emu.classify(c, cols, lb=lb)
+    want, want_lb = _oracle(wl, c, cols, n)
+    _cmp(got, want, cols)
+    assert (lb == want_lb).all()
