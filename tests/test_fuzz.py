@@ -264,6 +264,24 @@ def test_random_dual_stack_rule_sets_product_equals_oracle(rules, cols, dns):
         for j, v in enumerate((e, g)):
             want[k, j] = (v[1], v[0], v[2], v[3], v[4])
     _cmp(emu.classify(c, cols), want, cols)
+    # IPv6 packets of the same batch (addresses from the IPv6 peers' universe) through the IPv6 image
+    import ipaddress
+    pool6 = [int(ipaddress.IPv6Address("fd00::%x" % i)) for i in range(1, 6)] + [int(ipaddress.IPv6Address("fe80::1"))]
+    rng = np.random.default_rng(int(cols["src"][0]) ^ n)
+    s6 = [pool6[k] for k in rng.integers(0, len(pool6), n)]
+    d6 = [pool6[k] for k in rng.integers(0, len(pool6), n)]
+    cols6 = {k: v for k, v in cols.items() if k not in ("src", "dst")}
+    cols6["proto"] = np.where(cols["proto"] == 1, 58, cols["proto"]).astype(np.uint8)
+    cols6["src6"] = np.array([list(x.to_bytes(16, "big")) for x in s6], np.uint8)
+    cols6["dst6"] = np.array([list(x.to_bytes(16, "big")) for x in d6], np.uint8)
+    want6 = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
+    for k in range(n):
+        pkt = {key: int(v[k]) for key, v in cols6.items() if v.ndim == 1}
+        pkt.update(src=s6[k], dst=d6[k], eth=0x86DD)
+        e, g = pipe.classify(pkt)
+        for j, v in enumerate((e, g)):
+            want6[k, j] = (v[1], v[0], v[2], v[3], v[4])
+    _cmp(emu.classify6(c, cols6), want6, cols6)
     # the C restatement (the full-scale checker and CPU baseline) agrees with the Python one
     from oracle.cls_c import CPipeline
     cp = CPipeline(fnp.dump_flows(), tiers, procs=1)
