@@ -184,7 +184,22 @@ def test_random_churn_product_equals_oracle(case, cols):
         e, g = pipe.classify({key: int(v[k]) for key, v in cols.items()})
         for j, v in enumerate((e, g)):
             want[k, j] = (v[1], v[0], v[2], v[3], v[4])
-    _cmp(emu.classify(c, cols), want, cols)
+    _, slots = c.counters()
+    cnt = np.zeros((max(1, len(slots)), 3), np.uint64)
+    _cmp(emu.classify(c, cols, counters=cnt), want, cols)
+    per_conj = {int(s): tuple(int(x) for x in cnt[i]) for i, s in enumerate(slots) if s and cnt[i].any()}
+    # a full rebuild (compaction) of the same state: same verdicts, same per-rule counts
+    emu.commit_host(c, full=True)
+    _, slots2 = c.counters()
+    cnt2 = np.zeros((max(1, len(slots2)), 3), np.uint64)
+    _cmp(emu.classify(c, cols, counters=cnt2), want, cols)
+    assert per_conj == {int(s): tuple(int(x) for x in cnt2[i]) for i, s in enumerate(slots2) if s and cnt2[i].any()}
+    # ... and the Metric-table counters of the C oracle over the oracle's flows (NetworkPolicyMetrics)
+    from oracle import parity
+    from oracle.cls_c import CPipeline
+    cp = CPipeline(fnp.dump_flows(), tiers, procs=1)
+    cp.classify(cols, threads=1, count=True)
+    assert per_conj == {k: v for k, v in parity.oracle_metrics(cp).items() if any(v)}
 
 
 IPS6 = ["fd00::%x" % i for i in range(1, 4)] + ["fd00::/126", "fd00::/64"]
