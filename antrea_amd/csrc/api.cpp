@@ -75,6 +75,7 @@ struct DevImage {  // one uploaded image (freed when the last epoch using it ret
   size_t bytes = 0;
   hipStream_t s = nullptr;
   uint8_t sort_table[2] = {0, 0};       // per policy stage: the table whose scan length orders lanes
+  uint32_t axes = 0;                    // axes read by the sub-indexes (group_axes)
   ~DevImage() {
     dev_free(d_hdr, s);
     dev_free(d_blob, s);
@@ -154,7 +155,8 @@ struct gpc_ctx {
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
   std::map<hipStream_t, StreamScratch> scratch;  // packet grouping buffers per stream (data)
-  uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // packet grouping key (classify.hip)
+  uint32_t group_key = GPC_GROUP_KEY_AUTO;                            // gpc_group_key (gpc_create)
+  uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // GPC_GROUP_KEY_ADDR key bits (classify.hip)
   uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 1, 0, 1);         // XCD-contiguous tiles
   // IPv6 grouping: implemented, not yet measured on the device -- opt in with GPC_GROUP_V6=1
   uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
@@ -250,6 +252,16 @@ static void lane_sort_tables(const HostImage& h, uint8_t* sort_table) {
   }
 }
 
+// Axes the driver sub-indexes of the image read: the packet columns the scan-length grouping key
+// (classify.hip scan_key) needs.
+static uint32_t group_axes(const HostImage& h) {
+  uint32_t m = 0;
+  for (const TableHdr& th : h.hdr.t)
+    for (int k = 0; k < 2; k++)
+      for (uint32_t i = 0; i < th.n_idx[k] && i < uint32_t(kIdxPerClause); i++) m |= 1u << th.idx[k][i].axis;
+  return m;
+}
+
 static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevImage>* out) {
   auto d = std::make_shared<DevImage>();
   d->s = s;
@@ -259,6 +271,7 @@ static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevIm
       hip_ok(hipMemcpyAsync(d->d_hdr, &h.hdr, sizeof(ImageHdr), hipMemcpyHostToDevice, s)))
     return -GPC_EDEV;
   lane_sort_tables(h, d->sort_table);
+  d->axes = group_axes(h);
   *out = std::move(d);
   return GPC_OK;
 }
@@ -426,8 +439,11 @@ const char* gpc_strerror(int err) {
 int gpc_create(const gpc_config* cfg, gpc_ctx** out) {
   if (!cfg || !out) return -GPC_EINVAL;
   if (!cfg->ipv4_enabled && !cfg->ipv6_enabled) return -GPC_EINVAL;
+  if (cfg->group_key < GPC_GROUP_KEY_AUTO || cfg->group_key > GPC_GROUP_KEY_SCAN) return -GPC_EINVAL;
   try {
     *out = new gpc_ctx(*cfg);
+    // grouping key: the environment (experiments) overrides the config
+    (*out)->group_key = env_u32("GPC_GROUP_KEY", uint32_t(cfg->group_key), GPC_GROUP_KEY_AUTO, GPC_GROUP_KEY_SCAN);
     if (cfg->compact_after >= 0) (*out)->comp.th = std::thread(compactor_main, *out);
     else (*out)->comp.enabled = false;
   } catch (...) {
@@ -867,6 +883,15 @@ static bool group_batch(const gpc_ctx* ctx, size_t n, size_t image_bytes) {
   return n && (gm > 0 || (gm == 0 && n >= kGroupMinPackets && image_bytes >= kGroupMinImageBytes));
 }
 
+// GPC_GROUP_KEY_AUTO: scan lengths where a wavefront's lanes scan very unequal driver lists (the
+// lane_sort_tables statistic: C2, 26.4 -> 16.3 ms per 64M packets), address bits where the image
+// lines a wave shares matter more (C3 13.2 ms by address vs 15.4 by scan length, C4 14.3 vs 16.4).
+static uint32_t group_key(const gpc_ctx* ctx) {
+  if (ctx->group_key != GPC_GROUP_KEY_AUTO) return ctx->group_key;
+  const DevImage& b = *ctx->cur.base;
+  return (b.sort_table[0] || b.sort_table[1]) ? uint32_t(GPC_GROUP_KEY_SCAN) : uint32_t(GPC_GROUP_KEY_ADDR);
+}
+
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
   return gpc_classify_lb(ctx, pk, n, out, nullptr, count, stream);
 }
@@ -886,7 +911,7 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
   // the next batch on that stream (launches of one stream run in order), so callers on different
   // streams never share one and the data path does no allocation once warm
-  GroupArgs ga{nullptr, ctx->group_src_bits, ctx->group_xcd, 0};
+  GroupArgs ga{nullptr, group_key(ctx), ctx->cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0};
   if (group_batch(ctx, n, ctx->cur.base->bytes))
     if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, false), &ga.scratch)) return e;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
@@ -972,7 +997,7 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm, {0, 0},
                uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  GroupArgs ga{nullptr, 8u, ctx->group_xcd, ctx->cur.v6_bit};
+  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, ctx->cur.v6_bit};
   if (ctx->group_v6 && group_batch(ctx, n, ctx->cur.v6->bytes))
     if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
   int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st);

@@ -161,18 +161,55 @@ __device__ __forceinline__ uint32_t group_key(uint32_t src, uint32_t dst, uint32
   return hi | (db ? dst >> (32u - db) : 0u);
 }
 
+// Scan-length key (GroupArgs.key == GPC_GROUP_KEY_SCAN): the candidate scan of a wavefront runs as
+// long as its longest lane, so lanes whose walks scan equally long driver lists belong together.
+// Per policy stage the packet's driver-list length (core.hpp scan_estimate, summed over the stage's
+// tables: the bucket offsets only, no entry is read) binned to 4 bits, floor(1.5 sqrt(len)) capped
+// at 15 (finer where most packets are); key = egress bin << 4 | ingress bin. `axes`: the axes the
+// image's sub-indexes read (only those columns are loaded); ax: this thread's LDS column of axes.
+__device__ __forceinline__ uint32_t scan_bin(uint32_t len) {
+  const uint32_t b = uint32_t(1.5f * sqrtf(float(len)));
+  return b < 15u ? b : 15u;
+}
+__device__ __forceinline__ uint32_t scan_key(const EpochArgs& ep, const gpc_pkt_soa& in, uint64_t i, uint32_t axes,
+                                             uint32_t* ax) {
+  auto has = [&](uint32_t a) { return (axes >> a) & 1u; };
+  const uint32_t src = has(AX_SRC) || (has(AX_CTSRC) && !in.ct_src) ? in.src[i] : 0u;
+  const uint32_t dst = has(AX_DST) || (has(AX_CTDST) && !in.ct_dst) ? in.dst[i] : 0u;
+  const bool l4 = has(AX_L4D) || has(AX_L4S);
+  Pkt p(ax, kGroupThreads);
+  make_axes(p, src, dst, has(AX_L4S) ? in.sport[i] : 0u, has(AX_L4D) ? in.dport[i] : 0u, l4 ? in.proto[i] : 0u,
+            has(AX_REG1) ? in.out_port[i] : 0u, has(AX_INPORT) && in.in_port ? in.in_port[i] : 0u,
+            has(AX_REG7) && in.svc_group ? in.svc_group[i] : 0u, has(AX_TUN) && in.tun_id ? in.tun_id[i] : 0u,
+            has(AX_CTSRC) && in.ct_src ? in.ct_src[i] : src, has(AX_CTDST) && in.ct_dst ? in.ct_dst[i] : dst,
+            has(AX_CTST) && in.ct_state ? in.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+  const Img im{ep.blob, ep.hdr, nullptr, nullptr};
+  uint32_t e = 0, g = 0;
+#pragma unroll
+  for (uint32_t t = 1; t <= 3; t++) {
+    e += scan_estimate(im, t, p);
+    g += scan_estimate(im, t + 3, p);
+  }
+  return scan_bin(e) << 4 | scan_bin(g);
+}
+
 // v6_bit >= 0: an IPv6 batch, keyed by 8 bits of ipv6_src from that bit (api.cpp picks the bits
-// just above the shortest prefix of the IPv6 image).
-__global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(gpc_pkt_soa in, uint64_t n, uint32_t src_bits,
+// just above the shortest prefix of the IPv6 image). Else key_mode GPC_GROUP_KEY_SCAN: scan_key;
+// GPC_GROUP_KEY_ADDR: group_key.
+__global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(EpochArgs ep, gpc_pkt_soa in, uint64_t n,
+                                                                    uint32_t key_mode, uint32_t axes, uint32_t src_bits,
                                                                     int32_t v6_bit, gpc_pkt_soa g, uint32_t* __restrict__ orig) {
   __shared__ uint32_t stage[kGroupTile];  // the tile's keys, then one column of the tile
   __shared__ uint16_t from[kGroupTile];   // grouped position -> tile position
   __shared__ uint32_t cur[kGroupBins];
+  __shared__ uint32_t axl[AX_N * kGroupThreads];  // scan_key: per-thread packet axes, [axis][thread]
   const uint32_t tid = threadIdx.x;
   const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
   const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
   if (tid < kGroupBins) cur[tid] = 0;
-  if (v6_bit >= 0) {
+  if (v6_bit < 0 && key_mode == GPC_GROUP_KEY_SCAN) {
+    for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = scan_key(ep, in, base + j, axes, axl + tid);
+  } else if (v6_bit >= 0) {
     for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = group_key6(in.src6 + (base + j) * 16, uint32_t(v6_bit));
   } else if (src_bits == 8u) {
     for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = in.src[base + j] >> 24;
@@ -457,9 +494,9 @@ uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6) {
 }
 
 // Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
-static int launch_group(const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group, hipStream_t stream,
-                        gpc_pkt_soa* g, uint32_t** orig, void** mid) {
-  if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120) return -GPC_EINVAL;
+static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group,
+                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid) {
+  if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120 || (group.key != GPC_GROUP_KEY_ADDR && group.key != GPC_GROUP_KEY_SCAN)) return -GPC_EINVAL;
   uint8_t* q = group.scratch;
   auto take = [&](uint64_t bytes) {
     uint8_t* r = q;
@@ -497,8 +534,8 @@ static int launch_group(const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupA
   if (v6) in.src = in.dst = in.ct_src = in.ct_dst = nullptr;
   else in.src6 = in.dst6 = in.ct_src6 = in.ct_dst6 = nullptr;
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
-  hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, in, n, group.src_bits,
-                     v6 ? group.v6_bit : -1, *g, *orig);
+  hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, ep, in, n, group.key,
+                     group.axes, group.src_bits, v6 ? group.v6_bit : -1, *g, *orig);
   return 0;
 }
 
@@ -512,7 +549,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   void* mid = nullptr;
   uint32_t xo = 0;
   if (group) {
-    if (const int rc = launch_group(pk, n, true, *group, stream, &g, &orig, &mid)) return rc;
+    if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
@@ -534,15 +571,17 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   void* mid = nullptr;
   uint32_t xo = 0;
   if (group) {
-    if (const int rc = launch_group(pk, n, false, *group, stream, &g, &orig, &mid)) return rc;
+    if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
+  EpochArgs e = ep;
+  if (group && group->key == GPC_GROUP_KEY_SCAN) e.sort_table[0] = e.sort_table[1] = 0;  // lanes already grouped by scan length
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
-  if (delta && svc) launch<true, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
-  else if (delta) launch<true, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
-  else if (svc) launch<false, true>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
-  else launch<false, false>(ep, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  if (delta && svc) launch<true, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  else if (svc) launch<false, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
+  else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

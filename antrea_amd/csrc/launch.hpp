@@ -29,12 +29,14 @@ int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t
 int launch_merge_counters(unsigned long long* dst, const unsigned long long* src, uint64_t src_stride, uint32_t copies,
                           uint64_t n_words, hipStream_t stream);
 // Packet grouping of a batch (classify.hip group_tiles_kernel): the batch is classified in the
-// order of an 8-bit key of nw_src / nw_dst top bits within every tile of 16384 packets, from a grouped copy in
+// order of an 8-bit key (scan lengths or address bits) within every tile of 16384 packets, from a grouped copy in
 // `scratch` (group_scratch_bytes(pk, n) bytes of device memory, live until the launches have run:
 // stream-ordered).
 struct GroupArgs {
   uint8_t* scratch;
-  uint32_t src_bits;   // key = top src_bits of nw_src, then the top 8 - src_bits of nw_dst
+  uint32_t key;        // GPC_GROUP_KEY_ADDR or GPC_GROUP_KEY_SCAN (IPv4 batches)
+  uint32_t axes;       // SCAN: bit a = axis a is read by a sub-index of the image (group_axes)
+  uint32_t src_bits;   // ADDR: key = top src_bits of nw_src, then the top 8 - src_bits of nw_dst
   uint32_t xcd_order;  // 1: the blocks of one tile run on one XCD (classify.hip block_xcd_order)
   int32_t v6_bit;      // IPv6 batches: key = 8 bits of ipv6_src from this bit (0 = most significant)
 };

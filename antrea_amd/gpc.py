@@ -30,6 +30,8 @@ ACT_NAMES = ["NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "B
 
 # verdict dtype: gpc_verdict (8 B)
 VERDICT_DTYPE = np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"), ("flags", "u1")])
+GROUP_KEY_AUTO, GROUP_KEY_ADDR, GROUP_KEY_SCAN = 0, 1, 2  # gpc_group_key
+
 LB_DTYPE = np.dtype([("endpoint_ip", "<u4"), ("endpoint_port", "<u2"), ("flags", "u1"), ("reserved", "u1"),
                      ("group_id", "<u4"), ("out_port", "<u4")])
 LB_HIT, LB_NO_ENDPOINT, LB_DNAT, LB_REMOTE = 1, 2, 4, 8
@@ -41,7 +43,7 @@ class gpc_config(C.Structure):
     _fields_ = [("ipv4_enabled", C.c_int32), ("ipv6_enabled", C.c_int32), ("enable_antrea_policy", C.c_int32),
                 ("enable_deny_tracking", C.c_int32), ("cookie", C.c_uint64), ("device", C.c_int32),
                 ("compact_after", C.c_int32), ("ovs_meters", C.c_int32), ("external_node", C.c_int32),
-                ("group_packets", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("group_packets", C.c_int32), ("group_key", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 class gpc_addr(C.Structure):
@@ -344,13 +346,15 @@ class Classifier:
     """One gpc context (one GPU)."""
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
-                 cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True, group_packets=0):
+                 cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True, group_packets=0,
+                 group_key=0):
         self.lib = load()
         cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
                          enable_antrea_policy=int(enable_antrea_policy),
                          enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device,
                          compact_after=int(compact_after), ovs_meters=int(ovs_meters),
-                         external_node=int(not k8s_node), group_packets=int(group_packets))
+                         external_node=int(not k8s_node), group_packets=int(group_packets),
+                         group_key=int(group_key))
         h = C.c_void_p()
         _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
         self.h = h

@@ -132,8 +132,17 @@ typedef struct gpc_config {
                                     0 = batches of >= 2^18 packets against an image of >= 4 MB,
                                     > 0 = always, < 0 = never (gpc_classify6: only with the
                                     environment GPC_GROUP_V6=1, not yet measured)               */
-  int32_t reserved[3];
+  int32_t group_key;             /* grouping key of IPv4 batches (gpc_group_key; environment
+                                    GPC_GROUP_KEY overrides): 0 = per image, SCAN when waves' scan
+                                    lengths are very unequal (long driver lists), else ADDR       */
+  int32_t reserved[2];
 } gpc_config;
+
+/* Order a grouped batch is classified in, inside every tile of 16384 packets (results never depend
+   on it): ADDR = top bits of nw_src (then nw_dst; GPC_GROUP_SRC_BITS) -- lanes of a wavefront share
+   image lines; SCAN = the driver-list length each policy stage will scan -- lanes of a wavefront
+   finish their candidate scans together. */
+typedef enum gpc_group_key { GPC_GROUP_KEY_AUTO = 0, GPC_GROUP_KEY_ADDR = 1, GPC_GROUP_KEY_SCAN = 2 } gpc_group_key;
 
 typedef struct gpc_addr {        /* 24 bytes */
   uint8_t kind;                  /* gpc_addr_kind */

@@ -275,3 +275,14 @@ def test_get_match_flow_updates_reassign():
     assert not any("priority=100," in f or "priority=200," in f for f in ap)
     assert any("priority=101" in f and "nw_src=192.168.1.40" in f and "conjunction(10,1/2)" in f for f in ap)
     assert any("priority=202" in f and "conj_id=12" in f for f in ap)
+
+
+def test_group_key_config_validated():
+    """gpc_config.group_key: AUTO / ADDR / SCAN are accepted, anything else is -GPC_EINVAL at
+    gpc_create (no device work)."""
+    for k in (gpc.GROUP_KEY_AUTO, gpc.GROUP_KEY_ADDR, gpc.GROUP_KEY_SCAN):
+        gpc.Classifier(group_key=k)
+    for k in (-1, 3):
+        with pytest.raises(gpc.GpcError) as e:
+            gpc.Classifier(group_key=k)
+        assert e.value.code == gpc.GPC_EINVAL

@@ -1,8 +1,9 @@
 """GPU tier: the packet grouping pre-pass of gpc_classify (classify.hip group_*: counting sort of
-the batch by the top byte of nw_src, classification in grouped order, verdicts and LB results
-scattered back to caller order) is invisible in the results: verdicts, LB results and per-rule
-counters equal the ungrouped launch's exactly, for ragged batch sizes around the 8192-packet tile
-and with every optional packet column present."""
+every tile of the batch by a key -- the scan lengths of both policy stages, or the top byte of
+nw_src -- classification in grouped order, verdicts and LB results scattered back to caller order)
+is invisible in the results: verdicts, LB results and per-rule counters equal the ungrouped
+launch's exactly, for both keys, for ragged batch sizes around the 16384-packet tile and with every
+optional packet column present."""
 import copy
 import os
 
@@ -22,10 +23,14 @@ def _built():
     assert torch.cuda.is_available(), "GPU tier needs a HIP device"
 
 
-def _pair(wl, services=False):
+KEYS = [gpc.GROUP_KEY_SCAN, gpc.GROUP_KEY_ADDR]
+
+
+def _pair(wl, services=False, keys=(gpc.GROUP_KEY_SCAN,)):
+    """[plain, grouped with each key...]"""
     out = []
-    for g in (-1, 1):
-        c = gpc.Classifier(group_packets=g)
+    for g, k in [(-1, 0)] + [(1, k) for k in keys]:
+        c = gpc.Classifier(group_packets=g, group_key=k)
         c.initialize()
         c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
         if services:
@@ -53,11 +58,12 @@ def _optional_columns(cols, rng):
     return cols
 
 
-@pytest.mark.parametrize("n", [1, 63, 8191, 8192, 8193, 3 * 8192 + 5, (1 << 18) + 7])
-def test_grouped_equals_plain_ragged(n):
+@pytest.mark.parametrize("key", KEYS)
+@pytest.mark.parametrize("n", [1, 63, 16383, 16384, 16385, 3 * 16384 + 5, (1 << 18) + 7])
+def test_grouped_equals_plain_ragged(n, key):
     wl = workload.config1(seed=9)
     cols = workload.gen_packets(wl, n, seed=9)
-    plain, grouped = _pair(wl)
+    plain, grouped = _pair(wl, keys=(key,))
     a = plain.classify_host(cols, count=True)
     b = grouped.classify_host(cols, count=True)
     assert (a == b).all()
@@ -69,12 +75,27 @@ def test_grouped_equals_plain_optional_columns_c3():
     rng = np.random.default_rng(12)
     n = 150_000
     cols = _optional_columns(workload.gen_packets(wl, n, seed=12), rng)
-    plain, grouped = _pair(wl)
+    plain, *grouped = _pair(wl, keys=KEYS)
     a = plain.classify_host(cols, count=True)
-    b = grouped.classify_host(cols, count=True)
-    assert (a == b).all()
-    assert _metrics(plain) == _metrics(grouped)
+    for g in grouped:
+        b = g.classify_host(cols, count=True)
+        assert (a == b).all()
+        assert _metrics(plain) == _metrics(g)
     assert len(np.unique(a["action"])) >= 4
+
+
+def test_grouped_equals_plain_c2_lane_sort():
+    """C2: the plain launch regroups lanes inside each block (lane-sort kernels); the scan-key
+    grouped launch runs the plain kernels over tiles already ordered by scan length."""
+    wl = workload.config2()
+    n = 200_000
+    cols = workload.gen_packets(wl, n, seed=14)
+    plain, *grouped = _pair(wl, keys=KEYS)
+    a = plain.classify_host(cols, count=True)
+    for g in grouped:
+        b = g.classify_host(cols, count=True)
+        assert (a == b).all()
+        assert _metrics(plain) == _metrics(g)
 
 
 def test_grouped_equals_plain_services_lb():
@@ -82,12 +103,13 @@ def test_grouped_equals_plain_services_lb():
     wl = _svc_workload("C1", 61)
     n = 50_000
     cols = workload.gen_packets(wl, n, seed=13)
-    plain, grouped = _pair(wl, services=True)
+    plain, *grouped = _pair(wl, services=True, keys=KEYS)
     a, la = plain.classify_host(cols, count=True, lb=True)
-    b, lbb = grouped.classify_host(cols, count=True, lb=True)
-    assert (a == b).all() and (la == lbb).all()
     assert ((la["flags"] & gpc.LB_HIT) != 0).any()
-    assert _metrics(plain) == _metrics(grouped)
+    for g in grouped:
+        b, lbb = g.classify_host(cols, count=True, lb=True)
+        assert (a == b).all() and (la == lbb).all()
+        assert _metrics(plain) == _metrics(g)
 
 
 def test_grouped_device_stream_batch():
