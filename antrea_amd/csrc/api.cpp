@@ -1159,6 +1159,10 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   out->n_full_builds = ctx->n_full;
   out->n_delta_builds = ctx->n_delta;
   out->n_background_builds = ctx->n_bg;
+  if (ctx->cur.base) {
+    out->group_key = group_key(ctx);
+    out->lane_sort = ctx->cur.base->sort_table[0] | uint32_t(ctx->cur.base->sort_table[1]) << 8;
+  }
   for (int i = 0; i < 6; i++) {
     out->n_rules[i] = ctx->last.n_rules[i];
     out->n_hard[i] = ctx->last.n_hard[i];

@@ -96,7 +96,8 @@ class gpc_image_stats(C.Structure):
                 ("bytes_records", C.c_uint64), ("bytes_ext", C.c_uint64), ("bytes_bucket_offsets", C.c_uint64),
                 ("bytes_entries", C.c_uint64), ("bytes_hash", C.c_uint64), ("overlay_bytes", C.c_uint64),
                 ("n_overlay_rules", C.c_uint32), ("n_tombstones", C.c_uint32), ("n_full_builds", C.c_uint64),
-                ("n_delta_builds", C.c_uint64), ("n_background_builds", C.c_uint64)]
+                ("n_delta_builds", C.c_uint64), ("n_background_builds", C.c_uint64), ("group_key", C.c_uint32),
+                ("lane_sort", C.c_uint32)]
 
 
 class gpc_endpoint(C.Structure):
@@ -625,4 +626,5 @@ class Classifier:
                           "entries": st.bytes_entries, "hash": st.bytes_hash},
                 "overlay_bytes": st.overlay_bytes, "n_overlay_rules": st.n_overlay_rules,
                 "n_tombstones": st.n_tombstones, "n_full_builds": st.n_full_builds,
-                "n_delta_builds": st.n_delta_builds, "n_background_builds": st.n_background_builds}
+                "n_delta_builds": st.n_delta_builds, "n_background_builds": st.n_background_builds,
+                "group_key": st.group_key, "lane_sort": [st.lane_sort & 0xff, st.lane_sort >> 8]}

@@ -220,7 +220,7 @@ def main():
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
     ap.add_argument("--group", type=int, default=0,
-                    help="gpc_config.group_packets: 0 = auto (batches >= 2^18 grouped by nw_src), 1 = on, -1 = off")
+                    help="gpc_config.group_packets: 0 = auto (batches >= 2^18 against images >= 4 MB), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),
                     help="6: the workload's addresses embedded in fd00:10::/96, IPv6 packets (gpc_classify6)")
     args = ap.parse_args()
@@ -411,8 +411,10 @@ def main():
                    "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
                    "verdict_mix": mix, "build_s": round(t_build, 1),
-                   "packet_grouping": ("key: top %s bits of nw_src + %d of nw_dst, 16384-packet tiles" % (
+                   "packet_grouping": (("key: top %s bits of nw_src + %d of nw_dst, 16384-packet tiles" % (
                        os.environ.get("GPC_GROUP_SRC_BITS", "8"), 8 - int(os.environ.get("GPC_GROUP_SRC_BITS", "8"))))
+                       if st["group_key"] == gpc.GROUP_KEY_ADDR else
+                       "key: egress x ingress scan-length bins, 16384-packet tiles")
                    if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18 and st["device_bytes"] >= 4 << 20))
                    else "off"},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)

@@ -308,6 +308,8 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint32_t n_tombstones;         /* superseded or removed rule copies (base + journal)         */
   uint64_t n_full_builds, n_delta_builds;
   uint64_t n_background_builds;  /* full rebuilds done by the background compactor and installed */
+  uint32_t group_key;            /* gpc_group_key grouped IPv4 batches of this epoch use (ADDR/SCAN) */
+  uint32_t lane_sort;            /* lane-regrouping table per policy stage: egress | ingress << 8   */
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */

@@ -78,6 +78,16 @@ def main():
                 key = u(col) >> (32 - bits)
             tile_id = torch.arange(len(key), device=key.device) // int(t)
             perm = torch.argsort((tile_id << bits) | key, stable=True)
+        elif name.startswith("gxcd_"):  # gxcd_<col><bits>: global stable sort, XCD x runs the x-th eighth
+            col, bits = name[5:8], int(name[8:])
+            srt = torch.argsort((base[col].to(torch.int64) & 0xFFFFFFFF) >> (32 - bits), stable=True)
+            G = len(srt) // 64
+            q, r = G // 8, G % 8
+            b = torch.arange(G, device=srt.device)
+            x = b % 8
+            logical = x * q + torch.minimum(x, torch.full_like(x, r)) + b // 8
+            perm = (logical[:, None] * 64 + torch.arange(64, device=srt.device)[None, :]).reshape(-1)
+            perm = srt[perm]
         elif name.startswith("xcd_"):
             col, bits = name[4:7], int(name[7:])
             perm = xcd_perm(torch, (base[col].to(torch.int64) & 0xFFFFFFFF) >> (32 - bits))
