@@ -157,7 +157,9 @@ struct gpc_ctx {
   std::map<hipStream_t, StreamScratch> scratch;  // packet grouping buffers per stream (data)
   uint32_t group_key = GPC_GROUP_KEY_AUTO;                            // gpc_group_key (gpc_create)
   uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // GPC_GROUP_KEY_ADDR key bits (classify.hip)
-  uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 1, 0, 1);         // XCD-contiguous tiles
+  // block order of grouped batches (classify.hip logical_block; 64M packets, ms per step for orders
+  // 1 / 2 / 3: C2 16.04 / 15.66 / 15.77, C3 13.29 / 13.25 / 13.28, C4 14.57 / 14.16 / 14.06)
+  uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 2, 0, 3);
   // IPv6 grouping: implemented, not yet measured on the device -- opt in with GPC_GROUP_V6=1
   uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads

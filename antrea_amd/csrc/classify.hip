@@ -270,6 +270,25 @@ __device__ __forceinline__ uint64_t block_xcd_order() {
   return uint64_t(x) * q + (x < r ? x : r) + (b >> 3);
 }
 
+// Logical block of this workgroup for a grouped batch (GroupArgs.xcd_order):
+//   1: XCD-contiguous tiles (block_xcd_order);
+//   2: tile-interleaved -- workgroups running at the same time take the same position of many
+//      tiles (wave k of tiles t, t+1, ...), so the whole chip works on one key range at a time (the
+//      image lines of that address region stay in every L2), as after a global sort by key;
+//   3: as 2, with the tiles of XCD x = those with t % 8 == x (its verdict stores stay in its L2).
+// kTileBlocks workgroups per full tile; the blocks of a last partial tile keep their order.
+template <int kTileBlocks>
+__device__ __forceinline__ uint64_t logical_block(uint32_t mode) {
+  if (mode == 1) return block_xcd_order();
+  const uint32_t b = blockIdx.x, T = gridDim.x / kTileBlocks;
+  if (mode < 2 || T == 0 || b >= T * kTileBlocks) return b;
+  if (mode == 3 && (T & 7u) == 0) {
+    const uint32_t x = b & 7u, j = b >> 3, tx = T >> 3;
+    return uint64_t(x + 8u * (j % tx)) * kTileBlocks + j / tx;
+  }
+  return uint64_t(b % T) * kTileBlocks + b / T;
+}
+
 // kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
 // orig != null: a grouped batch (group_tiles_kernel): pk holds the grouped columns, lane i of the
 // logical block order classifies grouped packet i, whose caller index is orig[i].
@@ -283,7 +302,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   uint4* const mid6 = reinterpret_cast<uint4*>(midv);
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
-  const uint64_t block_base = (xcd_order ? block_xcd_order() : uint64_t(blockIdx.x)) * block_threads<kSort>();
+  const uint64_t block_base = logical_block<kGroupTile / block_threads<kSort>()>(xcd_order) * block_threads<kSort>();
   uint64_t i = block_base + threadIdx.x;
   if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
   if (i >= n) return;

@@ -561,6 +561,70 @@ constexpr int kLists = kIdxPerClause + 1;  // always list + sub-indexes of the d
 #endif
 constexpr int kScanUnroll = GPC_SCAN_UNROLL;  // entry loads in flight per lane in the candidate scan
 
+// One pass of the candidate scan over the first kL driver lists, flattened: entry j of the
+// sequence is entry j + dl[l] of the image for the list l holding it (dl[l] = first entry of list l
+// minus the entries of lists 0..l-1; upto[l] = cumulative end of list l). Every entry is loaded and
+// prefiltered with a branch-free body; the two smallest passing record offsets above `after` and
+// below `rH` (the two best-ranked candidates) are kept in c0 < c1; `more` = a third one passed.
+// kL = 2 (tables whose clauses have one sub-index, e.g. AddressGroup / ofport rules) locates an
+// entry with one compare instead of kLists - 1.
+template <int kL>
+GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const uint32_t* upto, uint32_t total,
+                       uint32_t after, uint32_t rH, uint32_t& c0, uint32_t& c1, bool& more) {
+  const Ent* E = reinterpret_cast<const Ent*>(im.blob);
+  c0 = c1 = 0xffffffffu;
+  more = false;
+  // wave-uniform trip count (the wave's longest candidate list); finished lanes read the zero
+  // entry at index 0 (offset 0 is never a record), so the body has no divergent branches.
+  // kScanUnroll entries are loaded before any is used: that many loads in flight per lane.
+  for (uint32_t j0 = 0; GPC_WAVE_ANY(j0 < total); j0 += kScanUnroll) {
+    Ent ev[kScanUnroll];
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; u++) {
+      const uint32_t j = j0 + u;
+      uint32_t d = dl[0];
+#pragma unroll
+      for (int l = 1; l < kL; l++) d = j >= upto[l - 1] ? dl[l] : d;
+      const uint32_t idx = j < total ? j + d : 0u;
+      GPC_TOUCH(&E[idx], 16);
+      GPC_STAT(4, j < total ? 1 : 0);
+      ev[u] = E[idx];
+    }
+    bool ps[kScanUnroll];
+    bool probe = false;
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; u++) {
+      const uint32_t off = ent_off(ev[u].x);
+      ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u]);
+      probe |= ps[u] & ((ev[u].x & 15u) - 8u < 7u);
+    }
+    // Probe entries that passed: exact membership of the packet in the non-driver point-set
+    // clause (point hash, both choices loaded before the compare), one entry slot at a time
+    // and only when a lane of the wave needs it.
+    if (GPC_WAVE_ANY(probe)) {
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; u++) {
+        const uint32_t pax = (ev[u].x & 15u) - 8u;
+        const bool need = ps[u] & (pax < 7u);
+        if (GPC_WAVE_ANY(need)) {
+          if (need) ps[u] = hash_contains(im, point_key(ent_off(ev[u].x), pax, p.ax[pax]));
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; u++) {
+      const uint32_t off = ent_off(ev[u].x);
+      const bool pass = ps[u];
+      const uint32_t v = pass ? off : 0xffffffffu;
+      const bool fresh = (v != 0xffffffffu) & (v != c0) & (v != c1);
+      more |= fresh & (c1 != 0xffffffffu);  // a third distinct survivor: one of them is dropped
+      const bool lt0 = fresh & (v < c0), lt1 = fresh & (v < c1);
+      c1 = lt0 ? c0 : (lt1 ? v : c1);
+      c0 = lt0 ? v : c0;
+    }
+  }
+}
+
 // One rule table (table = 1..6). All per-list merge state is indexed with compile-time indices
 // only (unrolled), so it stays in VGPRs.
 GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
@@ -626,21 +690,20 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   GPC_STAT(1, d1 ? cnt1 : cnt0);
   GPC_STAT(2, d1 ? cnt0 : cnt1);
   // Candidate scan. The driver lists (0 = always list, 1.. = sub-index buckets) are walked as one
-  // flattened sequence: every entry is loaded and prefiltered with a branch-free body, and only the
-  // two smallest passing record offsets (= the two best-ranked candidates) are kept. They are then
+  // flattened sequence (scan_lists), keeping the two best-ranked prefilter survivors. They are then
   // verified in rank order; if more candidates passed and no decision was reached, the lists are
   // rescanned above the last verified offset. Same result as a k-way merge in rank order.
-  const Ent* E = reinterpret_cast<const Ent*>(im.blob);
-  uint32_t base[kLists], upto[kLists];  // first entry index; cumulative end in the flattened scan
-  base[0] = th.always_off[d] / 4;
+  uint32_t dl[kLists], upto[kLists];  // entry index offset per list; cumulative end in the flattened scan
+  dl[0] = th.always_off[d] / 4;
   upto[0] = th.always_n[d];
 #pragma unroll
   for (int i = 0; i < kIdxPerClause; i++) {
     const uint32_t lo = d1 ? lo1[i] : lo0[i], hi = d1 ? hi1[i] : hi0[i];
-    base[i + 1] = lo;
+    dl[i + 1] = lo - upto[i];
     upto[i + 1] = upto[i] + (hi - lo);
   }
   const uint32_t total = upto[kLists - 1];
+  const bool one_idx = n0 <= 1 && n1 <= 1;  // table-uniform: every driver clause has <= 1 sub-index
   uint32_t after = 0;       // rescan bound (exclusive); record offsets are > 0
   int have = 0;             // result found
   uint32_t level = 0xffffffffu;
@@ -648,58 +711,10 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   uint32_t win = 0;         // winner record offset (soft) when have == 1 and !noact
   bool done = total == 0;
   while (!done) {
-    uint32_t c0 = 0xffffffffu, c1 = 0xffffffffu;
-    bool more = false;
-    // wave-uniform trip count (the wave's longest candidate list); finished lanes read the zero
-    // entry at index 0 (offset 0 is never a record), so the body has no divergent branches.
-    // kScanUnroll entries are loaded before any is used: that many loads in flight per lane.
-    for (uint32_t j0 = 0; GPC_WAVE_ANY(j0 < total); j0 += kScanUnroll) {
-      Ent ev[kScanUnroll];
-#pragma unroll
-      for (int u = 0; u < kScanUnroll; u++) {
-        const uint32_t j = j0 + u;
-        uint32_t idx = base[0] + j;
-#pragma unroll
-        for (int l = 1; l < kLists; l++)
-          if (j >= upto[l - 1]) idx = base[l] + (j - upto[l - 1]);
-        idx = j < total ? idx : 0u;
-        GPC_TOUCH(&E[idx], 16);
-        GPC_STAT(4, j < total ? 1 : 0);
-        ev[u] = E[idx];
-      }
-      bool ps[kScanUnroll];
-      bool probe = false;
-#pragma unroll
-      for (int u = 0; u < kScanUnroll; u++) {
-        const uint32_t off = ent_off(ev[u].x);
-        ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u]);
-        probe |= ps[u] & ((ev[u].x & 15u) - 8u < 7u);
-      }
-      // Probe entries that passed: exact membership of the packet in the non-driver point-set
-      // clause (point hash, both choices loaded before the compare), one entry slot at a time
-      // and only when a lane of the wave needs it.
-      if (GPC_WAVE_ANY(probe)) {
-#pragma unroll
-        for (int u = 0; u < kScanUnroll; u++) {
-          const uint32_t pax = (ev[u].x & 15u) - 8u;
-          const bool need = ps[u] & (pax < 7u);
-          if (GPC_WAVE_ANY(need)) {
-            if (need) ps[u] = hash_contains(im, point_key(ent_off(ev[u].x), pax, p.ax[pax]));
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kScanUnroll; u++) {
-        const uint32_t off = ent_off(ev[u].x);
-        const bool pass = ps[u];
-        const uint32_t v = pass ? off : 0xffffffffu;
-        const bool fresh = (v != 0xffffffffu) & (v != c0) & (v != c1);
-        more |= fresh & (c1 != 0xffffffffu);  // a third distinct survivor: one of them is dropped
-        const bool lt0 = fresh & (v < c0), lt1 = fresh & (v < c1);
-        c1 = lt0 ? c0 : (lt1 ? v : c1);
-        c0 = lt0 ? v : c0;
-      }
-    }
+    uint32_t c0, c1;
+    bool more;
+    if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, c0, c1, more);
+    else scan_lists<kLists>(im, p, dl, upto, total, after, rH, c0, c1, more);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
       const uint32_t off = q ? c1 : c0;

@@ -37,7 +37,7 @@ struct GroupArgs {
   uint32_t key;        // GPC_GROUP_KEY_ADDR or GPC_GROUP_KEY_SCAN (IPv4 batches)
   uint32_t axes;       // SCAN: bit a = axis a is read by a sub-index of the image (group_axes)
   uint32_t src_bits;   // ADDR: key = top src_bits of nw_src, then the top 8 - src_bits of nw_dst
-  uint32_t xcd_order;  // 1: the blocks of one tile run on one XCD (classify.hip block_xcd_order)
+  uint32_t xcd_order;  // block order (classify.hip logical_block): 1 = the blocks of one tile run on one XCD
   int32_t v6_bit;      // IPv6 batches: key = 8 bits of ipv6_src from this bit (0 = most significant)
 };
 uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6);
