@@ -5,7 +5,6 @@ is invisible in the results: verdicts, LB results and per-rule counters equal th
 launch's exactly, for both keys, for ragged batch sizes around the 16384-packet tile and with every
 optional packet column present."""
 import copy
-import os
 
 import numpy as np
 import pytest
@@ -184,10 +183,11 @@ def test_grouped_many_streams():
         assert torch.equal(o, ref)
 
 
-@pytest.mark.skipif(os.environ.get("GPC_GROUP_V6") != "1", reason="IPv6 grouping is opt-in (GPC_GROUP_V6=1)")
-@pytest.mark.parametrize("n", [1, 8191, 8193, 3 * 8192 + 5])
-def test_grouped_ipv6_equals_plain(n):
-    """IPv6 batches (gpc_classify6): grouped == plain, verdicts and counters, with ct_*6 columns."""
+@pytest.mark.parametrize("n", [1, 16383, 16385, 3 * 16384 + 5])
+def test_grouped_ipv6_equals_plain(n, monkeypatch):
+    """IPv6 batches (gpc_classify6): grouped == plain, verdicts and counters, with ct_*6 columns.
+    IPv6 grouping is opt-in (GPC_GROUP_V6=1, read at gpc_create): measured no faster on C3 in IPv6."""
+    monkeypatch.setenv("GPC_GROUP_V6", "1")
     wl = workload.config1(seed=9)
     w6 = workload.to_ipv6(wl, dual=True)
     rng = np.random.default_rng(n)
