@@ -376,15 +376,16 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
       return;
     }
   }
-  Pkt p(pkt_lds + threadIdx.x, block_threads<kSort>());
-  make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
-           pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
   View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
   if (kDelta) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
     if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
     im.n_img = 2u;
   }
+  Pkt p(pkt_lds + threadIdx.x, block_threads<kSort>());
+  make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
+           pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
+           view_bloom_axes(im));
   PacketOut o = classify_packet<kDelta, kStage>(im, p, dest, ct_mark);
   if (count && (o.ecounted || o.gcounted)) {
     const uint32_t len = pk.len ? pk.len[i] : 0u;
@@ -448,15 +449,16 @@ __global__ void trace_kernel(EpochArgs ep, gpc_pkt_soa pk, uint4* __restrict__ o
     }
   }
   lb_out[0] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
-  Pkt p(pkt_lds, 1);
-  make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[0] : 0u, svc_group,
-           pk.tun_id ? pk.tun_id[0] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
   View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
   if (ep.pool) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
     if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
     im.n_img = 2u;
   }
+  Pkt p(pkt_lds, 1);
+  make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[0] : 0u, svc_group,
+           pk.tun_id ? pk.tun_id[0] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
+           view_bloom_axes(im));
   const PacketOut o = classify_packet<true, 0, true>(im, p, dest, ct_mark, steps, n_steps);
   out[0] = make_uint4(o.e.conj, o.e.packed, o.g.conj, o.g.packed);
 }

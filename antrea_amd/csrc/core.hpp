@@ -121,6 +121,7 @@ struct ImageHdr {
   uint32_t n_slots;
   uint32_t v6_lpm;      // IPv6 image: word offset of its V6Lpm block (0 in IPv4 images)
   uint32_t isc;         // IngressSecurityClassifier bypasses installed (kIsc* bits)
+  uint32_t bloom_axes;  // bit a: some driver entry tests the Bloom bits of axis a (Pkt::fm[a] is needed)
 };
 // IngressSecurityClassifier (pipeline.go:2144-2182), from the installed flows: bit d (gpc_dest d =
 // gateway 1, tunnel 2, uplink 3) -- packets to that destination skip to IngressMetric; kIscHairpin
@@ -402,6 +403,7 @@ struct JournalHdr {
   uint32_t pt_off;         // page table: 2^(lg-8) words, word offset of each head page (0: empty)
   uint32_t bdead_off;      // base tombstones: page table (0: none), see rule_dead
   uint32_t odead_off;      // journal tombstones: page table (0: none)
+  uint32_t bloom_axes;     // as ImageHdr.bloom_axes, over every journal entry so far
   JournalTable t[6];
 };
 constexpr uint32_t kJEntWords = 8;
@@ -1157,11 +1159,20 @@ GPC_HD void make_axes(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32
   p.ax[AX_L4S] = (proto << 16) | (ported ? sport : 0u);
   p.ax[AX_CTST] = ct_state;
 }
+// Axes whose Bloom bits the entries of an epoch test (base image and journal): make_pkt hashes only
+// those (wave-uniform), the others are never read.
+GPC_HD uint32_t view_bloom_axes(const View& v) {
+  uint32_t m = v.base.hdr->bloom_axes;
+  if (v.n_img > 1) m |= reinterpret_cast<const JournalHdr*>(v.ovl.blob + v.jhdr)->bloom_axes;
+  return m;
+}
+// bloom_axes: bit a = compute the filter bits of axis a (view_bloom_axes; ~0u = all).
 GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto, uint32_t out_port,
-                     uint32_t in_port, uint32_t svc_group, uint32_t tun_id, uint32_t ct_src, uint32_t ct_dst, uint32_t ct_state) {
+                     uint32_t in_port, uint32_t svc_group, uint32_t tun_id, uint32_t ct_src, uint32_t ct_dst, uint32_t ct_state,
+                     uint32_t bloom_axes) {
   make_axes(p, src, dst, sport, dport, proto, out_port, in_port, svc_group, tun_id, ct_src, ct_dst, ct_state);
 #pragma unroll
-  for (uint32_t a = 0; a < 8; a++) p.fm[a] = filt_pkt_axis(a, p.ax[a]);
+  for (uint32_t a = 0; a < 8; a++) p.fm[a] = (bloom_axes >> a) & 1u ? filt_pkt_axis(a, p.ax[a]) : 0u;
   p.l4m = filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12) |
           filt_l4x_bit(proto_class(proto), p.ax[AX_L4D] & 0xffffu);
 }

@@ -756,6 +756,10 @@ std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint
   return {((off >> 4) << 8) | (ch.axis << 4) | axis, ipbits | l4bits, ch.lo, ch.hi};
 }
 
+// ImageHdr / JournalHdr bloom_axes bit of an entry's Bloom axis (core.hpp entry_pass reads
+// fm[x & 7] unless the axis field is kFiltNoAxis).
+uint32_t bloom_axis_bit(uint32_t x) { return (x & 15u) == kFiltNoAxis ? 0u : 1u << (x & 7u); }
+
 // Point hash (core.hpp hash_contains): 2-choice cuckoo hash of kHashSlots-slot 16-B buckets,
 // sized to <= 70 % load (random-walk insertion; a failed build retries with twice the buckets).
 bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vector<uint64_t>* tab) {
@@ -1161,6 +1165,7 @@ void Journal::reset(const HostImage* base, uint32_t lg) {
   hdr_off = 0;
   n_versions = n_live = 0;
   any_noact = false;
+  bloom_axes_ = 0;
   heads_.assign(size_t(1) << lg_, 0u);
   pt_.assign((size_t(1) << lg_) / kJPageHeads, 0u);
   bdead_.clear();
@@ -1304,6 +1309,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       JournalTable& jt = tables_[t - 1];
       for (int k = 0; k < 2 && k < r.n; k++) {
         const std::array<uint32_t, 4> pf = entry_of(r, k, 0u, span);
+        bloom_axes_ |= bloom_axis_bit(pf[0]);
         for (auto& a : r.clause[k]) {
           AtomKey key;
           const bool keyed = atom_key(a, &key) && journal_keys(key, &keys);
@@ -1354,6 +1360,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     dirty.clear();
     return append(pt.data(), pt.size(), 16);
   };
+  h.bloom_axes = bloom_axes_;
   h.bdead_off = publish(bdead_, bpt_, bdirty_, base_->n_rids);
   h.odead_off = publish(odead_, opt_, odirty_, n_versions);
   for (int t = 0; t < 6; t++) {
@@ -1507,6 +1514,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         RuleB& r = *rs[rank];
         if (r.hard || k >= r.n) continue;
         std::array<uint32_t, 4> ent = entry_of(r, k, rec_off[rank], span);
+        out->hdr.bloom_axes |= bloom_axis_bit(ent[0]);
         for (auto& a : r.clause[k]) {
           AtomKey key;
           if (!atom_key(a, &key)) {

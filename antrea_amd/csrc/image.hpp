@@ -87,6 +87,7 @@ class Journal {
   std::unordered_map<uint32_t, uint32_t> live_;  // conj -> journal rule id of its live version
   std::vector<uint32_t> hard_orids_[6], hard_offs_[6];
   JournalTable tables_[6];
+  uint32_t bloom_axes_ = 0;  // JournalHdr.bloom_axes
 };
 
 }  // namespace gpc

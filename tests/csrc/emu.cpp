@@ -60,7 +60,8 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
     uint32_t pst[kPktWords];
     Pkt p(pst, 1);
     make_pkt(p, src, dst, sport, dport, proto, out_port, pk->in_port ? pk->in_port[i] : 0u, svc_group,
-             pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+             pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst, pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
+             view_bloom_axes(im));
     g_lines.clear();
     g_line_site.clear();
     const unsigned long long v0 = ::gpc_emu_stats[3], s0 = ::gpc_emu_stats[4];
@@ -98,7 +99,8 @@ extern "C" int emu_trace(const uint32_t* blob, const void* hdr, const uint32_t* 
   Pkt p(pst, 1);
   make_pkt(p, src, dst, pk->sport[0], pk->dport[0], pk->proto[0], pk->out_port[0], pk->in_port ? pk->in_port[0] : 0u,
            pk->svc_group ? pk->svc_group[0] : 0u, pk->tun_id ? pk->tun_id[0] : 0u, pk->ct_src ? pk->ct_src[0] : src,
-           pk->ct_dst ? pk->ct_dst[0] : dst, pk->ct_state ? pk->ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+           pk->ct_dst ? pk->ct_dst[0] : dst, pk->ct_state ? pk->ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
+           view_bloom_axes(im));
   *n_steps = 0;
   PacketOut o = classify_packet<true, 0, true>(im, p, pk->dest ? pk->dest[0] : 0u, pk->ct_mark ? pk->ct_mark[0] : 0u, steps,
                                                n_steps);
@@ -138,7 +140,7 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pk
     Pkt p(pst, 1);
     make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
              pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst,
-             pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK));
+             pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK), view_bloom_axes(im));
     PacketOut o = classify_packet<false, 0>(im, p, dest, pk->ct_mark ? pk->ct_mark[i] : 0u);
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
