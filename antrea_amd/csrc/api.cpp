@@ -160,7 +160,7 @@ struct gpc_ctx {
   // block order of grouped batches (classify.hip logical_block; 64M packets, ms per step for orders
   // 1 / 2 / 3: C2 16.04 / 15.66 / 15.77, C3 13.29 / 13.25 / 13.28, C4 14.57 / 14.16 / 14.06)
   uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 2, 0, 3);
-  // IPv6 grouping: implemented, not yet measured on the device -- opt in with GPC_GROUP_V6=1
+  // IPv6 grouping: opt in with GPC_GROUP_V6=1 (C3 in IPv6, 64M packets: 31.57 ms plain, 31.69 grouped)
   uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;

@@ -71,12 +71,14 @@ def test_device_vs_oracle_fullscale(config, group):
     assert {1, 2} <= acts and (3 in acts or 5 in acts), acts
 
 
-@pytest.mark.parametrize("group", [-1, pytest.param(1, marks=pytest.mark.skipif(
-    os.environ.get("GPC_GROUP_V6") != "1", reason="IPv6 grouping is opt-in (GPC_GROUP_V6=1)"))], ids=["plain", "grouped"])
-def test_device_ipv6_vs_oracle_fullscale_c3(group):
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
+def test_device_ipv6_vs_oracle_fullscale_c3(group, monkeypatch):
     """gpc_classify6 on full C3 embedded in fd00:10::/96 (IPv6 image, device LPM) equals the C
     oracle's IPv4 verdicts of the same packets (the embedding preserves every match), with the
-    grouping pre-pass off and on (IPv6 key: the 8 ipv6_src bits above the shortest prefix)."""
+    grouping pre-pass off and on (IPv6 key: the 8 ipv6_src bits above the shortest prefix; IPv6
+    grouping is opt-in, GPC_GROUP_V6=1 read at gpc_create)."""
+    if group == 1:
+        monkeypatch.setenv("GPC_GROUP_V6", "1")
     f, wl, cols = _inputs("C3")
     c = _classifier(wl, ipv6=True, rules=workload.to_ipv6(wl).rules, group=group)
     got = c.classify6_host(workload.packets_to_v6(cols), count=True)
