@@ -160,6 +160,9 @@ struct gpc_ctx {
   // block order of grouped batches (classify.hip logical_block; 64M packets, ms per step for orders
   // 1 / 2 / 3: C2 16.04 / 15.66 / 15.77, C3 13.29 / 13.25 / 13.28, C4 14.57 / 14.16 / 14.06)
   uint32_t group_xcd = env_u32("GPC_GROUP_XCD", 2, 0, 3);
+  // ingress verdicts of a grouped batch stored in grouped order, then put in caller order by
+  // unpermute_kernel (1) or stored at the caller index by the ingress launch (0)
+  uint32_t group_unpermute = env_u32("GPC_GROUP_UNPERMUTE", 1, 0, 1);
   // IPv6 grouping: opt in with GPC_GROUP_V6=1 (C3 in IPv6, 64M packets: 31.57 ms plain, 31.69 grouped)
   uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
@@ -913,7 +916,7 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
   // the next batch on that stream (launches of one stream run in order), so callers on different
   // streams never share one and the data path does no allocation once warm
-  GroupArgs ga{nullptr, group_key(ctx), ctx->cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0};
+  GroupArgs ga{nullptr, group_key(ctx), ctx->cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0, ctx->group_unpermute};
   if (group_batch(ctx, n, ctx->cur.base->bytes))
     if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, false), &ga.scratch)) return e;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
@@ -999,7 +1002,7 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm, {0, 0},
                uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, ctx->cur.v6_bit};
+  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, ctx->cur.v6_bit, ctx->group_unpermute};
   if (ctx->group_v6 && group_batch(ctx, n, ctx->cur.v6->bytes))
     if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
   int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st);

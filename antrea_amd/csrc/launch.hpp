@@ -39,6 +39,7 @@ struct GroupArgs {
   uint32_t src_bits;   // ADDR: key = top src_bits of nw_src, then the top 8 - src_bits of nw_dst
   uint32_t xcd_order;  // block order (classify.hip logical_block): 1 = the blocks of one tile run on one XCD
   int32_t v6_bit;      // IPv6 batches: key = 8 bits of ipv6_src from this bit (0 = most significant)
+  uint32_t unpermute;  // 1: the ingress launch stores in grouped order, unpermute_kernel restores caller order
 };
 uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6);
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,

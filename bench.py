@@ -130,6 +130,9 @@ def _pmc_pass(counters, args):
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600, check=True)
         rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            if args.keep_pmc:  # the raw per-dispatch counter rows behind `roofline` (profiles/)
+                os.makedirs(args.keep_pmc, exist_ok=True)
+                shutil.copy(f, os.path.join(args.keep_pmc, "pmc_%s_%s.csv" % (args.config, "_".join(counters))))
             with open(f) as fh:
                 rows += [r for r in csv.DictReader(fh)
                          if "classify_kernel" in r.get("Kernel_Name", "") or "group_tiles" in r.get("Kernel_Name", "")]
@@ -217,6 +220,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed batch")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child passes")
+    ap.add_argument("--keep-pmc", default="", help="directory that keeps the PMC passes' counter CSVs")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
     ap.add_argument("--group", type=int, default=0,
