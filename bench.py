@@ -418,7 +418,9 @@ def main():
                    "packet_grouping": (("key: top %s bits of nw_src + %d of nw_dst, 16384-packet tiles" % (
                        os.environ.get("GPC_GROUP_SRC_BITS", "8"), 8 - int(os.environ.get("GPC_GROUP_SRC_BITS", "8"))))
                        if st["group_key"] == gpc.GROUP_KEY_ADDR else
-                       "key: egress x ingress scan-length bins, 16384-packet tiles")
+                       "key: egress x ingress scan-length bins, 16384-packet tiles") +
+                   (", ingress verdicts un-permuted" if os.environ.get("GPC_GROUP_UNPERMUTE", "1") != "0"
+                    and not getattr(wl, "services", None) else "")
                    if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18 and st["device_bytes"] >= 4 << 20))
                    else "off"},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)

@@ -39,12 +39,12 @@ for s in $STEPS; do
       tail -1 "$O/smoke.log" ;;
     bench)
       step bench
-      timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
+      timeout -k 10 900 python -u bench.py --keep-pmc "$O/pmc_bench" > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
       cat "$O/bench.json" ;;
     cfg:*)
       c=${s#cfg:}; step "bench $c"
       if [ "$c" = v6 ]; then a="--family 6"; else a="--config $c"; fi
-      timeout -k 10 900 python -u bench.py $a > "$O/bench_$c.json" 2> "$O/bench_$c.err" || { tail -20 "$O/bench_$c.err"; exit 1; }
+      timeout -k 10 900 python -u bench.py $a --keep-pmc "$O/pmc_bench" > "$O/bench_$c.json" 2> "$O/bench_$c.err" || { tail -20 "$O/bench_$c.err"; exit 1; }
       cat "$O/bench_$c.json" ;;
     kt)
       step "rocprof kernel trace"
