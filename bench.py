@@ -118,7 +118,7 @@ def _pmc_pass(counters, args):
     if not shutil.which("rocprofv3"):
         return None
     d = tempfile.mkdtemp(prefix="gpc_pmc_")
-    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel|group_tiles", "-d", d, "-o", "pmc",
+    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel|group_tiles|unpermute", "-d", d, "-o", "pmc",
                                                        "--output-format", "csv", "--", sys.executable,
                                                        os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
                                                        "--no-cpu-baseline", "--no-traffic", "--no-parity", "--config",
@@ -135,9 +135,10 @@ def _pmc_pass(counters, args):
                 shutil.copy(f, os.path.join(args.keep_pmc, "pmc_%s_%s.csv" % (args.config, "_".join(counters))))
             with open(f) as fh:
                 rows += [r for r in csv.DictReader(fh)
-                         if "classify_kernel" in r.get("Kernel_Name", "") or "group_tiles" in r.get("Kernel_Name", "")]
+                         if re.search(r"classify_kernel|group_tiles|unpermute", r.get("Kernel_Name", ""))]
         # one step = the grouping launch (if grouped) + two classify launches without Services
-        # (egress stage, ingress stage) or one with them: steps = dispatches of the first classify stage
+        # (egress stage, ingress stage) or one with them (+ the un-permute launch of a grouped batch
+        # without Services): steps = dispatches of the first classify stage
         first = [r for r in rows if re.search(r"classify_kernel<\w+, \w+, [01],", r.get("Kernel_Name", ""))]
         steps = len({r.get("Dispatch_Id") for r in first}) or 1
         out, by_kernel = {}, {}
@@ -181,7 +182,7 @@ def _roofline(pmc, kern_ms, n, b_in, b_out, lbar):
     pps_kernel = n / (kern_ms / 1e3)
     b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
     rl = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-          "basis": "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per step (grouping + classify launches) / HIP-event kernel time"}
+          "basis": "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per step (grouping, classify and un-permute launches) / HIP-event kernel time"}
     f, w = pmc.get("FETCH_SIZE"), pmc.get("WRITE_SIZE")
     if f is not None and w is not None:
         traffic = (2.0 * f + w) * 1024.0  # counters are in KB

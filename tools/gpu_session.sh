@@ -22,7 +22,7 @@ step() { echo "== $1 ($(date +%T))"; }
 KT_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-traffic --no-parity"
 pmc() {  # name, config, counters...
   local name=$1 cfg=$2; shift 2
-  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex classify -d "$O/pmc_${name}_$cfg" -o pmc \
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex "classify|unpermute" -d "$O/pmc_${name}_$cfg" -o pmc \
     --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-traffic --no-parity \
     --config $cfg > "$O/pmc_${name}_$cfg.log" 2>&1
 }
