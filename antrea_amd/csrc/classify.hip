@@ -296,7 +296,7 @@ template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = fal
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, void* __restrict__ midv,
-    uint32_t xcd_order, uint4* __restrict__ gout) {
+    uint32_t xcd_order, uint2* __restrict__ gout) {
   // grouped batches: the egress launch's result in grouped order (IPv6: 16 B, the address codes too)
   uint2* const mid = reinterpret_cast<uint2*>(midv);
   uint4* const mid6 = reinterpret_cast<uint4*>(midv);
@@ -321,11 +321,12 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   }
   // caller index of this packet (loaded where a result is stored: no register held over the walk)
   auto at = [&]() -> uint64_t { return orig ? uint64_t(orig[i]) : i; };
-  // the ingress launch's verdict pair: in grouped order into gout (unpermute_kernel puts it in
-  // caller order with full-line stores), else at the caller index
-  auto store2 = [&](uint4 v) {
-    if (gout) gout[i] = v;
-    else out[at()] = v;
+  // the ingress launch's result: its half of the verdict pair in grouped order into gout
+  // (unpermute_kernel joins it with the egress half in mid and stores the pair in caller order with
+  // whole-line stores), else the pair at the caller index
+  auto store2 = [&](uint32_t conj, uint32_t packed) {
+    if (gout) gout[i] = make_uint2(conj, packed);
+    else out[at()] = make_uint4(prev.x, prev.y, conj, packed);
   };
   if (kV6) {
     // The egress launch computes the src / dst codes (both LPMs in lock step) and parks them in the
@@ -374,11 +375,11 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
     const uint32_t ea = prev.y & 0xffu;
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
-      if (kV6 || orig) store2(make_uint4(prev.x, prev.y, 0u, 0u));  // ingress NONE (over the parked codes)
+      if (kV6 || orig) store2(0u, 0u);  // ingress NONE (over the parked codes)
       return;
     }
     if (const uint32_t b = ingress_bypass(ep.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
-      store2(make_uint4(prev.x, prev.y, 0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u)));
+      store2(0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
       return;
     }
   }
@@ -399,21 +400,24 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&copy[w], v); });
   }
   const VerdictOut e = o.e, g = o.g;
-  if (kStage == 2) store2(make_uint4(prev.x, prev.y, g.conj, g.packed));
+  if (kStage == 2) store2(g.conj, g.packed);
   else if (kV6 && kStage == 1 && orig) mid6[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
   else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);
   else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
   else out[at()] = make_uint4(e.conj, e.packed, g.conj, g.packed);  // ingress NONE until the second launch
 }
 
-// Ingress verdict pairs of a grouped batch from grouped order (gout, written by the ingress launch
-// with coalesced stores) to caller order: one 1024-thread block per grouping tile, each half of the
-// tile's caller range assembled in LDS (128 KB of 16-B pairs) from the tile's grouped pairs, then
-// written out with whole-line stores. Replaces the ingress launch's 16-B stores scattered over the
-// tile (C3: 0.75 ms of 13.3 per 64M packets) by 2 x 20 B of L2-served reads and 16 B of writes.
+// Verdict pairs of a grouped batch in caller order: the egress half from mid (grouped order, every
+// mid_words words) and the ingress half from gout (grouped order, both written with coalesced
+// stores by the two classification launches) joined and stored at the caller index. One
+// 1024-thread block per grouping tile; each half of the tile's caller range is assembled in LDS
+// (128 KB of 16-B pairs, loads four deep per thread) and written with whole-line stores. Replaces
+// the ingress launch's 16-B stores scattered over the tile (C3: 0.84 ms of 13.5 per 64M packets).
 constexpr uint32_t kUnpermHalf = kGroupTile / 2;
-__global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint4* __restrict__ gout, const uint32_t* __restrict__ orig,
-                                                                  uint64_t n, uint4* __restrict__ out) {
+__global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint32_t* __restrict__ mid, uint32_t mid_words,
+                                                                  const uint2* __restrict__ gout,
+                                                                  const uint32_t* __restrict__ orig, uint64_t n,
+                                                                  uint4* __restrict__ out) {
   __shared__ uint4 buf[kUnpermHalf];
   const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
   const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
@@ -433,8 +437,9 @@ __global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint4* _
       for (int u = 0; u < kU; u++) {
         x[u] = y[u] = z[u] = w[u] = 0;
         if (d[u] < cnt) {
-          const uint4 v = gout[base + k0 + u * kGroupThreads];
-          x[u] = v.x, y[u] = v.y, z[u] = v.z, w[u] = v.w;
+          const uint64_t k = base + k0 + u * kGroupThreads;
+          const uint2 e = *reinterpret_cast<const uint2*>(mid + k * mid_words), g = gout[k];
+          x[u] = e.x, y[u] = e.y, z[u] = g.x, w[u] = g.y;
         }
       }
 #pragma unroll
@@ -459,14 +464,16 @@ __global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint4* _
   }
 }
 
-static void launch_unpermute(const uint4* gout, const uint32_t* orig, uint64_t n, uint4* out, hipStream_t stream) {
+static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* gout, const uint32_t* orig, uint64_t n,
+                             uint4* out, hipStream_t stream) {
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
-  hipLaunchKernelGGL(unpermute_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, gout, orig, n, out);
+  hipLaunchKernelGGL(unpermute_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream,
+                     reinterpret_cast<const uint32_t*>(mid), mid_words, gout, orig, n, out);
 }
 
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                   unsigned long long* counters, int count, const uint32_t* orig, void* mid, uint32_t xo, uint4* gout,
+                   unsigned long long* counters, int count, const uint32_t* orig, void* mid, uint32_t xo, uint2* gout,
                    hipStream_t stream) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   uint4* const o = reinterpret_cast<uint4*>(out);
@@ -575,13 +582,13 @@ uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6) {
   per += v6 ? 32 + (pk.ct_src6 ? 16 : 0) + (pk.ct_dst6 ? 16 : 0) : 8 + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0);
   per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) +
          (pk.ct_state ? 1 : 0) + (pk.dest ? 1 : 0) + (pk.len ? 2 : 0) + (pk.ct_mark ? 1 : 0);
-  per += 16;  // gout: the ingress verdict pairs in grouped order (GroupArgs.unpermute)
+  per += 8;  // gout: the ingress halves of the verdict pairs in grouped order (GroupArgs.unpermute)
   return per * n + 25 * 256;  // every region 256-B aligned
 }
 
 // Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
 static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group,
-                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint4** gout) {
+                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint2** gout) {
   if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120 || (group.key != GPC_GROUP_KEY_ADDR && group.key != GPC_GROUP_KEY_SCAN)) return -GPC_EINVAL;
   uint8_t* q = group.scratch;
   auto take = [&](uint64_t bytes) {
@@ -592,7 +599,7 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
   *g = gpc_pkt_soa{};
   *mid = take((v6 ? 16 : 8) * n);
   *orig = reinterpret_cast<uint32_t*>(take(4 * n));
-  *gout = reinterpret_cast<uint4*>(take(16 * n));
+  *gout = reinterpret_cast<uint2*>(take(8 * n));
   if (v6) {
     g->src6 = take(16 * n);
     g->dst6 = take(16 * n);
@@ -636,7 +643,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   uint32_t* orig = nullptr;
   void* mid = nullptr;
   uint32_t xo = 0;
-  uint4* gout = nullptr;
+  uint2* gout = nullptr;
   if (group) {
     if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid, &gout)) return rc;
     xo = group->xcd_order;
@@ -647,7 +654,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
                      reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, nullptr);
   hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
                      reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, gout);
-  if (gout) launch_unpermute(gout, orig, n, reinterpret_cast<uint4*>(out), stream);
+  if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
@@ -660,7 +667,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   uint32_t* orig = nullptr;
   void* mid = nullptr;
   uint32_t xo = 0;
-  uint4* gout = nullptr;
+  uint2* gout = nullptr;
   if (group) {
     if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid, &gout)) return rc;
     xo = group->xcd_order;
@@ -674,7 +681,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
   else if (svc) launch<false, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
   else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
-  if (gout) launch_unpermute(gout, orig, n, reinterpret_cast<uint4*>(out), stream);
+  if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
