@@ -1,0 +1,177 @@
+"""Replay one e2e reachability case (tests/golden/e2e_reachability.json) through the oracle and
+the product (TEST INFRASTRUCTURE ONLY).
+
+Per step: apply the step's resources to the model controller, let one model reconciler drive
+the oracle compiler and another drive the product (`gpc.Classifier`) through the same
+openflow.Client calls, publish the product epoch, build one packet per (Pod pair, port) and
+classify it with
+
+* the Python OVS oracle over the oracle compiler's flow dump (always), and
+* the product: `backend="emu"` = host emulation of the kernel body over the committed image
+  (tests/csrc/emu.cpp, same core.hpp as the device), `backend="device"` = gpc_classify /
+  gpc_classify6 on the GPU.
+
+Returned per step: the expected marks (reference), the oracle's and the product's marks, the raw
+verdicts of both, the evaluation checks and the reconciler's call log.
+"""
+from __future__ import annotations
+
+import copy
+import ipaddress
+
+import numpy as np
+
+from antrea_amd import gpc
+from oracle import compiler as oc
+from oracle import ovs_cls
+from tests import e2e_model as em
+
+CT_NEW_TRK = ovs_cls.CT_NEW | ovs_cls.CT_TRK
+
+
+def universe(case):
+    u = case["universe"]
+    if u == "xyz":
+        return em.Universe({"x": {}, "y": {}, "z": {}})
+    if "namespaces" in u:
+        return em.Universe(u["namespaces"], [tuple(p) for p in u["pods"]], family=u.get("family", 4))
+    return em.Universe(u)
+
+
+def _pairs(uni, expected):
+    """Probed pairs: every non-self pair (a Pod's probe of its own IP never leaves its network
+    namespace, so it is not a classifier case; the reference sets those cells Connected)."""
+    return sorted((a, b) for (a, b) in expected if a != b)
+
+
+def _columns(uni, pkts):
+    n = len(pkts)
+    cols = {"sport": np.full(n, em.EPHEMERAL_SPORT, np.uint16),
+            "dport": np.array([p["port"] for p in pkts], np.uint16),
+            "proto": np.array([p["proto"] for p in pkts], np.uint8),
+            "out_port": np.array([uni.ofport[p["dst"]] for p in pkts], np.uint32),
+            "in_port": np.array([uni.ofport[p["src"]] for p in pkts], np.uint32),
+            "ct_state": np.full(n, CT_NEW_TRK, np.uint8)}
+    if uni.family == 4:
+        cols["src"] = np.array([int(ipaddress.ip_address(uni.ip[p["src"]])) for p in pkts], np.uint32)
+        cols["dst"] = np.array([int(ipaddress.ip_address(uni.ip[p["dst"]])) for p in pkts], np.uint32)
+    else:
+        for k in ("src", "dst"):
+            cols[k + "6"] = np.array([list(ipaddress.ip_address(uni.ip[p[k]]).packed) for p in pkts], np.uint8)
+    return cols
+
+
+def _oracle(pipe, uni, pkts):
+    out = []
+    for p in pkts:
+        d = {"src": int(ipaddress.ip_address(uni.ip[p["src"]])), "dst": int(ipaddress.ip_address(uni.ip[p["dst"]])),
+             "sport": em.EPHEMERAL_SPORT, "dport": p["port"], "proto": p["proto"], "out_port": uni.ofport[p["dst"]],
+             "in_port": uni.ofport[p["src"]], "ct_state": CT_NEW_TRK, "dest": ovs_cls.DEST_POD}
+        if uni.family == 6:
+            d["eth"] = 0x86DD
+        e, i = pipe.classify(d)
+        out.append((e, i))
+    return out
+
+
+def _product(clf, uni, cols, backend):
+    if backend == "emu":
+        from tests import emu
+        v = emu.classify(clf, cols) if uni.family == 4 else emu.classify6(clf, cols)
+    elif uni.family == 4:
+        v = clf.classify_host(cols)
+    else:
+        v = clf.classify6_host(cols)
+    return [tuple((int(v[i, j]["action"]), int(v[i, j]["conj_id"]), int(v[i, j]["table"]), int(v[i, j]["tier"]),
+                   int(v[i, j]["flags"])) for j in range(2)) for i in range(len(v))]
+
+
+def _marks(pairs, ports, verdicts):
+    out = {}
+    k = 0
+    for pr in pairs:
+        ms = set()
+        for _ in ports:
+            e, i = verdicts[k]
+            ms.add(em.connectivity(e[0], i[0]))
+            k += 1
+        out[pr] = ms.pop() if len(ms) == 1 else em.ERROR
+    return out
+
+
+def _publish(clf, backend, compact=False):
+    if backend == "emu":
+        from tests import emu
+        emu.commit_host(clf, full=compact)
+    elif compact:
+        clf.compact()
+    else:
+        clf.commit()
+
+
+def run_case(case, backend="emu", compact_last=True):
+    uni = universe(case)
+    fam4 = uni.family == 4
+    ctrl = em.Controller(uni)
+    fnp = oc.FeatureNetworkPolicy(ipv4=fam4, ipv6=not fam4)
+    fnp.initialize()
+    clf = gpc.Classifier(ipv4=fam4, ipv6=not fam4)
+    clf.initialize()
+    rec_o, rec_p = em.Reconciler(fnp, uni), em.Reconciler(clf, uni)
+    for r in case["base"]:
+        ctrl.apply(copy.deepcopy(r))
+    steps = []
+    nsteps = len(case["steps"])
+    for si, st in enumerate(case["steps"]):
+        for r in st["apply"]:
+            ctrl.apply(copy.deepcopy(r))
+        rules = ctrl.rules()
+        n_log = len(rec_p.log)
+        rec_o.sync(rules)
+        rec_p.sync(rules)
+        _publish(clf, backend)
+        expected = {(a, b): v for a, b, v in st["expected"]}
+        probes = [op for op in st["reach"] if op[0] == "probe"]
+        if probes:
+            pairs = sorted((op[1], op[2]) for op in probes)
+            ports = sorted({op[3] for op in probes})
+        else:
+            pairs, ports = _pairs(uni, expected), st["ports"]
+        pkts = em.probe_packets(uni, pairs, ports, st["protocol"])
+        cols = _columns(uni, pkts)
+        pipe = ovs_cls.Pipeline(fnp.dump_flows(), rec_o.conj_tier)
+        want = _oracle(pipe, uni, pkts)
+        phases = [("delta", _product(clf, uni, cols, backend))]
+        if compact_last and si == nsteps - 1:
+            _publish(clf, backend, compact=True)
+            phases.append(("compacted", _product(clf, uni, cols, backend)))
+        ev = []
+        for src, dst, name, action in st["eval"]:
+            k = pairs.index((src, dst)) * len(ports)
+            e, i = phases[0][1][k]
+            d = em.deciding(e, i)
+            got_name = None
+            if d is not None and d[1]:
+                found, ref, _, _, _ = clf.get_policy_info_from_conjunction(d[1])
+                got_name = ref[2] if found else "?"
+            ev.append({"src": src, "dst": dst, "want": [name, action], "action": None if d is None else d[0],
+                       "conj": None if d is None else d[1], "policy": got_name})
+        steps.append({"name": st["name"], "pairs": pairs, "ports": ports, "expected": {p: expected[p] for p in pairs},
+                      "oracle": _marks(pairs, ports, want), "oracle_verdicts": want,
+                      "product": {ph: (_marks(pairs, ports, v), v) for ph, v in phases}, "eval": ev,
+                      "flows_equal": sorted(clf.dump_flows()) == sorted(fnp.dump_flows()),
+                      "calls": rec_p.log[n_log:]})
+    clf.close()
+    return steps
+
+
+def check_eval(e):
+    """An NPEvaluation assertion against the data path's deciding verdict."""
+    name, action = e["want"]
+    if action == "<NONE>":
+        return e["action"] is None
+    if e["action"] != em.EVAL_ACTION[action]:
+        return False
+    if action == "Isolate":  # K8s isolation drop: no conjunction carries the policy (DefaultRule table)
+        return e["conj"] == 0
+    return e["policy"] == name
