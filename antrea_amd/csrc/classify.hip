@@ -10,6 +10,11 @@
 #include "gpc.h"
 #include "launch.hpp"
 
+// group_tiles_kernel (141 KB) and unpermute_kernel (128 KB) size their LDS for gfx950's 160 KB.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "classify.hip is written for gfx950 (CDNA4: 160 KB LDS per workgroup)"
+#endif
+
 namespace gpc {
 
 #ifndef GPC_WAVES_PER_EU
@@ -307,33 +312,48 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   uint32_t src, dst, ct_src, ct_dst;
-  uint4 prev = make_uint4(0u, 0u, 0u, 0u);
+  // Ingress launch: only the egress action (and, IPv6, the parked address codes) of the egress
+  // half is read here; nothing of it is held over the walk (the result is stored as a half).
+  uint32_t ea = 0, code_s = 0, code_d = 0;
   if (kStage == 2) {
+    uint4 prev;
     if (orig && kV6) {
       prev = mid6[i];
     } else if (orig) {
       const uint2 v = mid[i];
-      prev.x = v.x;
-      prev.y = v.y;
-    } else {
+      prev = make_uint4(v.x, v.y, 0u, 0u);
+    } else if (kV6) {
       prev = out[i];
+    } else {
+      const uint2 v = reinterpret_cast<const uint2*>(out)[2 * i];
+      prev = make_uint4(v.x, v.y, 0u, 0u);
     }
+    ea = prev.y & 0xffu;
+    code_s = prev.z;
+    code_d = prev.w;
   }
   // caller index of this packet (loaded where a result is stored: no register held over the walk)
   auto at = [&]() -> uint64_t { return orig ? uint64_t(orig[i]) : i; };
   // the ingress launch's result: its half of the verdict pair in grouped order into gout
   // (unpermute_kernel joins it with the egress half in mid and stores the pair in caller order with
-  // whole-line stores), else the pair at the caller index
+  // whole-line stores); ungrouped, the ingress half of the pair the egress launch stored; grouped
+  // without the un-permute, the pair at the caller index with the egress half re-read from mid
   auto store2 = [&](uint32_t conj, uint32_t packed) {
-    if (gout) gout[i] = make_uint2(conj, packed);
-    else out[at()] = make_uint4(prev.x, prev.y, conj, packed);
+    if (gout) {
+      gout[i] = make_uint2(conj, packed);
+    } else if (orig) {
+      const uint2 e = kV6 ? make_uint2(mid6[i].x, mid6[i].y) : mid[i];
+      out[at()] = make_uint4(e.x, e.y, conj, packed);
+    } else {
+      reinterpret_cast<uint2*>(out)[2 * i + 1] = make_uint2(conj, packed);
+    }
   };
   if (kV6) {
     // The egress launch computes the src / dst codes (both LPMs in lock step) and parks them in the
     // still empty ingress half of the verdict pair; the ingress launch takes them from there.
     if (kStage == 2) {
-      src = prev.z;
-      dst = prev.w;
+      src = code_s;
+      dst = code_d;
     } else {
       uint32_t sd[2];
       v6_code_pair(ep, pk.src6, pk.dst6, i, sd);
@@ -373,7 +393,6 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     lb_out[at()] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
-    const uint32_t ea = prev.y & 0xffu;
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
       if (kV6 || orig) store2(0u, 0u);  // ingress NONE (over the parked codes)
       return;
@@ -393,18 +412,43 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
            pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
            view_bloom_axes(im));
-  PacketOut o = classify_packet<kDelta, kStage>(im, p, dest, ct_mark);
-  if (count && (o.ecounted || o.gcounted)) {
+  auto count_one = [&](const StageOut& s) {  // a stage's Metric-table counters
+    if (!count || !s.counted) return;
     const uint32_t len = pk.len ? pk.len[i] : 0u;
     unsigned long long* const copy = counters + size_t(blockIdx.x & ep.ctr_mask) * ep.ctr_stride;
-    count_packet(o, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&copy[w], v); });
+    count_stage(s.v, s.slot, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&copy[w], v); });
+  };
+  if constexpr (kStage == 0) {
+    // Both stages in one launch (Services): the egress half is counted and stored before the
+    // ingress walk, so nothing of it is held over that walk.
+    const uint32_t byp = ingress_bypass(ep.hdr->isc, dest, ct_mark);
+    const StageOut s1 = walk_stage<kDelta, false>(im, p, 1u, nullptr, nullptr);
+    count_one(s1);
+    uint2* const o2 = reinterpret_cast<uint2*>(out);
+    o2[2 * at()] = make_uint2(s1.v.conj, s1.v.packed);
+    const uint32_t a1 = s1.v.packed & 0xffu;
+    uint32_t gc = 0u, gp = 0u;  // ingress NONE: dropped in egress
+    if (a1 != RV_DROP && a1 != RV_REJECT && a1 != RV_ISO_DROP) {
+      if (byp) {  // IngressSecurityClassifier
+        gp = pack_verdict(byp & 0xffu, 0, 0, (byp >> 8) ? 2u : 0u);
+      } else {
+        const StageOut s2 = walk_stage<kDelta, false>(im, p, 4u, nullptr, nullptr);
+        count_one(s2);
+        gc = s2.v.conj;
+        gp = s2.v.packed;
+      }
+    }
+    o2[2 * at() + 1] = make_uint2(gc, gp);
+    return;
   }
-  const VerdictOut e = o.e, g = o.g;
+  const StageOut s = walk_stage<kDelta, false>(im, p, kStage == 2 ? 4u : 1u, nullptr, nullptr);
+  count_one(s);
+  const VerdictOut e = s.v, g = s.v;
   if (kStage == 2) store2(g.conj, g.packed);
   else if (kV6 && kStage == 1 && orig) mid6[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
   else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);
   else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
-  else out[at()] = make_uint4(e.conj, e.packed, g.conj, g.packed);  // ingress NONE until the second launch
+  else out[i] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
 }
 
 // Verdict pairs of a grouped batch in caller order: the egress half from mid (grouped order, every
@@ -465,8 +509,9 @@ __global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint32_t
 }
 
 static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* gout, const uint32_t* orig, uint64_t n,
-                             uint4* out, hipStream_t stream) {
+                             uint4* out, hipStream_t stream, LaunchMarks* marks) {
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
+  launch_mark(marks, kLaunchUnpermute, stream);
   hipLaunchKernelGGL(unpermute_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream,
                      reinterpret_cast<const uint32_t*>(mid), mid_words, gout, orig, n, out);
 }
@@ -474,21 +519,24 @@ static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* g
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                    unsigned long long* counters, int count, const uint32_t* orig, void* mid, uint32_t xo, uint2* gout,
-                   hipStream_t stream) {
+                   hipStream_t stream, LaunchMarks* marks) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   uint4* const o = reinterpret_cast<uint4*>(out);
   if (kSvc) {
+    launch_mark(marks, kLaunchBoth, stream);
     hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
                        lb_out, counters, count, orig, mid, xo, nullptr);
     return;
   }
   const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
+  launch_mark(marks, kLaunchEgress, stream);
   if (ep.sort_table[0])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
                        ep, pk, n, o, lb_out, counters, count, orig, mid, xo, nullptr);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
                        lb_out, counters, count, orig, mid, xo, nullptr);
+  launch_mark(marks, kLaunchIngress, stream);
   if (ep.sort_table[1])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
                        ep, pk, n, o, lb_out, counters, count, orig, mid, xo, gout);
@@ -588,7 +636,7 @@ uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6) {
 
 // Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
 static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group,
-                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint2** gout) {
+                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint2** gout, LaunchMarks* marks) {
   if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120 || (group.key != GPC_GROUP_KEY_ADDR && group.key != GPC_GROUP_KEY_SCAN)) return -GPC_EINVAL;
   uint8_t* q = group.scratch;
   auto take = [&](uint64_t bytes) {
@@ -629,13 +677,15 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
   else in.src6 = in.dst6 = in.ct_src6 = in.ct_dst6 = nullptr;
   if (!group.unpermute) *gout = nullptr;
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
+  launch_mark(marks, kLaunchGroup, stream);
   hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, ep, in, n, group.key,
                      group.axes, group.src_bits, v6 ? group.v6_bit : -1, *g, *orig);
   return 0;
 }
 
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
-                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream) {
+                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
+                     LaunchMarks* marks) {
   if (n == 0) return 0;
   if (n > kMaxPackets) return -GPC_EINVAL;
   gpc_pkt_soa g;
@@ -645,21 +695,25 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   uint32_t xo = 0;
   uint2* gout = nullptr;
   if (group) {
-    if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid, &gout)) return rc;
+    if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid, &gout, marks)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  launch_mark(marks, kLaunchEgress, stream);
   hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
                      reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, nullptr);
+  launch_mark(marks, kLaunchIngress, stream);
   hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
                      reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, gout);
-  if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), stream);
+  if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), stream, marks);
+  launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                    unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream) {
+                    unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
+                    LaunchMarks* marks) {
   if (n == 0) return 0;
   if (n > kMaxPackets) return -GPC_EINVAL;
   gpc_pkt_soa g;
@@ -669,7 +723,7 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   uint32_t xo = 0;
   uint2* gout = nullptr;
   if (group) {
-    if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid, &gout)) return rc;
+    if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid, &gout, marks)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
@@ -677,11 +731,12 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   if (group && group->key == GPC_GROUP_KEY_SCAN) e.sort_table[0] = e.sort_table[1] = 0;  // lanes already grouped by scan length
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
   if (svc) gout = nullptr;  // one launch, verdicts and LB results stored at the caller index
-  if (delta && svc) launch<true, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
-  else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
-  else if (svc) launch<false, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
-  else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream);
-  if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), stream);
+  if (delta && svc) launch<true, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  else if (svc) launch<false, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), stream, marks);
+  launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

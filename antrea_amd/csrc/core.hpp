@@ -787,9 +787,9 @@ GPC_HD TablePart combine_parts(const View& v, const TablePart& a, TablePart b) {
   if (va && vb && al == bl) {  // both decided at one level: a tie; the lower conj id wins
     const uint32_t ca = (a.s & kSNoAct) ? 0xffffffffu : v.base.blob[a.win];
     const uint32_t cb = (b.s & kSNoAct) ? 0xffffffffu : v.ovl.blob[b.win];
-    const TablePart& w = cb < ca ? b : a;
-    r.s = w.s | kSTie;
-    r.win = w.win;
+    const bool pb = cb < ca;  // fields selected one by one: a reference select puts both parts on the stack
+    r.s = (pb ? b.s : a.s) | kSTie;
+    r.win = pb ? b.win : a.win;
   } else if (vb && (!va || bl > al)) {
     r.s = b.s;
     r.win = b.win;
@@ -869,6 +869,7 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
   }
   if (hfound) res.h = hprio | (hverdict << 16) | kHFound | htie;
   uint32_t cnt[2] = {jt.always[0] >> 24, jt.always[1] >> 24};
+#pragma unroll
   for (uint32_t k = 0; k < 2; k++)
     for (uint32_t i = 0; i < jt.n_kinds[k]; i++) {
       const uint32_t axis = jt.kinds[k][i] & 15u, band = jt.kinds[k][i] >> 4;
@@ -1050,19 +1051,19 @@ struct TraceStep {
 };
 constexpr uint32_t kMaxTraceSteps = 8;
 
-// kStage: 0 = both stages; 1 = egress only; 2 = ingress only (the caller has checked that the
-// egress verdict lets the packet reach the ingress tables).
-template <bool kJournal = true, int kStage = 0, bool kTrace = false>
-GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, uint32_t ct_mark,
-                                 TraceStep* trace = nullptr, uint32_t* n_trace = nullptr) {
-  PacketOut o;
-  o.e.conj = o.g.conj = 0;
-  o.e.packed = o.g.packed = 0;
-  o.eslot = o.gslot = 0;
-  o.ecounted = o.gcounted = 0;
-  uint32_t flags = 0, conj = 0, tier = 0;
-  uint32_t t = kStage == 2 ? 4u : 1u;
-  while (true) {
+// One policy stage: its three rule tables from t0 (1 = egress, 4 = ingress). Every exit returns from
+// inside the loop, so the only state carried from one table to the next is the Pass rule's conj id
+// and the packed flags | tier word (register pressure: the walk is the kernel's hot region).
+struct StageOut {
+  VerdictOut v;
+  uint32_t slot;
+  int counted;
+};
+template <bool kJournal, bool kTrace>
+GPC_HD StageOut walk_stage(const View& im, const Pkt& p, uint32_t t0, TraceStep* trace, uint32_t* n_trace) {
+  uint32_t conj = 0, ft = 0;  // ft = flags | tier << 8 (reg5/reg6 after a Pass keep its conj id and tier)
+  for (uint32_t i = 0;; i++) {
+    const uint32_t t = t0 + i;
     const TableResult r = eval_table<kJournal>(im, t, p);
     if (kTrace && *n_trace < kMaxTraceSteps) {
       TraceStep& st = trace[(*n_trace)++];
@@ -1073,48 +1074,75 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, ui
       st.priority = r.prio;
       st.candidates = scan_estimate(im.base, t, p);
     }
-    const uint32_t i = t <= 3 ? t - 1 : t - 4;  // position inside the stage
-    if (r.tie) flags |= 2;
-    flags |= r.pin;
-    uint32_t act = 0, slot = 0;
-    int counted = 0;
+    ft |= (r.tie ? 2u : 0u) | r.pin;
     if (r.verdict == RV_PASS) {
-      flags |= 1;
       conj = r.conj;
-      tier = r.tier;
-    } else if (r.verdict != RV_MISS) {
-      act = r.verdict;  // RV_* values 2..6 equal GPC_ACT_*
-      if (act != RV_ISO_DROP && act != RV_BYPASS) {
-        conj = r.conj;
-        tier = r.tier;
-      }
-      slot = r.slot;
-      counted = r.counted && (act == RV_ALLOW || act == RV_DROP || act == RV_REJECT);
+      ft = (ft & 0xffu) | 1u | (uint32_t(r.tier) << 8);
     }
-    if (act == 0 && i < 2) {
-      t++;
-      continue;
+    StageOut o;
+    o.slot = 0;
+    o.counted = 0;
+    if (r.verdict == RV_MISS || r.verdict == RV_PASS) {
+      if (i < 2) continue;
+      o.v.conj = conj;
+      o.v.packed = pack_verdict(1 /*NO_MATCH*/, 0, ft >> 8, ft & 0xffu);
+      return o;
     }
-    VerdictOut v;
-    v.conj = conj;
-    v.packed = act ? pack_verdict(act, i + 1, tier, flags) : pack_verdict(1 /*NO_MATCH*/, 0, tier, flags);
-    if (t >= 4) {
-      o.g = v;
-      o.gslot = slot;
-      o.gcounted = counted;
+    const uint32_t act = r.verdict;  // RV_* values 2..6 equal GPC_ACT_*
+    if (act != RV_ISO_DROP && act != RV_BYPASS) {
+      conj = r.conj;
+      ft = (ft & 0xffu) | (uint32_t(r.tier) << 8);
+    }
+    o.v.conj = conj;
+    o.v.packed = pack_verdict(act, i + 1, ft >> 8, ft & 0xffu);
+    o.slot = r.slot;
+    o.counted = r.counted && (act == RV_ALLOW || act == RV_DROP || act == RV_REJECT);
+    return o;
+  }
+}
+
+// kStage: 0 = both stages; 1 = egress only; 2 = ingress only (the caller has checked that the
+// egress verdict lets the packet reach the ingress tables). kStage 0 runs walk_stage in a loop over
+// the two stages so the table evaluation is instantiated once.
+template <bool kJournal = true, int kStage = 0, bool kTrace = false>
+GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, uint32_t ct_mark,
+                                 TraceStep* trace = nullptr, uint32_t* n_trace = nullptr) {
+  PacketOut o;
+  o.e.conj = o.g.conj = 0;
+  o.e.packed = o.g.packed = 0;
+  o.eslot = o.gslot = 0;
+  o.ecounted = o.gcounted = 0;
+  if (kStage == 1 || kStage == 2) {
+    const StageOut s = walk_stage<kJournal, kTrace>(im, p, kStage == 1 ? 1u : 4u, trace, n_trace);
+    if (kStage == 1) {
+      o.e = s.v;
+      o.eslot = s.slot;
+      o.ecounted = s.counted;
+    } else {
+      o.g = s.v;
+      o.gslot = s.slot;
+      o.gcounted = s.counted;
+    }
+    return o;
+  }
+#pragma nounroll
+  for (uint32_t stage = 0; stage < 2; stage++) {
+    const StageOut s = walk_stage<kJournal, kTrace>(im, p, stage ? 4u : 1u, trace, n_trace);
+    if (stage) {
+      o.g = s.v;
+      o.gslot = s.slot;
+      o.gcounted = s.counted;
       break;
     }
-    o.e = v;
-    o.eslot = slot;
-    o.ecounted = counted;
-    if (kStage == 1) break;
+    o.e = s.v;
+    o.eslot = s.slot;
+    o.ecounted = s.counted;
+    const uint32_t act = s.v.packed & 0xffu;
     if (act == RV_DROP || act == RV_REJECT || act == RV_ISO_DROP) break;  // ingress never reached (NONE)
     if (const uint32_t b = ingress_bypass(im.base.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
       o.g.packed = b & 0xffu ? pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u) : 0u;
       break;
     }
-    flags = conj = tier = 0;
-    t = 4;
   }
   return o;
 }
