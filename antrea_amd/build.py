@@ -24,6 +24,8 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libgpc.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+if ARCH != "gfx950":  # the grouping / un-permute kernels use up to 141 KB of LDS (gfx950: 160 KB)
+    raise RuntimeError("libgpc targets gfx950 only (PYTORCH_ROCM_ARCH=%s)" % ARCH)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HOST_SRCS = ["compiler.cpp", "image.cpp", "flowtext.cpp", "service.cpp"]

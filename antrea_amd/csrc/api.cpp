@@ -58,6 +58,18 @@ struct StreamScratch {  // device scratch of the packet grouping pre-pass on one
 };
 constexpr size_t kScratchStreams = 8;  // idle buffers of other streams are released past this many
 
+// Key of the per-stream state (grouping scratch, epoch lifetime events, gpc_stream_epoch). The
+// hipStreamPerThread handle names a different stream on every host thread, so it is keyed by the
+// calling thread too: two threads launching on it never share scratch or a lifetime event.
+struct StreamKey {
+  hipStream_t s;
+  std::thread::id t;
+  bool operator<(const StreamKey& o) const { return s != o.s ? s < o.s : t < o.t; }
+};
+static StreamKey stream_key(hipStream_t s) {
+  return StreamKey{s, s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id()};
+}
+
 // IPv6 grouping key: the 8 address bits just above the shortest prefix length of the image's prefix
 // tree (the bits in which its shortest prefixes differ; fd00:10::/96 embedding: the embedded IPv4
 // address's top byte).
@@ -91,7 +103,7 @@ struct DevEpoch {
   uint32_t v6_lpm = 0;                  // its ImageHdr.v6_lpm
   int32_t v6_bit = 0;                   // grouping key of IPv6 batches (v6_group_bit)
   uint64_t epoch = 0;
-  std::map<hipStream_t, hipEvent_t> last_use;  // last launch on each stream that used this epoch
+  std::map<StreamKey, hipEvent_t> last_use;  // last launch on each stream that used this epoch
 };
 
 struct RetiredEpoch {
@@ -154,7 +166,7 @@ struct gpc_ctx {
   DevEpoch cur;
   std::vector<RetiredEpoch> retired;
   hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
-  std::map<hipStream_t, StreamScratch> scratch;  // packet grouping buffers per stream (data)
+  std::map<StreamKey, StreamScratch> scratch;  // packet grouping buffers per stream (data)
   uint32_t group_key = GPC_GROUP_KEY_AUTO;                            // gpc_group_key (gpc_create)
   uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // GPC_GROUP_KEY_ADDR key bits (classify.hip)
   // block order of grouped batches (classify.hip logical_block; 64M packets, ms per step for orders
@@ -173,13 +185,33 @@ struct gpc_ctx {
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
   uint64_t epoch = 0, n_full = 0, n_delta = 0, n_bg = 0;
-  std::map<hipStream_t, uint64_t> launch_epoch;  // epoch of the last classify launch per stream (data)
+  std::map<StreamKey, uint64_t> launch_epoch;  // epoch of the last classify launch per stream (data)
   uint64_t commit_no = 0;                // commits so far (COMMIT markers in the log)
   bool comp_pending = false;             // a background compaction was requested, not installed yet
   std::vector<std::pair<uint64_t, FeatureNP::Dirty>> dirty_hist;  // per commit since the request
   Compactor comp;
+  std::vector<LaunchMarks> marks;        // gpc_set_launch_timing event sets (data)
+  size_t marks_next = 0, marks_used = 0, marks_dropped = 0;
   explicit gpc_ctx(const gpc_config& c) : cfg(c), np(c), svc(c) {}
 };
+
+// The event set of the next timed gpc_classify* call (ctx->data held), or null when timing is off.
+static LaunchMarks* next_marks(gpc_ctx* ctx) {
+  if (ctx->marks.empty()) return nullptr;
+  LaunchMarks* m = &ctx->marks[ctx->marks_next];
+  ctx->marks_next = (ctx->marks_next + 1) % ctx->marks.size();
+  if (ctx->marks_used == ctx->marks.size()) ctx->marks_dropped++;
+  else ctx->marks_used++;
+  m->n = 0;
+  return m;
+}
+
+static void free_marks(gpc_ctx* ctx) {
+  for (auto& m : ctx->marks)
+    for (auto& e : m.ev) (void)hipEventDestroy(e);
+  ctx->marks.clear();
+  ctx->marks_next = ctx->marks_used = ctx->marks_dropped = 0;
+}
 
 static void log_op(gpc_ctx* ctx, Op&& op) {
   {
@@ -481,6 +513,7 @@ void gpc_destroy(gpc_ctx* ctx) {
     }
     if (ctx->stage) (void)hipHostFree(ctx->stage);
   }
+  free_marks(ctx);
   delete ctx;
 }
 
@@ -782,7 +815,7 @@ int gpc_replay(gpc_ctx* ctx) {
   }
   DevEpoch old;
   unsigned long long* old_counters = nullptr;
-  std::map<hipStream_t, StreamScratch> old_scratch;
+  std::map<StreamKey, StreamScratch> old_scratch;
   {
     std::lock_guard<std::mutex> d(ctx->data);
     old = std::move(ctx->cur);
@@ -850,8 +883,10 @@ int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
 constexpr size_t kGroupMinPackets = size_t(1) << 18;
 constexpr size_t kGroupMinImageBytes = size_t(4) << 20;
 
-// Grouping scratch of stream st with at least `need` bytes (ctx->data held).
-static int group_scratch(gpc_ctx* ctx, hipStream_t st, size_t need, uint8_t** out) {
+// Grouping scratch of stream st with at least `need` bytes (ctx->data held). A buffer held for a
+// much larger earlier batch is given back when a batch needs less than an eighth of it.
+static int group_scratch(gpc_ctx* ctx, hipStream_t s, size_t need, uint8_t** out) {
+  const StreamKey st = stream_key(s);
   if (ctx->scratch.size() >= kScratchStreams && !ctx->scratch.count(st)) {
     for (auto it = ctx->scratch.begin(); it != ctx->scratch.end();) {  // streams whose last batch is done
       if (!it->second.done || hipEventQuery(it->second.done) == hipSuccess) {
@@ -865,8 +900,8 @@ static int group_scratch(gpc_ctx* ctx, hipStream_t st, size_t need, uint8_t** ou
     (void)hipGetLastError();
   }
   StreamScratch& sc = ctx->scratch[st];
-  if (sc.bytes < need) {
-    dev_free(sc.p, st);  // after the launches already queued on st
+  if (sc.bytes < need || sc.bytes / 8 > need) {
+    dev_free(sc.p, s);  // after the launches already queued on s
     sc.p = nullptr;
     sc.bytes = 0;
     if (hip_ok(hipMalloc((void**)&sc.p, need))) return -GPC_ENOMEM;
@@ -878,9 +913,23 @@ static int group_scratch(gpc_ctx* ctx, hipStream_t st, size_t need, uint8_t** ou
 
 // The grouping scratch of stream st is in use until the launches just queued there have run.
 static int group_scratch_used(gpc_ctx* ctx, hipStream_t st) {
-  StreamScratch& sc = ctx->scratch[st];
+  StreamScratch& sc = ctx->scratch[stream_key(st)];
   if (!sc.done && hip_ok(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(sc.done, st));
+}
+
+// Grouping scratch for a batch the pre-pass would speed up. Grouping is a performance choice: when
+// it was not forced (gpc_config.group_packets == 0) and its scratch cannot be had, the batch runs
+// ungrouped instead of failing.
+static int group_scratch_for(gpc_ctx* ctx, hipStream_t st, size_t need, uint8_t** out) {
+  *out = nullptr;
+  const int e = group_scratch(ctx, st, need, out);
+  if (e == -GPC_ENOMEM && ctx->cfg.group_packets == 0) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return GPC_OK;
+  }
+  return e;
 }
 
 static bool group_batch(const gpc_ctx* ctx, size_t n, size_t image_bytes) {
@@ -918,13 +967,13 @@ int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* 
   // streams never share one and the data path does no allocation once warm
   GroupArgs ga{nullptr, group_key(ctx), ctx->cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0, ctx->group_unpermute};
   if (group_batch(ctx, n, ctx->cur.base->bytes))
-    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, false), &ga.scratch)) return e;
+    if (const int e = group_scratch_for(ctx, st, group_scratch_bytes(*pk, n, false), &ga.scratch)) return e;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
-                           ga.scratch ? &ga : nullptr, st);
+                           ga.scratch ? &ga : nullptr, st, n ? next_marks(ctx) : nullptr);
   if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
   if (rc || n == 0) return rc;
-  ctx->launch_epoch[st] = ctx->cur.epoch;
-  hipEvent_t& ev = ctx->cur.last_use[st];  // epoch lifetime: retired epochs are freed once drained
+  ctx->launch_epoch[stream_key(st)] = ctx->cur.epoch;
+  hipEvent_t& ev = ctx->cur.last_use[stream_key(st)];  // epoch lifetime: retired epochs are freed once drained
   if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(ev, st));
 }
@@ -1004,12 +1053,13 @@ int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* ou
   hipStream_t st = (hipStream_t)stream;
   GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, ctx->cur.v6_bit, ctx->group_unpermute};
   if (ctx->group_v6 && group_batch(ctx, n, ctx->cur.v6->bytes))
-    if (const int e = group_scratch(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
-  int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st);
+    if (const int e = group_scratch_for(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
+  int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st,
+                            n ? next_marks(ctx) : nullptr);
   if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
   if (rc || n == 0) return rc;
-  ctx->launch_epoch[st] = ctx->cur.epoch;
-  hipEvent_t& ev = ctx->cur.last_use[st];
+  ctx->launch_epoch[stream_key(st)] = ctx->cur.epoch;
+  hipEvent_t& ev = ctx->cur.last_use[stream_key(st)];
   if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(ev, st));
 }
@@ -1211,10 +1261,69 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
   return GPC_OK;
 }
 
+int gpc_set_launch_timing(gpc_ctx* ctx, uint32_t slots) {
+  if (!ctx || slots > 4096) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> d(ctx->data);
+  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  for (auto& m : ctx->marks) (void)hipEventSynchronize(m.ev[LaunchMarks::kMax - 1]);
+  (void)hipDeviceSynchronize();  // no recorded event is still pending when its set is destroyed
+  free_marks(ctx);
+  ctx->marks.resize(slots);
+  for (auto& m : ctx->marks) {
+    m.n = 0;
+    for (auto& e : m.ev)
+      if (hip_ok(hipEventCreate(&e))) {
+        free_marks(ctx);
+        return -GPC_EDEV;
+      }
+  }
+  return GPC_OK;
+}
+
+int gpc_launch_times(gpc_ctx* ctx, gpc_launch_time* out, size_t cap, size_t* n) {
+  if (!ctx || !n || (!out && cap)) return -GPC_EINVAL;
+  static const char* const names[kLaunchKinds] = {"group_tiles", "classify_egress", "classify_ingress", "classify_both",
+                                                  "unpermute"};
+  double ms[kLaunchKinds] = {};
+  uint32_t cnt[kLaunchKinds] = {};
+  size_t dropped;
+  {
+    std::lock_guard<std::mutex> d(ctx->data);
+    const size_t S = ctx->marks.size();
+    for (size_t k = 0; k < ctx->marks_used; k++) {  // oldest first
+      LaunchMarks& m = ctx->marks[(ctx->marks_next + S - ctx->marks_used + k) % S];
+      if (m.n < 2 || hip_ok(hipEventSynchronize(m.ev[m.n - 1]))) continue;
+      for (int i = 0; i + 1 < m.n; i++) {
+        float t = 0.f;
+        if (m.kind[i] < kLaunchKinds && !hip_ok(hipEventElapsedTime(&t, m.ev[i], m.ev[i + 1]))) {
+          ms[m.kind[i]] += t;
+          cnt[m.kind[i]]++;
+        }
+      }
+    }
+    dropped = ctx->marks_dropped;
+    ctx->marks_used = ctx->marks_dropped = 0;
+  }
+  size_t k = 0;
+  for (int i = 0; i < kLaunchKinds; i++) {
+    if (!cnt[i]) continue;
+    if (k < cap) {
+      std::memset(&out[k], 0, sizeof(gpc_launch_time));
+      std::strncpy(out[k].kernel, names[i], sizeof(out[k].kernel) - 1);
+      out[k].launches = cnt[i];
+      out[k].dropped = uint32_t(dropped);
+      out[k].total_ms = ms[i];
+    }
+    k++;
+  }
+  *n = k;
+  return k > cap ? -GPC_ERANGE : GPC_OK;
+}
+
 int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch) {
   if (!ctx || !epoch) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
-  auto it = ctx->launch_epoch.find((hipStream_t)stream);
+  auto it = ctx->launch_epoch.find(stream_key((hipStream_t)stream));
   if (it == ctx->launch_epoch.end()) return -GPC_ENOTFOUND;
   *epoch = it->second;
   return GPC_OK;

@@ -324,9 +324,10 @@ uint8_t action_verdict(const Flow& f, bool* ok) {  // conj_id flows and hard flo
         else if (a.a == TB_OUTPUT) output = true;
         else *ok = false;
         break;
-      case ACT_GROUP:  // logging-and-resubmit group (model.hpp kLogGroup*): to the K8s rule table = Pass
-        if (a.a == kLogGroupEgressRule || a.a == kLogGroupIngressRule) pass = true;
-        else metric = true;
+      case ACT_GROUP:  // logging-and-resubmit group (pipeline.go:1739-1760, 1874-1881): the group id is
+        // the agent's allocation, so it is not read; a logged Pass flow also loads
+        // DispositionPassRegMark (reg0[11..12] = 3, detected above), every other one resubmits to Metric
+        metric = true;
         break;
       default: break;
     }

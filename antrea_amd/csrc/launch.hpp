@@ -42,9 +42,24 @@ struct GroupArgs {
   uint32_t unpermute;  // 1: the ingress launch stores in grouped order, unpermute_kernel restores caller order
 };
 uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6);
+// Launch timing (gpc_set_launch_timing): an event is recorded on the launch stream before every
+// kernel of one gpc_classify* call and after the last, named by the kernel that follows it.
+struct LaunchMarks {
+  static constexpr int kMax = 8;
+  hipEvent_t ev[kMax];
+  uint8_t kind[kMax];  // LaunchKind of the kernel starting at ev[i] (kLaunchEnd: the closing event)
+  int n;
+};
+enum LaunchKind : uint8_t { kLaunchGroup, kLaunchEgress, kLaunchIngress, kLaunchBoth, kLaunchUnpermute, kLaunchKinds, kLaunchEnd };
+inline void launch_mark(LaunchMarks* m, uint8_t kind, hipStream_t s) {
+  if (!m || m->n >= LaunchMarks::kMax) return;
+  if (hipEventRecord(m->ev[m->n], s) == hipSuccess) m->kind[m->n++] = kind;
+}
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                    unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream);
+                    unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
+                    LaunchMarks* marks = nullptr);
 // IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
-                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream);
+                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
+                     LaunchMarks* marks = nullptr);
 }

@@ -90,6 +90,10 @@ class gpc_rule_metric(C.Structure):
                 ("sessions", C.c_uint64)]
 
 
+class gpc_launch_time(C.Structure):
+    _fields_ = [("kernel", C.c_char * 32), ("launches", C.c_uint32), ("dropped", C.c_uint32), ("total_ms", C.c_double)]
+
+
 class gpc_image_stats(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("device_bytes", C.c_uint64), ("n_rules", C.c_uint32 * 6),
                 ("n_hard", C.c_uint32 * 6), ("n_flows", C.c_uint32), ("n_counter_slots", C.c_uint32),
@@ -120,7 +124,8 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
            "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
-           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay"]
+           "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay",
+           "gpc_set_launch_timing", "gpc_launch_times"]
 
 _lib = None
 
@@ -180,6 +185,8 @@ def load(path: str = LIB_PATH):
                                                  C.POINTER(sz)]
     lib.gpc_stream_epoch.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     lib.gpc_trace.argtypes = [vp, C.POINTER(gpc_pkt_soa), vp, vp, C.POINTER(gpc_trace_step), sz, C.POINTER(sz)]
+    lib.gpc_set_launch_timing.argtypes = [vp, C.c_uint32]
+    lib.gpc_launch_times.argtypes = [vp, C.POINTER(gpc_launch_time), sz, C.POINTER(sz)]
     lib.gpc_strerror.argtypes = [i32]
     lib.gpc_strerror.restype = C.c_char_p
     _lib = lib
@@ -579,6 +586,19 @@ class Classifier:
         e = C.c_uint64()
         _check(self.lib.gpc_stream_epoch(self.h, stream or None, C.byref(e)), "gpc_stream_epoch")
         return e.value
+
+    def set_launch_timing(self, slots: int):
+        """gpc_set_launch_timing: HIP events around every kernel of the next gpc_classify* calls."""
+        _check(self.lib.gpc_set_launch_timing(self.h, int(slots)), "gpc_set_launch_timing")
+
+    def launch_times(self) -> Dict[str, dict]:
+        """gpc_launch_times: {kernel: {"launches", "total_ms", "mean_ms", "dropped"}} since the last call."""
+        arr = (gpc_launch_time * 8)()
+        n = C.c_size_t()
+        _check(self.lib.gpc_launch_times(self.h, arr, 8, C.byref(n)), "gpc_launch_times")
+        return {arr[i].kernel.decode(): {"launches": arr[i].launches, "total_ms": arr[i].total_ms,
+                                         "mean_ms": arr[i].total_ms / max(1, arr[i].launches),
+                                         "dropped": arr[i].dropped} for i in range(n.value)}
 
     def counters(self):
         p = C.POINTER(C.c_uint64)()

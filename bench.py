@@ -20,8 +20,10 @@ Rank 0 at N = 1 also (all after the timed region, none of it timed):
     packet for packet against the C oracle (oracle/ovs_cls.c over the ORACLE compiler's flows),
     which a spawned CPU process prepares while the GPU works -> "parity": {checked, mismatches};
   * cpu_baseline: the same C oracle timed on the host cores (bounded sample, see oracle/parity.py);
-  * roofline: measured L2<->fabric bytes per step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate
-    child passes, MI355X_MICROARCH.md HBM section) / kernel time, against 8 TB/s.
+  * roofline: the dominant kernel's measured L2<->fabric bytes per launch (rocprofv3 FETCH_SIZE x2 +
+    WRITE_SIZE, separate child passes, MI355X_MICROARCH.md HBM section) / its mean duration from HIP
+    events recorded around every launch of the timed region (gpc_launch_times), against 8 TB/s; the
+    whole step's figures and every launch kind's beside it.
 """
 from __future__ import annotations
 
@@ -173,38 +175,88 @@ def _host_sample(cols, idx):
     return out
 
 
-def _roofline(pmc, kern_ms, n, b_in, b_out, lbar):
-    """Measured-bytes roofline of one step (all its launches). `achieved` = counter bytes per step
-    (FETCH_SIZE doubled on gfx950 + WRITE_SIZE; L2 <-> fabric traffic, Infinity-Cache hits
-    included, so an upper bound of the HBM bytes) / kernel time; frac <= 1 is enforced. B_alg /
-    L-bar stay as diagnostics: they price every image line the algorithm touches at
-    HBM cost although most are L2 / MALL hits."""
-    pps_kernel = n / (kern_ms / 1e3)
-    b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
-    rl = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-          "basis": "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per step (grouping, classify and un-permute launches) / HIP-event kernel time"}
-    f, w = pmc.get("FETCH_SIZE"), pmc.get("WRITE_SIZE")
-    if f is not None and w is not None:
-        traffic = (2.0 * f + w) * 1024.0  # counters are in KB
-        gbs = traffic / (kern_ms / 1e3) / 1e9
-        frac = gbs / HBM_PEAK_GBS
-        if frac > 1.0:
-            raise RuntimeError("roofline sanity: measured %.0f GB/s exceeds the HBM peak" % gbs)
-        rl.update(achieved=round(gbs, 1), frac=round(frac, 4), traffic=int(traffic),
-                  traffic_per_packet=round(traffic / n, 1))
-    hit, miss = pmc.get("TCC_HIT_sum"), pmc.get("TCC_MISS_sum")
-    if hit is not None and miss is not None and hit + miss > 0:
-        rl["l2_hit_rate"] = round(hit / (hit + miss), 4)
-        rl["l2_miss_bytes_per_packet"] = round(miss * 128.0 / n, 1)  # 128-B L2 lines
-    rl["algorithmic"] = {"bytes_per_packet": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
-                         "gbs_if_uncached": round(pps_kernel * b_alg / 1e9, 1),
-                         "compulsory_bytes_per_packet": b_in + b_out,
-                         "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
+KIND_STAGE = {"classify_egress": "1", "classify_ingress": "2", "classify_both": "0"}
+
+
+def _pmc_kernel(by_kernel, kind):
+    """PMC means per dispatch of one launch kind (pmc_by_kernel keys are kernel names)."""
+    for k, cs in by_kernel.items():
+        if kind in ("group_tiles", "unpermute"):
+            if kind in k:
+                return cs
+        else:
+            m = re.search(r"classify_kernel<\w+, \w+, (\d)", k)
+            if m and m.group(1) == KIND_STAGE.get(kind):
+                return cs
+    return None
+
+
+def _traffic(cs):
+    """L2 <-> fabric bytes of one launch: FETCH_SIZE x 2 (the gfx950 correction of
+    MI355X_MICROARCH.md) + WRITE_SIZE, counters in KB."""
+    if not cs or cs.get("FETCH_SIZE") is None or cs.get("WRITE_SIZE") is None:
+        return None, None
+    return (2.0 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0, (cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0
+
+
+def _roofline(pmc, kern_ms, n, b_in, b_out, lbar, launches):
+    """Roofline of the dominant kernel (the launch kind with the largest HIP-event time per step,
+    measured on the launch stream inside the timed region: gpc_launch_times), with the whole
+    step's figures beside it. Bytes are the measured L2 <-> fabric traffic of the PMC child passes
+    (FETCH_SIZE x 2 + WRITE_SIZE per launch; Infinity-Cache hits included, so an upper bound of
+    HBM bytes); frac <= 1 is enforced. The x2 FETCH correction is documented for 16-B/lane
+    streaming reads; for gathers it is unverified, so the fraction without it is reported too.
+    B_alg / L-bar price every image line at HBM cost although most are L2 / MALL
+    hits: kept as a diagnostic ("frac_if_uncached" > 1 shows it is not a physical byte count)."""
     by_kernel = {}
     for p in pmc.get("_passes", []):
         for k, cs in (p or {}).get("by_kernel", {}).items():
             short = k.split("(")[0].replace("void gpc::", "")
             by_kernel.setdefault(short, {}).update({c: round(v, 1) for c, v in cs.items()})
+    kernels = {}
+    for kind, t in (launches or {}).items():
+        ms = t["mean_ms"]
+        cs = _pmc_kernel(by_kernel, kind)
+        tr, tr1 = _traffic(cs)
+        d = {"ms": round(ms, 3), "launches_per_step": round(t["per_step"], 2)}
+        if tr is not None and ms > 0:
+            gbs = tr / (ms / 1e3) / 1e9
+            if gbs / HBM_PEAK_GBS > 1.0:
+                raise RuntimeError("roofline sanity: %s measured %.0f GB/s exceeds the HBM peak" % (kind, gbs))
+            d.update(gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_packet=round(tr / n, 1),
+                     frac_without_fetch_x2=round(tr1 / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4))
+        kernels[kind] = d
+    dom = max(kernels, key=lambda k: kernels[k]["ms"] * kernels[k]["launches_per_step"]) if kernels else None
+    rl = {"bound": "hbm", "kernel": dom, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+          "traffic": None,
+          "basis": "dominant kernel: its rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per launch / its mean HIP-event "
+                   "duration in the timed region (gpc_launch_times); step: the same over all launches / step time"}
+    if dom and "gbs" in kernels[dom]:
+        tr, _ = _traffic(_pmc_kernel(by_kernel, dom))
+        rl.update(achieved=kernels[dom]["gbs"], frac=kernels[dom]["frac"], traffic=int(tr),
+                  kernel_ms=kernels[dom]["ms"], frac_without_fetch_x2=kernels[dom]["frac_without_fetch_x2"])
+    rl["kernels"] = kernels
+    step = {"ms": round(kern_ms, 3)}
+    f, w = pmc.get("FETCH_SIZE"), pmc.get("WRITE_SIZE")
+    if f is not None and w is not None:
+        traffic = (2.0 * f + w) * 1024.0
+        gbs = traffic / (kern_ms / 1e3) / 1e9
+        if gbs / HBM_PEAK_GBS > 1.0:
+            raise RuntimeError("roofline sanity: measured %.0f GB/s exceeds the HBM peak" % gbs)
+        step.update(achieved=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4), traffic=int(traffic),
+                    traffic_per_packet=round(traffic / n, 1))
+    hit, miss = pmc.get("TCC_HIT_sum"), pmc.get("TCC_MISS_sum")
+    if hit is not None and miss is not None and hit + miss > 0:
+        step["l2_hit_rate"] = round(hit / (hit + miss), 4)
+        step["l2_miss_bytes_per_packet"] = round(miss * 128.0 / n, 1)  # 128-B L2 lines
+    rl["step"] = step
+    pps_kernel = n / (kern_ms / 1e3)
+    b_alg = b_in + b_out + (64.0 * lbar if lbar is not None else 0.0)
+    rl["algorithmic"] = {"bytes_per_packet": round(b_alg, 1), "lines_per_packet": round(lbar, 2) if lbar else None,
+                         "gbs_if_uncached": round(pps_kernel * b_alg / 1e9, 1),
+                         "frac_if_uncached": round(pps_kernel * b_alg / 1e9 / HBM_PEAK_GBS, 4),
+                         "compulsory_bytes_per_packet": b_in + b_out,
+                         "compulsory_frac": round(pps_kernel * (b_in + b_out) / 1e9 / HBM_PEAK_GBS, 4)}
     rl["pmc_by_kernel"] = by_kernel or None
     return rl
 
@@ -319,6 +371,8 @@ def main():
             time.sleep(0.01)
         lat.clear()
     _log("timed region: %d steps of %d packets" % (args.steps, n))
+    clf.set_launch_timing(args.steps)  # HIP events around each kernel of the timed calls (gpc_launch_times)
+    torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
@@ -349,6 +403,10 @@ def main():
                   "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"],
                   "background_builds": st["n_background_builds"]}
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+    launches = clf.launch_times()
+    clf.set_launch_timing(0)
+    for t in launches.values():
+        t["per_step"] = t["launches"] / args.steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -398,7 +456,7 @@ def main():
     b_in, b_out = (19 if getattr(wl, "services", None) else 17), 16  # +2 B len for C4
     if v6:
         b_in += 24  # 16-B instead of 4-B src / dst
-    roofline = _roofline(pmc, kern_ms, n, b_in, b_out, lbar)
+    roofline = _roofline(pmc, kern_ms, n, b_in, b_out, lbar, launches)
     cpu = None
     if worker is not None and not args.no_cpu_baseline:  # rank 0, N=1 only
         _log("CPU baseline (%.0f s)" % args.cpu_seconds)
@@ -425,7 +483,8 @@ def main():
                    if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18 and st["device_bytes"] >= 4 << 20))
                    else "off"},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)
-        "launches_per_step": 1 if getattr(wl, "services", None) else 2,
+        "launches_per_step": round(sum(t["per_step"] for t in launches.values()), 2),
+        "kernel_ms_by_launch": {k: round(t["mean_ms"], 3) for k, t in launches.items()},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity,

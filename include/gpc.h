@@ -403,7 +403,11 @@ int gpc_replay(gpc_ctx* ctx);
 #define GPC_MAX_BATCH (4294967296ull - 256ull)
 /* Classify n packets whose columns are DEVICE pointers; writes 2*n verdicts (device pointer).
  * n > GPC_MAX_BATCH: -GPC_EINVAL, nothing launched.
- * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t. */
+ * `count` != 0 updates the per-rule counters (Metric-table flows). `stream` is a hipStream_t; the
+ * library keeps per-stream scratch (packet grouping) and epoch-lifetime events, keyed by the
+ * stream and, for hipStreamPerThread, by the calling thread as well. With group_packets == 0 a
+ * batch whose grouping scratch cannot be allocated runs ungrouped; -GPC_ENOMEM only when
+ * grouping was forced (group_packets > 0). */
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
 /* gpc_classify plus the AntreaProxy stage in front of the policy tables: packets to a Service
  * (ServiceLB flow hit) get an Endpoint from the group (select bucket by a symmetric L4 hash of the
@@ -457,6 +461,20 @@ int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uin
 /* The epoch (gpc_image_stats.epoch) the last gpc_classify* launch on `stream` was bound to: with
  * classification concurrent to commits, every launch sees exactly this one committed epoch. */
 int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch);
+/* Launch timing (a measurement hook: bench.py's per-kernel roofline). With slots > 0 every
+ * gpc_classify* call records HIP events on its own stream before each of its kernels and after
+ * the last, into the next of `slots` event sets (reused round-robin: a set not read back by
+ * gpc_launch_times before it comes round again is overwritten and counted in `dropped`);
+ * slots = 0 (the default) records nothing. */
+typedef struct gpc_launch_time {
+  char kernel[32];   /* "group_tiles", "classify_egress", "classify_ingress", "classify_both", "unpermute" */
+  uint32_t launches; /* launches of that kernel since the previous gpc_launch_times */
+  uint32_t dropped;  /* event sets overwritten before they were read (all kinds) */
+  double total_ms;   /* summed HIP-event durations */
+} gpc_launch_time;
+int gpc_set_launch_timing(gpc_ctx* ctx, uint32_t slots);
+/* Waits for the recorded events and returns one entry per kernel kind that ran (cap entries at most). */
+int gpc_launch_times(gpc_ctx* ctx, gpc_launch_time* out, size_t cap, size_t* n);
 const char* gpc_strerror(int err);
 int gpc_abi_version(void);
 

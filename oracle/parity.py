@@ -152,6 +152,9 @@ def time_baseline(wl, pipe, seconds: float, chunk: int, threads: int) -> dict:
                      "the oracle compiler emits" % (done, chunk, elapsed, pipe.n_flows),
            "per_packet": per}
     out.update(host_info())
+    env = os.environ.get("OMP_NUM_THREADS")
+    out["cores_basis"] = ("OMP_NUM_THREADS=%s: the CPU share the GPU box grants this process (nproc counts the "
+                          "whole machine)" % env) if env and env.isdigit() else "the CPUs this process may run on"
     return out
 
 

@@ -101,3 +101,29 @@ def test_device_ipv6_vs_python_oracle_c1(dual):
     got = c.classify6_host(cols6)
     res = parity.compare(got, want)
     assert res["mismatches"] == 0, res
+
+
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
+def test_device_vs_oracle_after_churn_c3(group):
+    """Config 5's update path at full scale against the oracle: C3, then the seeded op log of
+    tests/golden/make_churn_fixture.py (2125 AddPolicyRuleAddress, 869 DeletePolicyRuleAddress incl.
+    original addresses, 200 UninstallPolicyRuleFlows, 99 reinstalls, 30 ReassignFlowPriorities)
+    published as delta epochs every 100 ops (journal + tombstones; the background compactor may
+    hand over meanwhile): verdicts and NetworkPolicyMetrics of 100k packets equal the C oracle's
+    over the oracle compiler's replay of the same log -- then again after gpc_compact."""
+    from tests.golden import make_churn_fixture as cf
+    f = cf.load()
+    wl, log, cols = cf.inputs()
+    assert fx.cols_digest(cols) == str(f["cols_sha256"]) and fx.rules_digest(wl) == str(f["rules_sha256"])
+    assert cf.log_digest(log) == str(f["log_sha256"]), "op log generator drifted from the fixture"
+    c = _classifier(wl, group=group)
+    cf.apply(c, log, on_commit=c.commit)
+    assert c.image_stats()["n_delta_builds"] > 0
+    for phase in ("delta", "compacted"):
+        if phase == "compacted":
+            c.compact()
+            c.reset_counters()
+        got = c.classify_host(cols, count=True)
+        res = parity.compare(got, f["verdicts"])
+        assert res["mismatches"] == 0, (phase, res)
+        assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"]), phase

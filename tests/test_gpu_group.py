@@ -202,3 +202,49 @@ def test_grouped_ipv6_equals_plain(n, monkeypatch):
         res.append((c.classify6_host(cols, count=True), _metrics(c)))
     assert (res[0][0] == res[1][0]).all()
     assert res[0][1] == res[1][1]
+
+
+def test_grouped_per_thread_default_stream_two_threads():
+    """hipStreamPerThread (handle 2) names a different stream on every host thread: two threads
+    classifying grouped batches on it at the same time get separate grouping scratch (keyed by
+    stream and thread), so their verdicts equal the plain launch's."""
+    import threading
+    import torch
+    HIP_STREAM_PER_THREAD = 2
+    wl = workload.config3(n_policies_per_dir=20, rules_per_policy=50)
+    n = 1 << 18
+    colsets = [workload.gen_packets_torch(wl, n, device="cuda", seed=s) for s in (31, 32)]
+    plain = gpc.Classifier(group_packets=-1)
+    grouped = gpc.Classifier(group_packets=1)
+    for c in (plain, grouped):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+        c.commit()
+    refs = []
+    for cols in colsets:
+        r = torch.zeros(2 * n * 8, dtype=torch.uint8, device="cuda")
+        plain.classify_device(gpc.pkt_soa_device(cols), n, r.data_ptr(), stream=0)
+        refs.append(r)
+    torch.cuda.synchronize()
+    outs = [[torch.zeros_like(refs[0]) for _ in range(4)] for _ in colsets]
+    errs = []
+
+    def work(k):
+        try:
+            soa = gpc.pkt_soa_device(colsets[k])
+            for o in outs[k]:
+                grouped.classify_device(soa, n, o.data_ptr(), stream=HIP_STREAM_PER_THREAD)
+            assert grouped.stream_epoch(HIP_STREAM_PER_THREAD) > 0  # keyed by this thread
+        except Exception as e:  # reported by the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for k in range(2):
+        for o in outs[k]:
+            assert torch.equal(o, refs[k])
