@@ -86,11 +86,16 @@ struct DevImage {  // one uploaded image (freed when the last epoch using it ret
   uint32_t* d_blob = nullptr;
   size_t bytes = 0;
   hipStream_t s = nullptr;
+  int device = 0;                       // HIP ordinal the buffers live on
   uint8_t sort_table[2] = {0, 0};       // per policy stage: the table whose scan length orders lanes
   uint32_t axes = 0;                    // axes read by the sub-indexes (group_axes)
   ~DevImage() {
+    int cur = 0;
+    const bool swap = hipGetDevice(&cur) == hipSuccess && cur != device;
+    if (swap) (void)hipSetDevice(device);
     dev_free(d_hdr, s);
     dev_free(d_blob, s);
+    if (swap) (void)hipSetDevice(cur);
   }
 };
 
@@ -120,6 +125,23 @@ struct RetiredEpoch {
   }
 };
 
+// The data-path state of one device slot of a context (gpc_create_multi: one control plane, several
+// devices). Every slot holds its own copy of each published epoch, counters, grouping scratch and
+// upload stream; the host shadow (compiler, images, journal, counter slots) is shared.
+struct DevState {
+  int device = 0;
+  DevEpoch cur;
+  std::vector<RetiredEpoch> retired;
+  hipStream_t ustream = nullptr;                 // uploads / frees (hipStreamNonBlocking)
+  std::map<StreamKey, StreamScratch> scratch;    // packet grouping buffers per stream (data)
+  std::map<StreamKey, uint64_t> launch_epoch;    // epoch of the last classify launch per stream (data)
+  unsigned long long* d_counters = nullptr;
+  size_t counter_cap = 0;                        // slots
+  uint32_t counter_copies = 1;                   // striped copies of the counter array (counter_copies_for)
+  std::vector<LaunchMarks> marks;                // gpc_set_launch_timing event sets (data)
+  size_t marks_next = 0, marks_used = 0, marks_dropped = 0;
+};
+
 // Delta commits append the changed rules to the journal of the current base (image.hpp Journal).
 // A full rebuild (compaction) happens when the journal holds more than
 // max(kDeltaMinRules, base rules / kDeltaFraction) live rules or its pool would pass its capacity.
@@ -146,7 +168,7 @@ struct Compactor {
   int rc = 0;
   std::unique_ptr<HostImage> base;
   std::unique_ptr<Journal> journal;
-  std::shared_ptr<DevImage> dbase, dpool;
+  std::vector<std::shared_ptr<DevImage>> dbase, dpool;  // per device slot (empty: not uploaded)
   size_t uploaded = 0;
   uint64_t at_commit = 0;
 };
@@ -162,11 +184,9 @@ struct gpc_ctx {
   SlotMap slots;
   HostImage last;    // base image of the current epoch: shadow state for re-upload + debug export
   HostImage last6;   // IPv6 image (ipv6_enabled): rebuilt in full by every commit that changes rules
-  Journal journal;   // delta epochs over `last` (host mirror of the device pool)
-  DevEpoch cur;
-  std::vector<RetiredEpoch> retired;
-  hipStream_t ustream = nullptr;         // uploads / frees (hipStreamNonBlocking)
-  std::map<StreamKey, StreamScratch> scratch;  // packet grouping buffers per stream (data)
+  Journal journal;   // delta epochs over `last` (host mirror of the device pools)
+  std::vector<DevState> dev;             // device slots (gpc_create: one, cfg.device)
+  uint64_t cur_epoch = 0;                // epoch every slot currently publishes (0: nothing committed)
   uint32_t group_key = GPC_GROUP_KEY_AUTO;                            // gpc_group_key (gpc_create)
   uint32_t group_src_bits = env_u32("GPC_GROUP_SRC_BITS", 8, 0, 8);  // GPC_GROUP_KEY_ADDR key bits (classify.hip)
   // block order of grouped batches (classify.hip logical_block; 64M packets, ms per step for orders
@@ -179,38 +199,35 @@ struct gpc_ctx {
   uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;
-  unsigned long long* d_counters = nullptr;
-  size_t counter_cap = 0;  // slots
-  uint32_t counter_copies = 1;  // striped copies of the counter array (counter_copies_for)
   std::vector<uint32_t> released_slots;
   std::vector<uint32_t> slot_conj;
   uint64_t epoch = 0, n_full = 0, n_delta = 0, n_bg = 0;
-  std::map<StreamKey, uint64_t> launch_epoch;  // epoch of the last classify launch per stream (data)
   uint64_t commit_no = 0;                // commits so far (COMMIT markers in the log)
   bool comp_pending = false;             // a background compaction was requested, not installed yet
   std::vector<std::pair<uint64_t, FeatureNP::Dirty>> dirty_hist;  // per commit since the request
   Compactor comp;
-  std::vector<LaunchMarks> marks;        // gpc_set_launch_timing event sets (data)
-  size_t marks_next = 0, marks_used = 0, marks_dropped = 0;
-  explicit gpc_ctx(const gpc_config& c) : cfg(c), np(c), svc(c) {}
+  gpc_ctx(const gpc_config& c, const std::vector<int>& devices) : cfg(c), np(c), svc(c), dev(devices.size()) {
+    for (size_t k = 0; k < devices.size(); k++) dev[k].device = devices[k];
+  }
 };
 
-// The event set of the next timed gpc_classify* call (ctx->data held), or null when timing is off.
-static LaunchMarks* next_marks(gpc_ctx* ctx) {
-  if (ctx->marks.empty()) return nullptr;
-  LaunchMarks* m = &ctx->marks[ctx->marks_next];
-  ctx->marks_next = (ctx->marks_next + 1) % ctx->marks.size();
-  if (ctx->marks_used == ctx->marks.size()) ctx->marks_dropped++;
-  else ctx->marks_used++;
+// The event set of the next timed gpc_classify* call on a slot (ctx->data held), or null when
+// timing is off.
+static LaunchMarks* next_marks(DevState& D) {
+  if (D.marks.empty()) return nullptr;
+  LaunchMarks* m = &D.marks[D.marks_next];
+  D.marks_next = (D.marks_next + 1) % D.marks.size();
+  if (D.marks_used == D.marks.size()) D.marks_dropped++;
+  else D.marks_used++;
   m->n = 0;
   return m;
 }
 
-static void free_marks(gpc_ctx* ctx) {
-  for (auto& m : ctx->marks)
+static void free_marks(DevState& D) {
+  for (auto& m : D.marks)
     for (auto& e : m.ev) (void)hipEventDestroy(e);
-  ctx->marks.clear();
-  ctx->marks_next = ctx->marks_used = ctx->marks_dropped = 0;
+  D.marks.clear();
+  D.marks_next = D.marks_used = D.marks_dropped = 0;
 }
 
 static void log_op(gpc_ctx* ctx, Op&& op) {
@@ -239,10 +256,10 @@ static uint32_t counter_copies_for(size_t cap) {
   while (r < 64 && cap * r < 65536) r <<= 1;
   return r;
 }
-static int fold_counters(gpc_ctx* ctx) {  // caller holds ctl; device synchronized on return
-  if (!ctx->d_counters || ctx->counter_copies <= 1) return GPC_OK;
-  if (hip_ok(hipSetDevice(ctx->cfg.device)) || hip_ok(hipDeviceSynchronize())) return -GPC_EDEV;
-  int rc = launch_fold_counters(ctx->d_counters, uint64_t(ctx->counter_cap) * kCounterWords, ctx->counter_copies, nullptr);
+static int fold_counters(DevState& D) {  // caller holds ctl; device synchronized on return
+  if (!D.d_counters || D.counter_copies <= 1) return GPC_OK;
+  if (hip_ok(hipSetDevice(D.device)) || hip_ok(hipDeviceSynchronize())) return -GPC_EDEV;
+  int rc = launch_fold_counters(D.d_counters, uint64_t(D.counter_cap) * kCounterWords, D.counter_copies, nullptr);
   if (!rc) rc = hip_ok(hipDeviceSynchronize());
   return rc;
 }
@@ -299,9 +316,10 @@ static uint32_t group_axes(const HostImage& h) {
   return m;
 }
 
-static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevImage>* out) {
+static int upload_image(const HostImage& h, int device, hipStream_t s, std::shared_ptr<DevImage>* out) {
   auto d = std::make_shared<DevImage>();
   d->s = s;
+  d->device = device;
   d->bytes = h.blob.size() * 4;
   if (hip_ok(dev_alloc((void**)&d->d_blob, d->bytes, s)) || hip_ok(dev_alloc((void**)&d->d_hdr, sizeof(ImageHdr), s)) ||
       hip_ok(hipMemcpyAsync(d->d_blob, h.blob.data(), d->bytes, hipMemcpyHostToDevice, s)) ||
@@ -313,9 +331,10 @@ static int upload_image(const HostImage& h, hipStream_t s, std::shared_ptr<DevIm
   return GPC_OK;
 }
 
-static int upload_words(const std::vector<uint32_t>& w, hipStream_t s, std::shared_ptr<DevImage>* out) {
+static int upload_words(const std::vector<uint32_t>& w, int device, hipStream_t s, std::shared_ptr<DevImage>* out) {
   auto d = std::make_shared<DevImage>();
   d->s = s;
+  d->device = device;
   d->bytes = w.size() * 4;
   if (hip_ok(dev_alloc((void**)&d->d_blob, d->bytes, s)) ||
       hip_ok(hipMemcpyAsync(d->d_blob, w.data(), d->bytes, hipMemcpyHostToDevice, s)))
@@ -324,18 +343,29 @@ static int upload_words(const std::vector<uint32_t>& w, hipStream_t s, std::shar
   return GPC_OK;
 }
 
-static void collect_retired(gpc_ctx* ctx, bool wait) {
-  if (wait && !ctx->retired.empty()) (void)hipDeviceSynchronize();
+static void collect_retired(DevState& D, bool wait) {  // the slot's device is current
+  if (wait && !D.retired.empty()) (void)hipDeviceSynchronize();
   size_t k = 0;
-  for (size_t i = 0; i < ctx->retired.size(); i++) {
-    if (wait || ctx->retired[i].drained()) {
-      ctx->retired[i].release(ctx->ustream);
+  for (size_t i = 0; i < D.retired.size(); i++) {
+    if (wait || D.retired[i].drained()) {
+      D.retired[i].release(D.ustream);
     } else {
-      if (k != i) ctx->retired[k] = std::move(ctx->retired[i]);
+      if (k != i) D.retired[k] = std::move(D.retired[i]);
       k++;
     }
   }
-  ctx->retired.resize(k);
+  D.retired.resize(k);
+}
+
+// A new journal pool on one slot (kPoolWords words, stream-ordered allocation).
+static int alloc_pool(int device, hipStream_t s, std::shared_ptr<DevImage>* out) {
+  auto pool = std::make_shared<DevImage>();
+  pool->s = s;
+  pool->device = device;
+  pool->bytes = kPoolWords * 4;
+  if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, s))) return -GPC_EDEV;
+  *out = std::move(pool);
+  return GPC_OK;
 }
 
 static int commit_impl(gpc_ctx* ctx, bool force_full);
@@ -345,9 +375,11 @@ static void compactor_main(gpc_ctx* ctx) {
   FeatureNP shadow(ctx->cfg);
   uint64_t shadow_commit = 0;
   bool at_marker = true;
-  hipStream_t bs = nullptr;
-  const bool dev_ok = hipSetDevice(ctx->cfg.device) == hipSuccess &&
-                      hipStreamCreateWithFlags(&bs, hipStreamNonBlocking) == hipSuccess;
+  std::vector<hipStream_t> bs(ctx->dev.size(), nullptr);  // one upload stream per device slot
+  bool dev_ok = true;
+  for (size_t k = 0; k < bs.size() && dev_ok; k++)
+    dev_ok = hipSetDevice(ctx->dev[k].device) == hipSuccess &&
+             hipStreamCreateWithFlags(&bs[k], hipStreamNonBlocking) == hipSuccess;
   if (!dev_ok) (void)hipGetLastError();
   auto grab = [&](std::vector<Op>* out, bool wait) {  // false: stop requested
     std::unique_lock<std::mutex> lk(C.mu);
@@ -417,19 +449,25 @@ static void compactor_main(gpc_ctx* ctx) {
     }
     if (const char* d = std::getenv("GPC_TEST_COMPACT_DELAY_MS"))  // tests: widen the handover race window
       std::this_thread::sleep_for(std::chrono::milliseconds(std::atoi(d)));
-    std::shared_ptr<DevImage> dbase, dpool;
+    std::vector<std::shared_ptr<DevImage>> dbase, dpool;
     size_t up = 0;
-    if (rc == GPC_OK && dev_ok) {
-      auto pool = std::make_shared<DevImage>();
-      pool->s = bs;
-      pool->bytes = kPoolWords * 4;
-      if (upload_image(*base, bs, &dbase) || hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, bs)) ||
-          (jn->active() && hip_ok(hipMemcpyAsync(pool->d_blob, jn->pool.data(), jn->pool.size() * 4,
-                                                 hipMemcpyHostToDevice, bs))) ||
-          hip_ok(hipStreamSynchronize(bs))) {
-        dbase.reset();
+    if (rc == GPC_OK && dev_ok) {  // the same base and journal on every device slot
+      bool ok = true;
+      dbase.resize(bs.size());
+      dpool.resize(bs.size());
+      for (size_t k = 0; k < bs.size() && ok; k++) {
+        const int dv = ctx->dev[k].device;
+        ok = hipSetDevice(dv) == hipSuccess && !upload_image(*base, dv, bs[k], &dbase[k]) &&
+             !alloc_pool(dv, bs[k], &dpool[k]) &&
+             !(jn->active() && hip_ok(hipMemcpyAsync(dpool[k]->d_blob, jn->pool.data(), jn->pool.size() * 4,
+                                                     hipMemcpyHostToDevice, bs[k])));
+      }
+      for (size_t k = 0; k < bs.size() && ok; k++) ok = hipStreamSynchronize(bs[k]) == hipSuccess;
+      if (!ok) {
+        (void)hipGetLastError();
+        dbase.clear();
+        dpool.clear();
       } else {
-        dpool = std::move(pool);
         up = jn->active() ? jn->pool.size() : 0;
       }
     }
@@ -446,13 +484,15 @@ static void compactor_main(gpc_ctx* ctx) {
   }
   {
     std::lock_guard<std::mutex> g(C.mu);  // results not installed are dropped with the context
-    C.dbase.reset();
-    C.dpool.reset();
+    C.dbase.clear();
+    C.dpool.clear();
   }
-  if (bs) {
-    (void)hipStreamSynchronize(bs);
-    (void)hipStreamDestroy(bs);
-  }
+  for (size_t k = 0; k < bs.size(); k++)
+    if (bs[k]) {
+      (void)hipSetDevice(ctx->dev[k].device);
+      (void)hipStreamSynchronize(bs[k]);
+      (void)hipStreamDestroy(bs[k]);
+    }
 }
 
 extern "C" {
@@ -474,11 +514,21 @@ const char* gpc_strerror(int err) {
 }
 
 int gpc_create(const gpc_config* cfg, gpc_ctx** out) {
-  if (!cfg || !out) return -GPC_EINVAL;
+  if (!cfg) return -GPC_EINVAL;
+  const int32_t d = cfg->device;
+  return gpc_create_multi(cfg, &d, 1, out);
+}
+
+int gpc_create_multi(const gpc_config* cfg, const int32_t* devices, size_t n, gpc_ctx** out) {
+  if (!cfg || !out || !devices || n == 0 || n > GPC_MAX_DEVICES) return -GPC_EINVAL;
   if (!cfg->ipv4_enabled && !cfg->ipv6_enabled) return -GPC_EINVAL;
   if (cfg->group_key < GPC_GROUP_KEY_AUTO || cfg->group_key > GPC_GROUP_KEY_SCAN) return -GPC_EINVAL;
+  for (size_t k = 0; k < n; k++)
+    if (devices[k] < 0) return -GPC_EINVAL;
   try {
-    *out = new gpc_ctx(*cfg);
+    gpc_config c = *cfg;
+    c.device = devices[0];
+    *out = new gpc_ctx(c, std::vector<int>(devices, devices + n));
     // grouping key: the environment (experiments) overrides the config
     (*out)->group_key = env_u32("GPC_GROUP_KEY", uint32_t(cfg->group_key), GPC_GROUP_KEY_AUTO, GPC_GROUP_KEY_SCAN);
     if (cfg->compact_after >= 0) (*out)->comp.th = std::thread(compactor_main, *out);
@@ -489,6 +539,23 @@ int gpc_create(const gpc_config* cfg, gpc_ctx** out) {
   return GPC_OK;
 }
 
+// Drops every device buffer of a slot (the slot's device is current, launches drained).
+static void drop_slot(DevState& D) {
+  D.retired.push_back(RetiredEpoch{std::move(D.cur)});
+  D.cur = DevEpoch();
+  collect_retired(D, true);
+  if (D.d_counters) (void)hipFree(D.d_counters);
+  D.d_counters = nullptr;
+  for (auto& kv : D.scratch) {
+    (void)hipFree(kv.second.p);
+    if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+  }
+  D.scratch.clear();
+  D.launch_epoch.clear();
+}
+
+int gpc_n_devices(gpc_ctx* ctx) { return ctx ? int(ctx->dev.size()) : -GPC_EINVAL; }
+
 void gpc_destroy(gpc_ctx* ctx) {
   if (!ctx) return;
   {
@@ -497,23 +564,19 @@ void gpc_destroy(gpc_ctx* ctx) {
   }
   ctx->comp.cv.notify_all();
   if (ctx->comp.th.joinable()) ctx->comp.th.join();
-  if (ctx->cur.base || ctx->d_counters || !ctx->retired.empty()) {
-    (void)hipSetDevice(ctx->cfg.device);
-    (void)hipDeviceSynchronize();
-    ctx->retired.push_back(RetiredEpoch{std::move(ctx->cur)});
-    collect_retired(ctx, true);
-    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
-    for (auto& kv : ctx->scratch) {
-      (void)hipFree(kv.second.p);
-      if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+  for (DevState& D : ctx->dev) {
+    if (D.cur.base || D.d_counters || !D.retired.empty() || D.ustream || !D.marks.empty()) {
+      (void)hipSetDevice(D.device);
+      (void)hipDeviceSynchronize();
+      drop_slot(D);
+      if (D.ustream) {
+        (void)hipStreamSynchronize(D.ustream);
+        (void)hipStreamDestroy(D.ustream);
+      }
+      free_marks(D);
     }
-    if (ctx->ustream) {
-      (void)hipStreamSynchronize(ctx->ustream);
-      (void)hipStreamDestroy(ctx->ustream);
-    }
-    if (ctx->stage) (void)hipHostFree(ctx->stage);
   }
-  free_marks(ctx);
+  if (ctx->stage) (void)hipHostFree(ctx->stage);
   delete ctx;
 }
 
@@ -803,76 +866,87 @@ int gpc_commit(gpc_ctx* ctx) { return commit_impl(ctx, false); }
 int gpc_replay(gpc_ctx* ctx) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  (void)hipDeviceSynchronize();  // may fail after a reset: the old buffers are dropped regardless
-  (void)hipGetLastError();
   {  // a background compaction result built on the old device state is dropped
     std::lock_guard<std::mutex> c(ctx->comp.mu);
     if (ctx->comp.busy) ctx->comp.discard = true;
-    ctx->comp.dbase.reset();
-    ctx->comp.dpool.reset();
+    ctx->comp.dbase.clear();
+    ctx->comp.dpool.clear();
     if (ctx->comp.ready) ctx->comp.discard = true;
   }
-  DevEpoch old;
-  unsigned long long* old_counters = nullptr;
-  std::map<StreamKey, StreamScratch> old_scratch;
+  std::vector<DevState> old(ctx->dev.size());
   {
     std::lock_guard<std::mutex> d(ctx->data);
-    old = std::move(ctx->cur);
-    ctx->cur = DevEpoch();
-    old_counters = ctx->d_counters;
-    ctx->d_counters = nullptr;
-    ctx->launch_epoch.clear();
-    old_scratch.swap(ctx->scratch);
+    for (size_t k = 0; k < ctx->dev.size(); k++) {
+      DevState& D = ctx->dev[k];
+      old[k].device = D.device;
+      old[k].cur = std::move(D.cur);
+      D.cur = DevEpoch();
+      old[k].d_counters = D.d_counters;
+      D.d_counters = nullptr;
+      D.launch_epoch.clear();
+      old[k].scratch.swap(D.scratch);
+      old[k].retired.swap(D.retired);
+      old[k].ustream = D.ustream;
+    }
+    ctx->cur_epoch = 0;
   }
-  for (auto& kv : old_scratch) {
-    (void)hipFree(kv.second.p);
-    if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+  for (DevState& O : old) {
+    if (hip_ok(hipSetDevice(O.device))) return -GPC_EDEV;
+    (void)hipDeviceSynchronize();  // may fail after a reset: the old buffers are dropped regardless
+    (void)hipGetLastError();
+    drop_slot(O);
+    (void)hipGetLastError();
   }
-  ctx->retired.push_back(RetiredEpoch{std::move(old)});
-  collect_retired(ctx, true);
-  if (old_counters) (void)hipFree(old_counters);
-  (void)hipGetLastError();
   if (ctx->last.blob.empty()) return GPC_OK;  // nothing committed yet
-  if (!ctx->ustream && hip_ok(hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking))) return -GPC_EDEV;
-  hipStream_t us = ctx->ustream;
-  DevEpoch ne;
-  int rc = upload_image(ctx->last, us, &ne.base);
-  Journal& jn = ctx->journal;
-  if (!rc && jn.active()) {
-    auto pool = std::make_shared<DevImage>();
-    pool->s = us;
-    pool->bytes = kPoolWords * 4;
-    if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, us)) ||
-        hip_ok(hipMemcpyAsync(pool->d_blob, jn.pool.data(), jn.pool.size() * 4, hipMemcpyHostToDevice, us)))
-      rc = -GPC_EDEV;
-    ne.pool = std::move(pool);
-    jn.uploaded = jn.pool.size();
-    ne.jhdr = jn.hdr_off;
-  }
-  if (!rc && !ctx->last6.blob.empty()) {
-    rc = upload_image(ctx->last6, us, &ne.v6);
-    ne.v6_lpm = ctx->last6.hdr.v6_lpm;
-    ne.v6_bit = v6_group_bit(ctx->last6);
-  }
-  if (!rc && !ctx->svc_blob.empty()) rc = upload_words(ctx->svc_blob, us, &ne.svc);
   const size_t cap = std::max<size_t>(1, ctx->slots.size());
   const uint32_t copies = counter_copies_for(cap);
-  unsigned long long* nc = nullptr;
-  if (!rc && (hip_ok(hipMalloc(&nc, cap * kCounterBytes * copies)) || hip_ok(hipMemset(nc, 0, cap * kCounterBytes * copies))))
-    rc = -GPC_EDEV;
-  if (!rc) rc = hip_ok(hipStreamSynchronize(us));
+  std::vector<DevEpoch> ne(ctx->dev.size());
+  std::vector<unsigned long long*> nc(ctx->dev.size(), nullptr);
+  Journal& jn = ctx->journal;
+  int rc = GPC_OK;
+  for (size_t k = 0; k < ctx->dev.size() && !rc; k++) {
+    DevState& D = ctx->dev[k];
+    if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
+    if (!D.ustream && hip_ok(hipStreamCreateWithFlags(&D.ustream, hipStreamNonBlocking))) return -GPC_EDEV;
+    hipStream_t us = D.ustream;
+    rc = upload_image(ctx->last, D.device, us, &ne[k].base);
+    if (!rc && jn.active()) {
+      rc = alloc_pool(D.device, us, &ne[k].pool);
+      if (!rc && hip_ok(hipMemcpyAsync(ne[k].pool->d_blob, jn.pool.data(), jn.pool.size() * 4, hipMemcpyHostToDevice, us)))
+        rc = -GPC_EDEV;
+      ne[k].jhdr = jn.hdr_off;
+    }
+    if (!rc && !ctx->last6.blob.empty()) {
+      rc = upload_image(ctx->last6, D.device, us, &ne[k].v6);
+      ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
+      ne[k].v6_bit = v6_group_bit(ctx->last6);
+    }
+    if (!rc && !ctx->svc_blob.empty()) rc = upload_words(ctx->svc_blob, D.device, us, &ne[k].svc);
+    if (!rc && (hip_ok(hipMalloc(&nc[k], cap * kCounterBytes * copies)) ||
+                hip_ok(hipMemset(nc[k], 0, cap * kCounterBytes * copies))))
+      rc = -GPC_EDEV;
+    if (!rc) rc = hip_ok(hipStreamSynchronize(us));
+  }
   if (rc) {
-    RetiredEpoch{std::move(ne)}.release(us);
-    if (nc) (void)hipFree(nc);
+    for (size_t k = 0; k < ctx->dev.size(); k++) {
+      (void)hipSetDevice(ctx->dev[k].device);
+      RetiredEpoch{std::move(ne[k])}.release(ctx->dev[k].ustream);
+      if (nc[k]) (void)hipFree(nc[k]);
+    }
     return rc;
   }
-  ne.epoch = ++ctx->epoch;
+  if (jn.active()) jn.uploaded = jn.pool.size();
+  const uint64_t epoch = ++ctx->epoch;
   std::lock_guard<std::mutex> d(ctx->data);
-  ctx->cur = std::move(ne);
-  ctx->d_counters = nc;
-  ctx->counter_cap = cap;
-  ctx->counter_copies = copies;
+  for (size_t k = 0; k < ctx->dev.size(); k++) {
+    DevState& D = ctx->dev[k];
+    ne[k].epoch = epoch;
+    D.cur = std::move(ne[k]);
+    D.d_counters = nc[k];
+    D.counter_cap = cap;
+    D.counter_copies = copies;
+  }
+  ctx->cur_epoch = epoch;
   return GPC_OK;
 }
 int gpc_compact(gpc_ctx* ctx) { return commit_impl(ctx, true); }
@@ -885,21 +959,21 @@ constexpr size_t kGroupMinImageBytes = size_t(4) << 20;
 
 // Grouping scratch of stream st with at least `need` bytes (ctx->data held). A buffer held for a
 // much larger earlier batch is given back when a batch needs less than an eighth of it.
-static int group_scratch(gpc_ctx* ctx, hipStream_t s, size_t need, uint8_t** out) {
+static int group_scratch(DevState& D, hipStream_t s, size_t need, uint8_t** out) {
   const StreamKey st = stream_key(s);
-  if (ctx->scratch.size() >= kScratchStreams && !ctx->scratch.count(st)) {
-    for (auto it = ctx->scratch.begin(); it != ctx->scratch.end();) {  // streams whose last batch is done
+  if (D.scratch.size() >= kScratchStreams && !D.scratch.count(st)) {
+    for (auto it = D.scratch.begin(); it != D.scratch.end();) {  // streams whose last batch is done
       if (!it->second.done || hipEventQuery(it->second.done) == hipSuccess) {
         (void)hipFree(it->second.p);
         if (it->second.done) (void)hipEventDestroy(it->second.done);
-        it = ctx->scratch.erase(it);
+        it = D.scratch.erase(it);
       } else {
         ++it;
       }
     }
     (void)hipGetLastError();
   }
-  StreamScratch& sc = ctx->scratch[st];
+  StreamScratch& sc = D.scratch[st];
   if (sc.bytes < need || sc.bytes / 8 > need) {
     dev_free(sc.p, s);  // after the launches already queued on s
     sc.p = nullptr;
@@ -912,8 +986,8 @@ static int group_scratch(gpc_ctx* ctx, hipStream_t s, size_t need, uint8_t** out
 }
 
 // The grouping scratch of stream st is in use until the launches just queued there have run.
-static int group_scratch_used(gpc_ctx* ctx, hipStream_t st) {
-  StreamScratch& sc = ctx->scratch[stream_key(st)];
+static int group_scratch_used(DevState& D, hipStream_t st) {
+  StreamScratch& sc = D.scratch[stream_key(st)];
   if (!sc.done && hip_ok(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming))) return -GPC_EDEV;
   return hip_ok(hipEventRecord(sc.done, st));
 }
@@ -921,9 +995,9 @@ static int group_scratch_used(gpc_ctx* ctx, hipStream_t st) {
 // Grouping scratch for a batch the pre-pass would speed up. Grouping is a performance choice: when
 // it was not forced (gpc_config.group_packets == 0) and its scratch cannot be had, the batch runs
 // ungrouped instead of failing.
-static int group_scratch_for(gpc_ctx* ctx, hipStream_t st, size_t need, uint8_t** out) {
+static int group_scratch_for(gpc_ctx* ctx, DevState& D, hipStream_t st, size_t need, uint8_t** out) {
   *out = nullptr;
-  const int e = group_scratch(ctx, st, need, out);
+  const int e = group_scratch(D, st, need, out);
   if (e == -GPC_ENOMEM && ctx->cfg.group_packets == 0) {
     (void)hipGetLastError();
     *out = nullptr;
@@ -942,40 +1016,52 @@ static bool group_batch(const gpc_ctx* ctx, size_t n, size_t image_bytes) {
 // lines a wave shares matter more (C3 13.2 ms by address vs 15.4 by scan length, C4 14.3 vs 16.4).
 static uint32_t group_key(const gpc_ctx* ctx) {
   if (ctx->group_key != GPC_GROUP_KEY_AUTO) return ctx->group_key;
-  const DevImage& b = *ctx->cur.base;
+  const DevImage& b = *ctx->dev[0].cur.base;
   return (b.sort_table[0] || b.sort_table[1]) ? uint32_t(GPC_GROUP_KEY_SCAN) : uint32_t(GPC_GROUP_KEY_ADDR);
 }
 
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
-  return gpc_classify_lb(ctx, pk, n, out, nullptr, count, stream);
+  return gpc_classify_on(ctx, 0, pk, n, out, nullptr, count, stream);
 }
 
 int gpc_classify_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, gpc_lb_result* lb_out, int32_t count,
                     void* stream) {
-  if (!ctx || !pk || (!out && n) || n > GPC_MAX_BATCH) return -GPC_EINVAL;
+  return gpc_classify_on(ctx, 0, pk, n, out, lb_out, count, stream);
+}
+
+// Epoch lifetime bookkeeping after launches on stream st of slot D (ctx->data held).
+static int note_launch(gpc_ctx* ctx, DevState& D, hipStream_t st) {
+  D.launch_epoch[stream_key(st)] = D.cur.epoch;
+  hipEvent_t& ev = D.cur.last_use[stream_key(st)];  // epoch lifetime: retired epochs are freed once drained
+  if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
+  (void)ctx;
+  return hip_ok(hipEventRecord(ev, st));
+}
+
+int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
+                    gpc_lb_result* lb_out, int32_t count, void* stream) {
+  if (!ctx || !pk || (!out && n) || n > GPC_MAX_BATCH || slot >= ctx->dev.size()) return -GPC_EINVAL;
   if (n && (!pk->src || !pk->dst || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
-  if (!ctx->cur.base) return -GPC_EINVAL;  // nothing committed yet
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.jhdr ? ctx->cur.pool->d_blob : nullptr, ctx->cur.jhdr,
-               ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr, 0u,
-               {ctx->cur.base->sort_table[0], ctx->cur.base->sort_table[1]},
-               uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
+  DevState& D = ctx->dev[slot];
+  if (!D.cur.base) return -GPC_EINVAL;  // nothing committed yet
+  if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
+  EpochArgs ep{D.cur.base->d_hdr, D.cur.base->d_blob, D.cur.jhdr ? D.cur.pool->d_blob : nullptr, D.cur.jhdr,
+               D.cur.svc ? D.cur.svc->d_blob : nullptr, 0u, {D.cur.base->sort_table[0], D.cur.base->sort_table[1]},
+               uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
   // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
   // the next batch on that stream (launches of one stream run in order), so callers on different
   // streams never share one and the data path does no allocation once warm
-  GroupArgs ga{nullptr, group_key(ctx), ctx->cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0, ctx->group_unpermute};
-  if (group_batch(ctx, n, ctx->cur.base->bytes))
-    if (const int e = group_scratch_for(ctx, st, group_scratch_bytes(*pk, n, false), &ga.scratch)) return e;
-  int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), ctx->d_counters, count,
-                           ga.scratch ? &ga : nullptr, st, n ? next_marks(ctx) : nullptr);
-  if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
+  GroupArgs ga{nullptr, group_key(ctx), D.cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0, ctx->group_unpermute,
+               D.cur.svc && lb_out && ctx->group_unpermute};
+  if (group_batch(ctx, n, D.cur.base->bytes))
+    if (const int e = group_scratch_for(ctx, D, st, group_scratch_bytes(*pk, n, false, ga.lb), &ga.scratch)) return e;
+  int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), D.d_counters, count,
+                           ga.scratch ? &ga : nullptr, st, n ? next_marks(D) : nullptr);
+  if (!rc && ga.scratch) rc = group_scratch_used(D, st);
   if (rc || n == 0) return rc;
-  ctx->launch_epoch[stream_key(st)] = ctx->cur.epoch;
-  hipEvent_t& ev = ctx->cur.last_use[stream_key(st)];  // epoch lifetime: retired epochs are freed once drained
-  if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
-  return hip_ok(hipEventRecord(ev, st));
+  return note_launch(ctx, D, st);
 }
 
 int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pk, gpc_verdict* out, gpc_lb_result* lb_out, gpc_trace_step* steps,
@@ -983,7 +1069,7 @@ int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pk, gpc_verdict* out, gpc_lb_resu
   static_assert(sizeof(gpc_trace_step) == sizeof(TraceStep), "gpc_trace_step mirrors core.hpp TraceStep");
   if (!ctx || !pk || !out || !pk->src || !pk->dst || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)
     return -GPC_EINVAL;
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  if (hip_ok(hipSetDevice(ctx->dev[0].device))) return -GPC_EDEV;
   // one packet: every present column's element 0 goes into one small device buffer
   struct Col {
     const void* h;
@@ -1015,11 +1101,12 @@ int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pk, gpc_verdict* out, gpc_lb_resu
   uint32_t* dn = reinterpret_cast<uint32_t*>(buf + 64 + kMaxTraceSteps * sizeof(TraceStep));
   if (!rc) {
     std::lock_guard<std::mutex> g(ctx->data);
-    if (!ctx->cur.base) {
+    const DevEpoch& cur = ctx->dev[0].cur;
+    if (!cur.base) {
       rc = -GPC_EINVAL;  // nothing committed yet
     } else {
-      EpochArgs ep{ctx->cur.base->d_hdr, ctx->cur.base->d_blob, ctx->cur.jhdr ? ctx->cur.pool->d_blob : nullptr,
-                   ctx->cur.jhdr, ctx->cur.svc ? ctx->cur.svc->d_blob : nullptr, 0u, {0, 0}, 0u, 0u};
+      EpochArgs ep{cur.base->d_hdr, cur.base->d_blob, cur.jhdr ? cur.pool->d_blob : nullptr, cur.jhdr,
+                   cur.svc ? cur.svc->d_blob : nullptr, 0u, {0, 0}, 0u, 0u};
       rc = launch_trace(ep, d, dout, dlb, dsteps, dn, nullptr);
       if (!rc) rc = hip_ok(hipDeviceSynchronize());  // the epoch stays alive while it is current
     }
@@ -1041,32 +1128,35 @@ int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict
 }
 
 int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count, void* stream) {
-  if (!ctx || !pk || (!out && n) || n > GPC_MAX_BATCH) return -GPC_EINVAL;
+  return gpc_classify6_on(ctx, 0, pk, n, out, count, stream);
+}
+
+int gpc_classify6_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count,
+                     void* stream) {
+  if (!ctx || !pk || (!out && n) || n > GPC_MAX_BATCH || slot >= ctx->dev.size()) return -GPC_EINVAL;
   if (n && (!pk->src6 || !pk->dst6 || !pk->sport || !pk->dport || !pk->proto || !pk->out_port)) return -GPC_EINVAL;
   for (const void* c : {(const void*)pk->src6, (const void*)pk->dst6, (const void*)pk->ct_src6, (const void*)pk->ct_dst6})
     if (reinterpret_cast<uintptr_t>(c) % 16) return -GPC_EINVAL;  // one 128-bit load per address
   std::lock_guard<std::mutex> d(ctx->data);
-  if (!ctx->cur.v6) return -GPC_EINVAL;  // IPv6 disabled or nothing committed yet
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  EpochArgs ep{ctx->cur.v6->d_hdr, ctx->cur.v6->d_blob, nullptr, 0u, nullptr, ctx->cur.v6_lpm, {0, 0},
-               uint32_t(ctx->counter_cap * kCounterWords), ctx->counter_copies - 1};
+  DevState& D = ctx->dev[slot];
+  if (!D.cur.v6) return -GPC_EINVAL;  // IPv6 disabled or nothing committed yet
+  if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
+  EpochArgs ep{D.cur.v6->d_hdr, D.cur.v6->d_blob, nullptr, 0u, nullptr, D.cur.v6_lpm, {0, 0},
+               uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, ctx->cur.v6_bit, ctx->group_unpermute};
-  if (ctx->group_v6 && group_batch(ctx, n, ctx->cur.v6->bytes))
-    if (const int e = group_scratch_for(ctx, st, group_scratch_bytes(*pk, n, true), &ga.scratch)) return e;
-  int rc = launch_classify6(ep, *pk, n, out, ctx->d_counters, count, ga.scratch ? &ga : nullptr, st,
-                            n ? next_marks(ctx) : nullptr);
-  if (!rc && ga.scratch) rc = group_scratch_used(ctx, st);
+  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, D.cur.v6_bit, ctx->group_unpermute};
+  if (ctx->group_v6 && group_batch(ctx, n, D.cur.v6->bytes))
+    if (const int e = group_scratch_for(ctx, D, st, group_scratch_bytes(*pk, n, true, false), &ga.scratch)) return e;
+  int rc = launch_classify6(ep, *pk, n, out, D.d_counters, count, ga.scratch ? &ga : nullptr, st,
+                            n ? next_marks(D) : nullptr);
+  if (!rc && ga.scratch) rc = group_scratch_used(D, st);
   if (rc || n == 0) return rc;
-  ctx->launch_epoch[stream_key(st)] = ctx->cur.epoch;
-  hipEvent_t& ev = ctx->cur.last_use[stream_key(st)];
-  if (!ev && hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return -GPC_EDEV;
-  return hip_ok(hipEventRecord(ev, st));
+  return note_launch(ctx, D, st);
 }
 
 int gpc_classify6_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, int32_t count) {
   if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  if (hip_ok(hipSetDevice(ctx->dev[0].device))) return -GPC_EDEV;
   if (n == 0) return GPC_OK;
   gpc_pkt_soa d{};
   std::vector<void*> allocs;
@@ -1109,8 +1199,13 @@ int gpc_classify6_host(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdic
 
 int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, gpc_lb_result* lb_out,
                          int32_t count) {
-  if (!ctx || !pk || (!out && n)) return -GPC_EINVAL;
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
+  return gpc_classify_host_on(ctx, 0, pk, n, out, lb_out, count);
+}
+
+int gpc_classify_host_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
+                         gpc_lb_result* lb_out, int32_t count) {
+  if (!ctx || !pk || (!out && n) || slot >= ctx->dev.size()) return -GPC_EINVAL;
+  if (hip_ok(hipSetDevice(ctx->dev[slot].device))) return -GPC_EDEV;
   if (n == 0) return GPC_OK;
   gpc_pkt_soa d{};
   std::vector<void*> allocs;
@@ -1145,7 +1240,7 @@ int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verd
   void* dlb = nullptr;
   if (!rc && hip_ok(hipMalloc(&dout, n * 2 * sizeof(gpc_verdict)))) rc = -GPC_EDEV;
   if (!rc && lb_out && hip_ok(hipMalloc(&dlb, n * sizeof(gpc_lb_result)))) rc = -GPC_EDEV;
-  if (!rc) rc = gpc_classify_lb(ctx, &d, n, (gpc_verdict*)dout, (gpc_lb_result*)dlb, count, nullptr);
+  if (!rc) rc = gpc_classify_on(ctx, slot, &d, n, (gpc_verdict*)dout, (gpc_lb_result*)dlb, count, nullptr);
   if (!rc && hip_ok(hipDeviceSynchronize())) rc = -GPC_EDEV;
   if (!rc && hip_ok(hipMemcpy(out, dout, n * 2 * sizeof(gpc_verdict), hipMemcpyDeviceToHost))) rc = -GPC_EDEV;
   if (!rc && lb_out && hip_ok(hipMemcpy(lb_out, dlb, n * sizeof(gpc_lb_result), hipMemcpyDeviceToHost))) rc = -GPC_EDEV;
@@ -1156,10 +1251,15 @@ int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pk, size_t n, gpc_verd
 }
 
 int gpc_counters(gpc_ctx* ctx, uint64_t** dev, const uint32_t** slot_conj, size_t* n_slots) {
-  if (!ctx) return -GPC_EINVAL;
+  return gpc_counters_on(ctx, 0, dev, slot_conj, n_slots);
+}
+
+int gpc_counters_on(gpc_ctx* ctx, uint32_t slot, uint64_t** dev, const uint32_t** slot_conj, size_t* n_slots) {
+  if (!ctx || slot >= ctx->dev.size()) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  if (int rc = fold_counters(ctx)) return rc;  // the caller sees one array (copy 0)
-  if (dev) *dev = reinterpret_cast<uint64_t*>(ctx->d_counters);
+  DevState& D = ctx->dev[slot];
+  if (int rc = fold_counters(D)) return rc;  // the caller sees one array (copy 0)
+  if (dev) *dev = reinterpret_cast<uint64_t*>(D.d_counters);
   if (slot_conj) *slot_conj = ctx->slot_conj.data();
   if (n_slots) *n_slots = ctx->slot_conj.size();
   return GPC_OK;
@@ -1168,23 +1268,28 @@ int gpc_counters(gpc_ctx* ctx, uint64_t** dev, const uint32_t** slot_conj, size_
 int gpc_reset_counters(gpc_ctx* ctx) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  if (!ctx->d_counters) return GPC_OK;
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  if (hip_ok(hipDeviceSynchronize()) ||
-      hip_ok(hipMemset(ctx->d_counters, 0, ctx->counter_cap * kCounterBytes * ctx->counter_copies)))
-    return -GPC_EDEV;
+  for (DevState& D : ctx->dev) {
+    if (!D.d_counters) continue;
+    if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
+    if (hip_ok(hipDeviceSynchronize()) || hip_ok(hipMemset(D.d_counters, 0, D.counter_cap * kCounterBytes * D.counter_copies)))
+      return -GPC_EDEV;
+  }
   return GPC_OK;
 }
 
+// NetworkPolicyMetrics over every device slot of the context: each slot's counters are folded,
+// copied back and summed per rule (the in-process counterpart of the RCCL all-reduce).
 int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
-  std::vector<unsigned long long> h(ctx->slot_conj.size() * kCounterWords, 0);
-  if (int rc = fold_counters(ctx)) return rc;
-  if (ctx->d_counters && !h.empty()) {
-    if (hip_ok(hipSetDevice(ctx->cfg.device)) || hip_ok(hipDeviceSynchronize()) ||
-        hip_ok(hipMemcpy(h.data(), ctx->d_counters, h.size() * 8, hipMemcpyDeviceToHost)))
+  std::vector<unsigned long long> h(ctx->slot_conj.size() * kCounterWords, 0), part(h.size());
+  for (DevState& D : ctx->dev) {
+    if (int rc = fold_counters(D)) return rc;
+    if (!D.d_counters || h.empty()) continue;
+    if (hip_ok(hipSetDevice(D.device)) || hip_ok(hipDeviceSynchronize()) ||
+        hip_ok(hipMemcpy(part.data(), D.d_counters, part.size() * 8, hipMemcpyDeviceToHost)))
       return -GPC_EDEV;
+    for (size_t i = 0; i < h.size(); i++) h[i] += part[i];
   }
   size_t k = 0;
   for (size_t s = 0; s < ctx->slot_conj.size(); s++) {
@@ -1207,16 +1312,17 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   std::lock_guard<std::mutex> g(ctx->ctl);
   std::memset(out, 0, sizeof *out);
   out->epoch = ctx->epoch;
-  out->device_bytes = ctx->cur.base ? ctx->cur.base->bytes : 0;
+  const DevEpoch& cur = ctx->dev[0].cur;
+  out->device_bytes = cur.base ? cur.base->bytes : 0;
   out->overlay_bytes = ctx->journal.active() ? ctx->journal.pool.size() * 4 : 0;
   out->n_overlay_rules = ctx->journal.n_live;
   out->n_tombstones = ctx->journal.n_tombstones();
   out->n_full_builds = ctx->n_full;
   out->n_delta_builds = ctx->n_delta;
   out->n_background_builds = ctx->n_bg;
-  if (ctx->cur.base) {
+  if (cur.base) {
     out->group_key = group_key(ctx);
-    out->lane_sort = ctx->cur.base->sort_table[0] | uint32_t(ctx->cur.base->sort_table[1]) << 8;
+    out->lane_sort = cur.base->sort_table[0] | uint32_t(cur.base->sort_table[1]) << 8;
   }
   for (int i = 0; i < 6; i++) {
     out->n_rules[i] = ctx->last.n_rules[i];
@@ -1264,18 +1370,19 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
 int gpc_set_launch_timing(gpc_ctx* ctx, uint32_t slots) {
   if (!ctx || slots > 4096) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  for (auto& m : ctx->marks) (void)hipEventSynchronize(m.ev[LaunchMarks::kMax - 1]);
-  (void)hipDeviceSynchronize();  // no recorded event is still pending when its set is destroyed
-  free_marks(ctx);
-  ctx->marks.resize(slots);
-  for (auto& m : ctx->marks) {
-    m.n = 0;
-    for (auto& e : m.ev)
-      if (hip_ok(hipEventCreate(&e))) {
-        free_marks(ctx);
-        return -GPC_EDEV;
-      }
+  for (DevState& D : ctx->dev) {
+    if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
+    (void)hipDeviceSynchronize();  // no recorded event is still pending when its set is destroyed
+    free_marks(D);
+    D.marks.resize(slots);
+    for (auto& m : D.marks) {
+      m.n = 0;
+      for (auto& e : m.ev)
+        if (hip_ok(hipEventCreate(&e))) {
+          free_marks(D);
+          return -GPC_EDEV;
+        }
+    }
   }
   return GPC_OK;
 }
@@ -1286,23 +1393,26 @@ int gpc_launch_times(gpc_ctx* ctx, gpc_launch_time* out, size_t cap, size_t* n) 
                                                   "unpermute"};
   double ms[kLaunchKinds] = {};
   uint32_t cnt[kLaunchKinds] = {};
-  size_t dropped;
+  size_t dropped = 0;
   {
     std::lock_guard<std::mutex> d(ctx->data);
-    const size_t S = ctx->marks.size();
-    for (size_t k = 0; k < ctx->marks_used; k++) {  // oldest first
-      LaunchMarks& m = ctx->marks[(ctx->marks_next + S - ctx->marks_used + k) % S];
-      if (m.n < 2 || hip_ok(hipEventSynchronize(m.ev[m.n - 1]))) continue;
-      for (int i = 0; i + 1 < m.n; i++) {
-        float t = 0.f;
-        if (m.kind[i] < kLaunchKinds && !hip_ok(hipEventElapsedTime(&t, m.ev[i], m.ev[i + 1]))) {
-          ms[m.kind[i]] += t;
-          cnt[m.kind[i]]++;
+    for (DevState& D : ctx->dev) {
+      const size_t S = D.marks.size();
+      if (S && hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
+      for (size_t k = 0; k < D.marks_used; k++) {  // oldest first
+        LaunchMarks& m = D.marks[(D.marks_next + S - D.marks_used + k) % S];
+        if (m.n < 2 || hip_ok(hipEventSynchronize(m.ev[m.n - 1]))) continue;
+        for (int i = 0; i + 1 < m.n; i++) {
+          float t = 0.f;
+          if (m.kind[i] < kLaunchKinds && !hip_ok(hipEventElapsedTime(&t, m.ev[i], m.ev[i + 1]))) {
+            ms[m.kind[i]] += t;
+            cnt[m.kind[i]]++;
+          }
         }
       }
+      dropped += D.marks_dropped;
+      D.marks_used = D.marks_dropped = 0;
     }
-    dropped = ctx->marks_dropped;
-    ctx->marks_used = ctx->marks_dropped = 0;
   }
   size_t k = 0;
   for (int i = 0; i < kLaunchKinds; i++) {
@@ -1323,10 +1433,14 @@ int gpc_launch_times(gpc_ctx* ctx, gpc_launch_time* out, size_t cap, size_t* n) 
 int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch) {
   if (!ctx || !epoch) return -GPC_EINVAL;
   std::lock_guard<std::mutex> d(ctx->data);
-  auto it = ctx->launch_epoch.find(stream_key((hipStream_t)stream));
-  if (it == ctx->launch_epoch.end()) return -GPC_ENOTFOUND;
-  *epoch = it->second;
-  return GPC_OK;
+  for (DevState& D : ctx->dev) {
+    auto it = D.launch_epoch.find(stream_key((hipStream_t)stream));
+    if (it != D.launch_epoch.end()) {
+      *epoch = it->second;
+      return GPC_OK;
+    }
+  }
+  return -GPC_ENOTFOUND;
 }
 
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr) {
@@ -1364,7 +1478,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   }
   // a background compaction result: install it, then append what changed after its commit
   bool installed = false;
-  std::shared_ptr<DevImage> bg_base, bg_pool;
+  std::vector<std::shared_ptr<DevImage>> bg_base, bg_pool;  // per device slot
   size_t bg_uploaded = 0;
   {
     std::unique_lock<std::mutex> lk(ctx->comp.mu);
@@ -1390,8 +1504,8 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       }
       ctx->comp.base.reset();
       ctx->comp.journal.reset();
-      ctx->comp.dbase.reset();
-      ctx->comp.dpool.reset();
+      ctx->comp.dbase.clear();
+      ctx->comp.dpool.clear();
       ctx->dirty_hist.clear();
     }
   }
@@ -1463,114 +1577,149 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   ctx->slot_conj = ctx->slots.slot_conj();
   if (full) ctx->n_full++;
   else ctx->n_delta++;
-  if (hip_ok(hipSetDevice(ctx->cfg.device))) return -GPC_EDEV;
-  if (!ctx->ustream && hip_ok(hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking))) return -GPC_EDEV;
-  hipStream_t us = ctx->ustream;
-  collect_retired(ctx, false);
-  DevEpoch ne;
-  if (installed && bg_base && bg_pool) {  // uploaded by the compactor
-    bg_base->s = us;
-    bg_pool->s = us;
-    ne.base = std::move(bg_base);
-    ne.pool = std::move(bg_pool);
-    ctx->journal.uploaded = bg_uploaded;
-  } else if (full || installed || !ctx->cur.base) {
-    if ((rc = upload_image(ctx->last, us, &ne.base))) return rc;
-    ctx->journal.uploaded = 0;  // the journal pool of the new base is allocated on first use
-  } else {
-    ne.base = ctx->cur.base;
-    ne.pool = ctx->cur.pool;
-  }
+  // The new epoch goes to every device slot: uploads on each slot's stream, one synchronize per
+  // slot, then all slots publish it under one data lock (no launch sees two epochs across slots).
+  const size_t nd = ctx->dev.size();
+  std::vector<DevEpoch> ne(nd);
+  std::vector<unsigned long long*> nc(nd, nullptr);
+  std::vector<size_t> new_cap(nd, 0);
+  std::vector<uint32_t> new_copies(nd, 1);
+  auto fail = [&](int r) {  // releases what this commit allocated on every slot
+    for (size_t k = 0; k < nd; k++) {
+      (void)hipSetDevice(ctx->dev[k].device);
+      if (ctx->dev[k].ustream) (void)hipStreamSynchronize(ctx->dev[k].ustream);
+      RetiredEpoch{std::move(ne[k])}.release(ctx->dev[k].ustream);
+      if (nc[k] && nc[k] != ctx->dev[k].d_counters) (void)hipFree(nc[k]);
+    }
+    return r;
+  };
+  const bool bg_ok = installed && bg_base.size() == nd && bg_pool.size() == nd;
   Journal& jn = ctx->journal;
-  if (jn.active() && !ne.pool) {
-    auto pool = std::make_shared<DevImage>();
-    pool->s = us;
-    pool->bytes = kPoolWords * 4;
-    if (hip_ok(dev_alloc((void**)&pool->d_blob, pool->bytes, us))) return -GPC_EDEV;
-    ne.pool = std::move(pool);
-    jn.uploaded = 0;
+  bool new_pool = false;
+  for (size_t k = 0; k < nd; k++) {
+    DevState& D = ctx->dev[k];
+    if (hip_ok(hipSetDevice(D.device))) return fail(-GPC_EDEV);
+    if (!D.ustream && hip_ok(hipStreamCreateWithFlags(&D.ustream, hipStreamNonBlocking))) return fail(-GPC_EDEV);
+    hipStream_t us = D.ustream;
+    collect_retired(D, false);
+    if (bg_ok && bg_base[k] && bg_pool[k]) {  // uploaded by the compactor
+      bg_base[k]->s = us;
+      bg_pool[k]->s = us;
+      ne[k].base = std::move(bg_base[k]);
+      ne[k].pool = std::move(bg_pool[k]);
+    } else if (full || installed || !D.cur.base) {
+      if ((rc = upload_image(ctx->last, D.device, us, &ne[k].base))) return fail(rc);
+    } else {
+      ne[k].base = D.cur.base;
+      ne[k].pool = D.cur.pool;
+    }
+    if (jn.active() && !ne[k].pool) {  // the journal pool of a new base is allocated on first use
+      if ((rc = alloc_pool(D.device, us, &ne[k].pool))) return fail(rc);
+      new_pool = true;
+    }
   }
-  if (jn.active() && jn.pool.size() > jn.uploaded) {
-    // Append-only: only the new tail travels, through a pinned buffer and padded to at least
-    // kMinUploadBytes (the padding lands in not-yet-used pool space) so the runtime takes the DMA
-    // path; a small copy may otherwise run as a blit kernel queued behind in-flight classification.
-    const size_t tail = (jn.pool.size() - jn.uploaded) * 4;
-    const size_t room = ne.pool->bytes - jn.uploaded * 4;
-    const size_t bytes = std::min(std::max(tail, kMinUploadBytes), room);
-    if (ctx->stage_bytes < bytes) {
+  if (bg_ok) jn.uploaded = bg_uploaded;
+  else if (full || installed || !ctx->dev[0].cur.base) jn.uploaded = 0;
+  if (new_pool) jn.uploaded = 0;
+  // Append-only: only the new journal tail travels, staged once in a pinned buffer and padded to at
+  // least kMinUploadBytes (the padding lands in not-yet-used pool space) so the runtime takes the
+  // DMA path; a small copy may otherwise run as a blit kernel queued behind in-flight classification.
+  const bool tail = jn.active() && jn.pool.size() > jn.uploaded;
+  size_t tail_bytes = 0, copy_bytes = 0;
+  if (tail) {
+    tail_bytes = (jn.pool.size() - jn.uploaded) * 4;
+    copy_bytes = std::min(std::max(tail_bytes, kMinUploadBytes), kPoolWords * 4 - jn.uploaded * 4);
+    if (ctx->stage_bytes < copy_bytes) {
       if (ctx->stage) (void)hipHostFree(ctx->stage);
       ctx->stage = nullptr;
       ctx->stage_bytes = 0;
-      const size_t cap = std::max(bytes, size_t(4) << 20);
-      if (hip_ok(hipHostMalloc(&ctx->stage, cap, hipHostMallocDefault))) return -GPC_EDEV;
+      const size_t cap = std::max(copy_bytes, size_t(4) << 20);
+      if (hip_ok(hipHostMalloc(&ctx->stage, cap, hipHostMallocPortable))) return fail(-GPC_EDEV);
       ctx->stage_bytes = cap;
     }
-    std::memcpy(ctx->stage, jn.pool.data() + jn.uploaded, tail);
-    if (hip_ok(hipMemcpyAsync(ne.pool->d_blob + jn.uploaded, ctx->stage, bytes, hipMemcpyHostToDevice, us)))
-      return -GPC_EDEV;
-    jn.uploaded = jn.pool.size();
+    std::memcpy(ctx->stage, jn.pool.data() + jn.uploaded, tail_bytes);
   }
-  ne.jhdr = jn.active() ? jn.hdr_off : 0;
-  if (!v6_changed) {
-    ne.v6 = ctx->cur.v6;
-    ne.v6_lpm = ctx->cur.v6_lpm;
-    ne.v6_bit = ctx->cur.v6_bit;
-  } else if (!ctx->last6.blob.empty()) {
-    if ((rc = upload_image(ctx->last6, us, &ne.v6))) return rc;
-    ne.v6_lpm = ctx->last6.hdr.v6_lpm;
-    ne.v6_bit = v6_group_bit(ctx->last6);
-  }
-  if (!svc_changed) ne.svc = ctx->cur.svc;
-  else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, us, &ne.svc))) return rc;
-  ne.epoch = ++ctx->epoch;
-  // counters: grow to the slot count, zero released slots (their Metric flows were deleted)
-  size_t need = ctx->slots.size() ? ctx->slots.size() : 1;
-  unsigned long long* nc = ctx->d_counters;
-  bool grow = need > ctx->counter_cap;
-  const size_t new_cap = grow ? std::max(need, ctx->counter_cap * 2) : ctx->counter_cap;
-  const uint32_t new_copies = grow ? counter_copies_for(new_cap) : ctx->counter_copies;
-  if (grow) {
-    const size_t bytes = new_cap * kCounterBytes * new_copies;
-    if (hip_ok(hipMalloc(&nc, bytes)) || hip_ok(hipMemset(nc, 0, bytes))) {
-      RetiredEpoch{std::move(ne)}.release(us);
-      return -GPC_EDEV;
+  const uint32_t jhdr = jn.active() ? jn.hdr_off : 0;
+  const uint64_t epoch = ctx->epoch + 1;
+  const size_t need = ctx->slots.size() ? ctx->slots.size() : 1;
+  for (size_t k = 0; k < nd; k++) {
+    DevState& D = ctx->dev[k];
+    hipStream_t us = D.ustream;
+    if (hip_ok(hipSetDevice(D.device))) return fail(-GPC_EDEV);
+    if (tail && hip_ok(hipMemcpyAsync(ne[k].pool->d_blob + jn.uploaded, ctx->stage, copy_bytes, hipMemcpyHostToDevice, us)))
+      return fail(-GPC_EDEV);
+    ne[k].jhdr = jhdr;
+    if (!v6_changed) {
+      ne[k].v6 = D.cur.v6;
+      ne[k].v6_lpm = D.cur.v6_lpm;
+      ne[k].v6_bit = D.cur.v6_bit;
+    } else if (!ctx->last6.blob.empty()) {
+      if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
+      ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
+      ne[k].v6_bit = v6_group_bit(ctx->last6);
+    }
+    if (!svc_changed) ne[k].svc = D.cur.svc;
+    else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, D.device, us, &ne[k].svc))) return fail(rc);
+    ne[k].epoch = epoch;
+    // counters: grow to the slot count, zero released slots (their Metric flows were deleted)
+    nc[k] = D.d_counters;
+    new_cap[k] = D.counter_cap;
+    new_copies[k] = D.counter_copies;
+    if (need > D.counter_cap) {
+      new_cap[k] = std::max(need, D.counter_cap * 2);
+      new_copies[k] = counter_copies_for(new_cap[k]);
+      const size_t bytes = new_cap[k] * kCounterBytes * new_copies[k];
+      nc[k] = nullptr;
+      if (hip_ok(hipMalloc(&nc[k], bytes)) || hip_ok(hipMemset(nc[k], 0, bytes))) return fail(-GPC_EDEV);
     }
   }
-  if (hip_ok(hipStreamSynchronize(us))) {  // the new epoch is resident before it is published
-    RetiredEpoch{std::move(ne)}.release(us);
-    return -GPC_EDEV;
-  }
-  DevEpoch old;
-  unsigned long long* old_counters = nullptr;
-  const size_t old_cap = ctx->counter_cap;
-  const uint32_t old_copies = ctx->counter_copies;
+  for (size_t k = 0; k < nd; k++)  // the new epoch is resident on every slot before it is published
+    if (hip_ok(hipSetDevice(ctx->dev[k].device)) || hip_ok(hipStreamSynchronize(ctx->dev[k].ustream)))
+      return fail(-GPC_EDEV);
+  if (tail) jn.uploaded = jn.pool.size();
+  ctx->epoch = epoch;
+  std::vector<DevEpoch> old(nd);
+  std::vector<unsigned long long*> old_counters(nd, nullptr);
+  std::vector<size_t> old_cap(nd);
+  std::vector<uint32_t> old_copies(nd);
   {
     std::lock_guard<std::mutex> d(ctx->data);
-    old = std::move(ctx->cur);
-    ctx->cur = std::move(ne);
-    if (grow) {
-      old_counters = ctx->d_counters;
-      ctx->d_counters = nc;
-      ctx->counter_cap = new_cap;
-      ctx->counter_copies = new_copies;
+    for (size_t k = 0; k < nd; k++) {
+      DevState& D = ctx->dev[k];
+      old[k] = std::move(D.cur);
+      D.cur = std::move(ne[k]);
+      old_cap[k] = D.counter_cap;
+      old_copies[k] = D.counter_copies;
+      if (nc[k] != D.d_counters) {
+        old_counters[k] = D.d_counters;
+        D.d_counters = nc[k];
+        D.counter_cap = new_cap[k];
+        D.counter_copies = new_copies[k];
+      }
     }
+    ctx->cur_epoch = epoch;
   }
-  // the previous epoch is freed once every stream that launched on it has passed that launch
-  ctx->retired.push_back(RetiredEpoch{std::move(old)});
-  if (old_counters) {
-    // Every launch that could still add to the old array was queued before the swap: once the
-    // device has drained them, all its replicas are merged into the new copy 0 (atomically: new
-    // launches may already be adding to it), so no count is lost however the growth interleaves.
-    (void)hipDeviceSynchronize();
-    (void)launch_merge_counters(ctx->d_counters, old_counters, uint64_t(old_cap) * kCounterWords, old_copies,
-                                uint64_t(old_cap) * kCounterWords, nullptr);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(old_counters);
+  for (size_t k = 0; k < nd; k++) {
+    DevState& D = ctx->dev[k];
+    (void)hipSetDevice(D.device);
+    // the previous epoch is freed once every stream that launched on it has passed that launch
+    D.retired.push_back(RetiredEpoch{std::move(old[k])});
+    if (old_counters[k]) {
+      // Every launch that could still add to the old array was queued before the swap: once the
+      // device has drained them, all its replicas are merged into the new copy 0 (atomically: new
+      // launches may already be adding to it), so no count is lost however the growth interleaves.
+      (void)hipDeviceSynchronize();
+      (void)launch_merge_counters(D.d_counters, old_counters[k], uint64_t(old_cap[k]) * kCounterWords, old_copies[k],
+                                  uint64_t(old_cap[k]) * kCounterWords, nullptr);
+      (void)hipDeviceSynchronize();
+      (void)hipFree(old_counters[k]);
+    }
+    for (uint32_t s : ctx->released_slots)
+      if (s < D.counter_cap)
+        for (uint32_t r = 0; r < D.counter_copies; r++)
+          (void)hipMemsetAsync(D.d_counters + kCounterWords * (size_t(r) * D.counter_cap + s), 0, kCounterBytes,
+                               D.ustream);
   }
-  for (uint32_t s : ctx->released_slots)
-    if (s < ctx->counter_cap)
-      for (uint32_t r = 0; r < ctx->counter_copies; r++)
-        (void)hipMemsetAsync(ctx->d_counters + kCounterWords * (size_t(r) * ctx->counter_cap + s), 0, kCounterBytes, us);
   ctx->released_slots.clear();
   return GPC_OK;
 }

@@ -384,9 +384,16 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if (kSvc) {  // both launches derive the same Endpoint (the selection is a pure function of the packet)
     uint32_t lb[4];
     const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
-    if (kStage != 2 && lb_out) lb_out[at()] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+    // grouped with the un-permute (gout): results in grouped order, unpermute_kernel stores them
+    if (kStage != 2 && lb_out) lb_out[gout ? i : at()] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
     if (f & GPC_LB_NO_ENDPOINT) {  // EndpointDNAT serviceNoEndpointFlow: rejected before the policy stages
-      if (kStage != 2) out[at()] = make_uint4(0u, pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0), 0u, 0u);
+      const uint32_t rj = pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0);
+      if (kStage == 0 && gout) {
+        mid[i] = make_uint2(0u, rj);
+        gout[i] = make_uint2(0u, 0u);
+      } else if (kStage != 2) {
+        out[at()] = make_uint4(0u, rj, 0u, 0u);
+      }
       return;
     }
   } else if (kStage != 2 && lb_out) {
@@ -425,7 +432,8 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     const StageOut s1 = walk_stage<kDelta, false>(im, p, 1u, nullptr, nullptr);
     count_one(s1);
     uint2* const o2 = reinterpret_cast<uint2*>(out);
-    o2[2 * at()] = make_uint2(s1.v.conj, s1.v.packed);
+    if (gout) mid[i] = make_uint2(s1.v.conj, s1.v.packed);  // grouped order (un-permuted afterwards)
+    else o2[2 * at()] = make_uint2(s1.v.conj, s1.v.packed);
     const uint32_t a1 = s1.v.packed & 0xffu;
     uint32_t gc = 0u, gp = 0u;  // ingress NONE: dropped in egress
     if (a1 != RV_DROP && a1 != RV_REJECT && a1 != RV_ISO_DROP) {
@@ -438,7 +446,8 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
         gp = s2.v.packed;
       }
     }
-    o2[2 * at() + 1] = make_uint2(gc, gp);
+    if (gout) gout[i] = make_uint2(gc, gp);
+    else o2[2 * at() + 1] = make_uint2(gc, gp);
     return;
   }
   const StageOut s = walk_stage<kDelta, false>(im, p, kStage == 2 ? 4u : 1u, nullptr, nullptr);
@@ -453,23 +462,22 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
 
 // Verdict pairs of a grouped batch in caller order: the egress half from mid (grouped order, every
 // mid_words words) and the ingress half from gout (grouped order, both written with coalesced
-// stores by the two classification launches) joined and stored at the caller index. One
-// 1024-thread block per grouping tile; each half of the tile's caller range is assembled in LDS
-// (128 KB of 16-B pairs, loads four deep per thread) and written with whole-line stores. Replaces
-// the ingress launch's 16-B stores scattered over the tile (C3: 0.84 ms of 13.5 per 64M packets).
+// stores by the classification launches) joined and stored at the caller index; with lbg, the
+// Service launch's LB results (grouped order) too. One 1024-thread block per grouping tile; each
+// half of the tile's caller range is assembled in LDS (128 KB of 16-B records, loads four deep per
+// thread) and written with whole-line stores. Replaces 16-B stores scattered over the tile (C3:
+// 0.84 ms of 13.5 per 64M packets).
 constexpr uint32_t kUnpermHalf = kGroupTile / 2;
-__global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint32_t* __restrict__ mid, uint32_t mid_words,
-                                                                  const uint2* __restrict__ gout,
-                                                                  const uint32_t* __restrict__ orig, uint64_t n,
-                                                                  uint4* __restrict__ out) {
-  __shared__ uint4 buf[kUnpermHalf];
-  const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
-  const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
+
+// One tile's 16-B records, grouped position k -> caller position orig[k], through buf.
+template <typename Load>
+__device__ __forceinline__ void permute_tile(uint4* buf, const uint32_t* __restrict__ orig, uint64_t base, uint32_t m,
+                                             Load load, uint4* __restrict__ dst) {
   constexpr int kU = 4;  // loads in flight per thread (all issued before any is used)
-  // (the staged pairs are held as word arrays: arrays of uint4 are not promoted to registers)
+  // (the staged records are held as word arrays: arrays of uint4 are not promoted to registers)
   for (uint32_t h = 0; h * kUnpermHalf < m; h++) {
     const uint32_t lo = h * kUnpermHalf, cnt = m - lo < kUnpermHalf ? m - lo : kUnpermHalf;
-    if (h) __syncthreads();  // the previous half's reads of buf are done
+    __syncthreads();  // the previous pass's reads of buf are done
     for (uint32_t k0 = threadIdx.x; k0 < m; k0 += kU * kGroupThreads) {
       uint32_t d[kU], x[kU], y[kU], z[kU], w[kU];
 #pragma unroll
@@ -481,9 +489,8 @@ __global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint32_t
       for (int u = 0; u < kU; u++) {
         x[u] = y[u] = z[u] = w[u] = 0;
         if (d[u] < cnt) {
-          const uint64_t k = base + k0 + u * kGroupThreads;
-          const uint2 e = *reinterpret_cast<const uint2*>(mid + k * mid_words), g = gout[k];
-          x[u] = e.x, y[u] = e.y, z[u] = g.x, w[u] = g.y;
+          const uint4 v = load(base + k0 + u * kGroupThreads);
+          x[u] = v.x, y[u] = v.y, z[u] = v.z, w[u] = v.w;
         }
       }
 #pragma unroll
@@ -503,17 +510,35 @@ __global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint32_t
       }
 #pragma unroll
       for (int u = 0; u < kU; u++)
-        if (j0 + u * kGroupThreads < cnt) out[base + lo + j0 + u * kGroupThreads] = make_uint4(x[u], y[u], z[u], w[u]);
+        if (j0 + u * kGroupThreads < cnt) dst[base + lo + j0 + u * kGroupThreads] = make_uint4(x[u], y[u], z[u], w[u]);
     }
   }
 }
 
+__global__ __launch_bounds__(kGroupThreads) void unpermute_kernel(const uint32_t* __restrict__ mid, uint32_t mid_words,
+                                                                  const uint2* __restrict__ gout,
+                                                                  const uint32_t* __restrict__ orig, uint64_t n,
+                                                                  uint4* __restrict__ out, const uint4* __restrict__ lbg,
+                                                                  uint4* __restrict__ lb_out) {
+  __shared__ uint4 buf[kUnpermHalf];
+  const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
+  const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
+  permute_tile(
+      buf, orig, base, m,
+      [&](uint64_t k) {
+        const uint2 e = *reinterpret_cast<const uint2*>(mid + k * mid_words), g = gout[k];
+        return make_uint4(e.x, e.y, g.x, g.y);
+      },
+      out);
+  if (lbg) permute_tile(buf, orig, base, m, [&](uint64_t k) { return lbg[k]; }, lb_out);
+}
+
 static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* gout, const uint32_t* orig, uint64_t n,
-                             uint4* out, hipStream_t stream, LaunchMarks* marks) {
+                             uint4* out, const uint4* lbg, uint4* lb_out, hipStream_t stream, LaunchMarks* marks) {
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
   launch_mark(marks, kLaunchUnpermute, stream);
   hipLaunchKernelGGL(unpermute_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream,
-                     reinterpret_cast<const uint32_t*>(mid), mid_words, gout, orig, n, out);
+                     reinterpret_cast<const uint32_t*>(mid), mid_words, gout, orig, n, out, lbg, lb_out);
 }
 
 template <bool kDelta, bool kSvc>
@@ -525,7 +550,7 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
   if (kSvc) {
     launch_mark(marks, kLaunchBoth, stream);
     hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid, xo, nullptr);
+                       lb_out, counters, count, orig, mid, xo, gout);
     return;
   }
   const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
@@ -625,18 +650,20 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
 constexpr uint64_t kMaxPackets = (1ull << 32) - uint64_t(kSortBlock);
 static_assert(kMaxPackets == GPC_MAX_BATCH, "gpc.h GPC_MAX_BATCH mirrors the launch limit");
 
-uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6) {
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6, bool lb) {
   uint64_t per = 4 /*orig*/ + (v6 ? 16 : 8) /*mid*/ + 2 + 2 + 1 + 4;  // + sport dport proto out_port
   per += v6 ? 32 + (pk.ct_src6 ? 16 : 0) + (pk.ct_dst6 ? 16 : 0) : 8 + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0);
   per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) +
          (pk.ct_state ? 1 : 0) + (pk.dest ? 1 : 0) + (pk.len ? 2 : 0) + (pk.ct_mark ? 1 : 0);
   per += 8;  // gout: the ingress halves of the verdict pairs in grouped order (GroupArgs.unpermute)
-  return per * n + 25 * 256;  // every region 256-B aligned
+  if (lb) per += 16;  // lbg: the Service launch's LB results in grouped order
+  return per * n + 26 * 256;  // every region 256-B aligned
 }
 
 // Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
 static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group,
-                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint2** gout, LaunchMarks* marks) {
+                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint2** gout, uint4** lbg,
+                        LaunchMarks* marks) {
   if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120 || (group.key != GPC_GROUP_KEY_ADDR && group.key != GPC_GROUP_KEY_SCAN)) return -GPC_EINVAL;
   uint8_t* q = group.scratch;
   auto take = [&](uint64_t bytes) {
@@ -648,6 +675,7 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
   *mid = take((v6 ? 16 : 8) * n);
   *orig = reinterpret_cast<uint32_t*>(take(4 * n));
   *gout = reinterpret_cast<uint2*>(take(8 * n));
+  if (lbg) *lbg = group.lb ? reinterpret_cast<uint4*>(take(16 * n)) : nullptr;
   if (v6) {
     g->src6 = take(16 * n);
     g->dst6 = take(16 * n);
@@ -675,7 +703,10 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
   gpc_pkt_soa in = pk;
   if (v6) in.src = in.dst = in.ct_src = in.ct_dst = nullptr;
   else in.src6 = in.dst6 = in.ct_src6 = in.ct_dst6 = nullptr;
-  if (!group.unpermute) *gout = nullptr;
+  if (!group.unpermute) {
+    *gout = nullptr;
+    if (lbg) *lbg = nullptr;
+  }
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
   launch_mark(marks, kLaunchGroup, stream);
   hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, ep, in, n, group.key,
@@ -695,7 +726,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   uint32_t xo = 0;
   uint2* gout = nullptr;
   if (group) {
-    if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid, &gout, marks)) return rc;
+    if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid, &gout, nullptr, marks)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
@@ -706,7 +737,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
   launch_mark(marks, kLaunchIngress, stream);
   hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
                      reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, gout);
-  if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), stream, marks);
+  if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), nullptr, nullptr, stream, marks);
   launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
@@ -722,20 +753,24 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   void* mid = nullptr;
   uint32_t xo = 0;
   uint2* gout = nullptr;
+  uint4* lbg = nullptr;  // grouped Service batch with the un-permute: LB results in grouped order
   if (group) {
-    if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid, &gout, marks)) return rc;
+    if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid, &gout, &lbg, marks)) return rc;
     xo = group->xcd_order;
     p = &g;
   }
   EpochArgs e = ep;
   if (group && group->key == GPC_GROUP_KEY_SCAN) e.sort_table[0] = e.sort_table[1] = 0;  // lanes already grouped by scan length
   const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
-  if (svc) gout = nullptr;  // one launch, verdicts and LB results stored at the caller index
-  if (delta && svc) launch<true, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  // with Services one launch does both stages; grouped, it stores both verdict halves (and the LB
+  // results) in grouped order for the un-permute, like the two launches without Services
+  if (svc && lb_out && gout && !lbg) return -GPC_EINVAL;  // the caller sized the scratch without lb
+  uint4* const lbk = lbg ? lbg : lb_out;
+  if (delta && svc) launch<true, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, stream, marks);
   else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
-  else if (svc) launch<false, true>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  else if (svc) launch<false, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, stream, marks);
   else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
-  if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), stream, marks);
+  if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), svc ? lbg : nullptr, lb_out, stream, marks);
   launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }

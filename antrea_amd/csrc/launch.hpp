@@ -30,7 +30,7 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
                           uint64_t n_words, hipStream_t stream);
 // Packet grouping of a batch (classify.hip group_tiles_kernel): the batch is classified in the
 // order of an 8-bit key (scan lengths or address bits) within every tile of 16384 packets, from a grouped copy in
-// `scratch` (group_scratch_bytes(pk, n) bytes of device memory, live until the launches have run:
+// `scratch` (group_scratch_bytes(pk, n, v6, lb) bytes of device memory, live until the launches have run:
 // stream-ordered).
 struct GroupArgs {
   uint8_t* scratch;
@@ -40,8 +40,9 @@ struct GroupArgs {
   uint32_t xcd_order;  // block order (classify.hip logical_block): 1 = the blocks of one tile run on one XCD
   int32_t v6_bit;      // IPv6 batches: key = 8 bits of ipv6_src from this bit (0 = most significant)
   uint32_t unpermute;  // 1: the ingress launch stores in grouped order, unpermute_kernel restores caller order
+  uint32_t lb;         // 1: a Service batch with lb_out: its LB results are un-permuted too (scratch for them)
 };
-uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6);
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6, bool lb);
 // Launch timing (gpc_set_launch_timing): an event is recorded on the launch stream before every
 // kernel of one gpc_classify* call and after the last, named by the kernel that follows it.
 struct LaunchMarks {

@@ -125,7 +125,8 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
            "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
            "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay",
-           "gpc_set_launch_timing", "gpc_launch_times"]
+           "gpc_set_launch_timing", "gpc_launch_times", "gpc_create_multi", "gpc_n_devices", "gpc_classify_on",
+           "gpc_classify6_on", "gpc_classify_host_on", "gpc_counters_on"]
 
 _lib = None
 
@@ -139,6 +140,13 @@ def load(path: str = LIB_PATH):
     lib = C.CDLL(path)
     vp, i32, sz = C.c_void_p, C.c_int32, C.c_size_t
     lib.gpc_create.argtypes = [C.POINTER(gpc_config), C.POINTER(vp)]
+    lib.gpc_create_multi.argtypes = [C.POINTER(gpc_config), C.POINTER(i32), sz, C.POINTER(vp)]
+    lib.gpc_n_devices.argtypes = [vp]
+    lib.gpc_classify_on.argtypes = [vp, C.c_uint32, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32, vp]
+    lib.gpc_classify6_on.argtypes = [vp, C.c_uint32, C.POINTER(gpc_pkt_soa), sz, vp, i32, vp]
+    lib.gpc_classify_host_on.argtypes = [vp, C.c_uint32, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32]
+    lib.gpc_counters_on.argtypes = [vp, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
+                                    C.POINTER(sz)]
     lib.gpc_destroy.argtypes = [vp]
     lib.gpc_destroy.restype = None
     lib.gpc_initialize.argtypes = [vp]
@@ -351,11 +359,13 @@ def pkt_soa_device(cols: Dict[str, "object"]):
 
 
 class Classifier:
-    """One gpc context (one GPU)."""
+    """One gpc context: one control plane over one GPU (`device`) or several (`devices`, a list of
+    HIP ordinals: gpc_create_multi; every commit is published on each of them, the `slot` argument
+    of the data-path calls picks one, metrics sum over all)."""
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
                  cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True, group_packets=0,
-                 group_key=0):
+                 group_key=0, devices=None):
         self.lib = load()
         cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
                          enable_antrea_policy=int(enable_antrea_policy),
@@ -364,8 +374,18 @@ class Classifier:
                          external_node=int(not k8s_node), group_packets=int(group_packets),
                          group_key=int(group_key))
         h = C.c_void_p()
-        _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
+        if devices is None:
+            _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
+        else:
+            devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            _check(self.lib.gpc_create_multi(C.byref(cfg), devs, len(devices), C.byref(h)), "gpc_create_multi")
         self.h = h
+
+    @property
+    def n_devices(self) -> int:
+        n = self.lib.gpc_n_devices(self.h)
+        _check(min(n, 0), "gpc_n_devices")
+        return n
 
     def close(self):
         if self.h:
@@ -536,12 +556,12 @@ class Classifier:
         """Publish with a full image rebuild (empties the overlay)."""
         _check(self.lib.gpc_compact(self.h), "gpc_compact")
 
-    def classify_host(self, cols: Dict[str, np.ndarray], count=False, lb=False):
+    def classify_host(self, cols: Dict[str, np.ndarray], count=False, lb=False, slot=0):
         """Verdicts (n, 2); with lb=True also the Service stage results (n,) of LB_DTYPE."""
         soa, keep, n = pkt_soa_host(cols)
         out = np.zeros(2 * n, dtype=VERDICT_DTYPE)
         lbo = np.zeros(n, dtype=LB_DTYPE) if lb else None
-        _check(self.lib.gpc_classify_host_lb(self.h, C.byref(soa), n, out.ctypes.data,
+        _check(self.lib.gpc_classify_host_on(self.h, int(slot), C.byref(soa), n, out.ctypes.data,
                                              lbo.ctypes.data if lb else None, int(count)), "gpc_classify_host")
         return (out.reshape(n, 2), lbo) if lb else out.reshape(n, 2)
 
@@ -552,8 +572,9 @@ class Classifier:
         _check(self.lib.gpc_classify6_host(self.h, C.byref(soa), n, out.ctypes.data, int(count)), "gpc_classify6_host")
         return out.reshape(n, 2)
 
-    def classify6_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0):
-        _check(self.lib.gpc_classify6(self.h, C.byref(soa), n, out_ptr, int(count), stream or None), "gpc_classify6")
+    def classify6_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, slot=0):
+        _check(self.lib.gpc_classify6_on(self.h, int(slot), C.byref(soa), n, out_ptr, int(count), stream or None),
+               "gpc_classify6")
 
     def debug_image6(self):
         """(blob pointer, n_words, hdr pointer) of the committed IPv6 image (None when absent)."""
@@ -564,9 +585,10 @@ class Classifier:
         _check(self.lib.gpc_debug_image6(self.h, C.byref(b), C.byref(n), C.byref(h), C.byref(hb)), "gpc_debug_image6")
         return (C.cast(b, C.c_void_p).value if n.value else None), n.value, h.value
 
-    def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, lb_ptr: int = 0):
-        _check(self.lib.gpc_classify_lb(self.h, C.byref(soa), n, out_ptr, lb_ptr or None, int(count), stream or None),
-               "gpc_classify")
+    def classify_device(self, soa: gpc_pkt_soa, n: int, out_ptr: int, count=False, stream: int = 0, lb_ptr: int = 0,
+                        slot=0):
+        _check(self.lib.gpc_classify_on(self.h, int(slot), C.byref(soa), n, out_ptr, lb_ptr or None, int(count),
+                                        stream or None), "gpc_classify")
 
     def trace(self, pkt: Dict[str, int]):
         """gpc_trace of one packet (dict of column values): (verdicts (2,), [step dicts], lb result)."""
@@ -600,11 +622,11 @@ class Classifier:
                                          "mean_ms": arr[i].total_ms / max(1, arr[i].launches),
                                          "dropped": arr[i].dropped} for i in range(n.value)}
 
-    def counters(self):
+    def counters(self, slot=0):
         p = C.POINTER(C.c_uint64)()
         s = C.POINTER(C.c_uint32)()
         n = C.c_size_t()
-        _check(self.lib.gpc_counters(self.h, C.byref(p), C.byref(s), C.byref(n)), "gpc_counters")
+        _check(self.lib.gpc_counters_on(self.h, int(slot), C.byref(p), C.byref(s), C.byref(n)), "gpc_counters")
         slots = [s[i] for i in range(n.value)]
         return C.cast(p, C.c_void_p).value, slots
 

@@ -71,40 +71,80 @@ def _lbar(wl, clf, n=20000, family=4):
         return None
 
 
-def _churn_loop(clf, wl, rate, max_batch, stop, rec, seed):
-    """Control-plane thread of C5. Address ops (alternating add / delete of /32 peers on random
-    rules) become due at `rate` per second; each pass applies every op due so far (at most
-    `max_batch`) and publishes them with one gpc_commit. Per op, the update latency is the time
-    from the op being due to the commit that made it visible returning; rec gets
-    (ops, commit_seconds, [latencies]) per commit."""
+class _ChurnOps:
+    """The C5 address-op stream: alternating add / delete of /32 src peers on random rules, drawn
+    from one seeded generator. Every rank uses the same seed, so all ranks apply one op stream
+    (they replicate one policy); only how the ops are batched into commits is rank-local."""
+
+    def __init__(self, clf, wl, seed):
+        import numpy as np
+        self.clf = clf
+        self.rng = np.random.default_rng(seed)
+        self.rules = [r for r in wl.rules if r.get("from")]
+        self.added = []
+        self.issued = 0
+
+    def apply(self, k):
+        rng, clf = self.rng, self.clf
+        for _ in range(k):
+            if self.added and rng.random() < 0.5:
+                rid, a, prio = self.added.pop(int(rng.integers(len(self.added))))
+                clf.delete_policy_rule_address(rid, "src", [a], prio)
+            else:
+                r = self.rules[int(rng.integers(len(self.rules)))]
+                v = int(rng.integers(0, 1 << 32))
+                a = "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+                clf.add_policy_rule_address(r["flow_id"], "src", [a], r.get("priority"))
+                self.added.append((r["flow_id"], a, r.get("priority")))
+        self.issued += k
+
+
+def _churn_loop(ops, rate, max_batch, stop, rec):
+    """Control-plane thread of C5. Address ops (_ChurnOps) become due at `rate` per second; each
+    pass applies every op due so far (at most `max_batch`) and publishes them with one gpc_commit.
+    Per op, the update latency is the time from the op being due to the commit that made it
+    visible returning; rec gets (ops, commit_seconds, [latencies]) per commit."""
     import numpy as np
-    rng = np.random.default_rng(seed)
-    rules = [r for r in wl.rules if r.get("from")]
-    added = []
     t0 = time.perf_counter()
-    issued = 0
+    base = ops.issued
     while not stop.is_set():
-        due = int((time.perf_counter() - t0) * rate) - issued
+        due = int((time.perf_counter() - t0) * rate) - (ops.issued - base)
         if due <= 0:
             time.sleep(0.0002)
             continue
         due = min(due, max_batch)
-        for _ in range(due):
-            if added and rng.random() < 0.5:
-                rid, a, prio = added.pop(int(rng.integers(len(added))))
-                clf.delete_policy_rule_address(rid, "src", [a], prio)
-            else:
-                r = rules[int(rng.integers(len(rules)))]
-                v = int(rng.integers(0, 1 << 32))
-                a = "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
-                clf.add_policy_rule_address(r["flow_id"], "src", [a], r.get("priority"))
-                added.append((r["flow_id"], a, r.get("priority")))
+        first = ops.issued - base
+        ops.apply(due)
         tc = time.perf_counter()
-        clf.commit()
+        ops.clf.commit()
         done = time.perf_counter()
-        due_t = t0 + (issued + np.arange(due)) / rate
+        due_t = t0 + (first + np.arange(due)) / rate
         rec.append((due, done - tc, done - due_t))
-        issued += due
+
+
+def _churn_converge(ops, wl, dev, world):
+    """After the timed region of C5 at N>1: every rank catches up to the longest op prefix any
+    rank applied, commits, and the ranks compare a digest of their realized flows and of their
+    device verdicts on one shared packet sample -- the replicated policy is the same everywhere."""
+    import hashlib
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from antrea_amd import workload
+    t = torch.tensor([ops.issued], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ops.apply(int(t.item()) - ops.issued)
+    ops.clf.commit()
+    cols = workload.gen_packets(wl, 1 << 16, seed=4242)
+    v = ops.clf.classify_host(cols)
+    h = hashlib.sha256("\n".join(ops.clf.dump_flows()).encode())
+    h.update(np.ascontiguousarray(v).tobytes())
+    mine = torch.tensor(np.frombuffer(h.digest()[:8], np.int64).copy(), device=dev)
+    lo, hi = mine.clone(), mine.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return {"ops_applied": int(t.item()), "ranks_identical": bool(lo.item() == hi.item()),
+            "digest": h.hexdigest()[:16]}
 
 
 def _pmc_pass(counters, args):
@@ -364,8 +404,9 @@ def main():
         import threading
         sys.setswitchinterval(2e-4)  # the control thread must not wait 5 ms for the GIL behind launches
         stop = threading.Event()
-        th = threading.Thread(target=_churn_loop, args=(clf, wl, args.churn_rate, args.max_batch, stop, lat,
-                                                        1234 + rank), daemon=True)
+        churn_ops = _ChurnOps(clf, wl, seed=1234)  # the same op stream on every rank
+        th = threading.Thread(target=_churn_loop, args=(churn_ops, args.churn_rate, args.max_batch, stop, lat),
+                              daemon=True)
         th.start()
         while len(lat) < 5:  # control loop running before the timed region
             time.sleep(0.01)
@@ -402,6 +443,8 @@ def main():
                   "overlay_rules_end": st["n_overlay_rules"], "tombstones_end": st["n_tombstones"],
                   "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"],
                   "background_builds": st["n_background_builds"]}
+        if world > 1:
+            update["ranks"] = _churn_converge(churn_ops, wl, dev, world)
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     launches = clf.launch_times()
     clf.set_launch_timing(0)

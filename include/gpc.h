@@ -27,7 +27,9 @@
 extern "C" {
 #endif
 
-#define GPC_ABI_VERSION 3
+#define GPC_ABI_VERSION 4
+/* device slots of one context (gpc_create_multi) */
+#define GPC_MAX_DEVICES 16
 
 /* ---------------------------------------------------------------------------- error codes */
 #define GPC_OK 0
@@ -314,6 +316,14 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
 
 /* ---------------------------------------------------------------------------- lifecycle */
 int gpc_create(const gpc_config* cfg, gpc_ctx** out);
+/* One control plane over several devices (MI355X: one agent process driving the GPUs of a node).
+ * The compiler, host image and journal exist once; every gpc_commit uploads the new epoch to each
+ * device in devices[0..n) and publishes it on all of them together (a launch on any slot sees the
+ * same epoch number). Slot k is devices[k] (a device may repeat). cfg->device is ignored.
+ * gpc_create(cfg) == gpc_create_multi(cfg, &cfg->device, 1). n in [1, GPC_MAX_DEVICES]. */
+int gpc_create_multi(const gpc_config* cfg, const int32_t* devices, size_t n, gpc_ctx** out);
+/* Device slots of the context. */
+int gpc_n_devices(gpc_ctx* ctx);
 void gpc_destroy(gpc_ctx* ctx);
 /* Client.Initialize NP part: skipPolicyRuleCheckFlows (network_policy.go:2144-2211). */
 int gpc_initialize(gpc_ctx* ctx);
@@ -429,6 +439,14 @@ int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pkt, gpc_verdict* out, gpc_lb_res
  * image in full (no delta epochs, no AntreaProxy stage for IPv6). Same verdict / counter layout.
  * -GPC_EINVAL if the IPv6 prefixes of the rule set need more than 32 code bits (core.hpp). */
 int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
+/* The data path on device slot `slot` of a gpc_create_multi context: pkts / out / lb_out live on
+ * that slot's device and `stream` belongs to it (NULL: its null stream). gpc_classify* == slot 0. */
+int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out,
+                    gpc_lb_result* lb_out, int32_t count, void* stream);
+int gpc_classify6_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count,
+                     void* stream);
+int gpc_classify_host_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out,
+                         gpc_lb_result* lb_out, int32_t count);
 int gpc_classify6_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
 /* Same with HOST pointers (copies in and out; synchronous). */
 int gpc_classify_host(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count);
@@ -441,6 +459,9 @@ int gpc_classify_host_lb(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_ve
  * striped replicas of the array (few rules: many same-address atomics); this call folds them into
  * the returned buffer (synchronizes the device), so call it again to see later classifications. */
 int gpc_counters(gpc_ctx* ctx, uint64_t** dev_counters, const uint32_t** slot_conj, size_t* n_slots);
+/* The counters of device slot `slot` alone (gpc_counters == slot 0). gpc_metrics sums every slot;
+ * gpc_reset_counters zeroes every slot. */
+int gpc_counters_on(gpc_ctx* ctx, uint32_t slot, uint64_t** dev_counters, const uint32_t** slot_conj, size_t* n_slots);
 int gpc_reset_counters(gpc_ctx* ctx);
 
 /* ---------------------------------------------------------------------------- introspection */

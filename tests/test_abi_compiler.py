@@ -28,7 +28,7 @@ def test_exports_every_header_symbol():
     exported = set(re.findall(r"\bT (gpc_\w+)", syms))
     assert declared <= exported, declared - exported
     lib = gpc.load()
-    assert lib.gpc_abi_version() == 3  # 3: ct_mark column, DNS conjunction trio, flow keys (2: IPv6 columns)
+    assert lib.gpc_abi_version() == 4  # 4: multi-device contexts (3: ct_mark column, DNS trio, flow keys; 2: IPv6)
 
 
 @pytest.mark.parametrize("case", GOLD["cases"], ids=[c["name"] for c in GOLD["cases"]])
@@ -80,3 +80,29 @@ def test_batch_limit_checked_before_any_device_work():
     for n in ((1 << 32) - 255, 1 << 40):
         assert c.lib.gpc_classify(c.h, C.byref(soa), C.c_size_t(n), C.addressof(dummy), 0, None) == -gpc.GPC_EINVAL
         assert c.lib.gpc_classify6(c.h, C.byref(soa), C.c_size_t(n), C.addressof(dummy), 0, None) == -gpc.GPC_EINVAL
+
+
+def test_create_multi_arguments():
+    """gpc_create_multi: 1..GPC_MAX_DEVICES slots of non-negative ordinals (no device is touched
+    before the first commit, so this runs here); out-of-range slots are -GPC_EINVAL before any
+    device work."""
+    import ctypes as C
+    hdr = open(gpc.os.path.join(gpc.os.path.dirname(gpc.HERE), "include", "gpc.h")).read()
+    assert re.search(r"#define GPC_MAX_DEVICES 16\b", hdr)
+    lib = gpc.load()
+    cfg = gpc.gpc_config(ipv4_enabled=1, enable_antrea_policy=1, compact_after=-1)
+    h = C.c_void_p()
+    for devs in ([], [0] * 17, [0, -1]):
+        arr = (C.c_int32 * max(1, len(devs)))(*devs)
+        assert lib.gpc_create_multi(C.byref(cfg), arr, len(devs), C.byref(h)) == -gpc.GPC_EINVAL, devs
+    c = gpc.Classifier(devices=[0, 1, 0])
+    assert c.n_devices == 3
+    soa = gpc.gpc_pkt_soa()
+    dummy = (C.c_uint8 * 64)()
+    assert lib.gpc_classify_on(c.h, 3, C.byref(soa), 1, C.addressof(dummy), None, 0, None) == -gpc.GPC_EINVAL
+    assert lib.gpc_classify6_on(c.h, 7, C.byref(soa), 1, C.addressof(dummy), 0, None) == -gpc.GPC_EINVAL
+    p = C.POINTER(C.c_uint64)()
+    s = C.POINTER(C.c_uint32)()
+    n = C.c_size_t()
+    assert lib.gpc_counters_on(c.h, 3, C.byref(p), C.byref(s), C.byref(n)) == -gpc.GPC_EINVAL
+    assert gpc.Classifier().n_devices == 1

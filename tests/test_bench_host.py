@@ -25,12 +25,38 @@ class _Stub:
 def test_churn_loop_paces_ops_and_records_latency():
     wl = workload.config1()
     stub, rec, stop = _Stub(), [], threading.Event()
-    th = threading.Thread(target=bench._churn_loop, args=(stub, wl, 5000.0, 2000, stop, rec, 1))
+    ops = bench._ChurnOps(stub, wl, seed=1)
+    th = threading.Thread(target=bench._churn_loop, args=(ops, 5000.0, 2000, stop, rec))
     th.start()
     time.sleep(0.5)
     stop.set()
     th.join()
-    ops = sum(r[0] for r in rec)
-    assert ops == stub.ops and len(rec) == stub.commits
+    n = sum(r[0] for r in rec)
+    assert n == stub.ops == ops.issued and len(rec) == stub.commits
+    ops = n
     assert 1500 <= ops <= 3500  # ~5000 ops/s for 0.5 s
     assert all(len(r[2]) == r[0] and (r[2] >= 0).all() for r in rec)
+
+
+def test_churn_ops_same_seed_same_stream():
+    """C5 at N>1: every rank draws the same op sequence, whatever its batching."""
+    wl = workload.config1()
+
+    class Rec(_Stub):
+        def __init__(self):
+            super().__init__()
+            self.seq = []
+
+        def add_policy_rule_address(self, *a):
+            self.seq.append(("add",) + tuple(map(str, a)))
+
+        def delete_policy_rule_address(self, *a):
+            self.seq.append(("del",) + tuple(map(str, a)))
+
+    a, b = Rec(), Rec()
+    oa, ob = bench._ChurnOps(a, wl, seed=1234), bench._ChurnOps(b, wl, seed=1234)
+    for _ in range(50):
+        oa.apply(7)
+    for _ in range(7):
+        ob.apply(50)
+    assert a.seq == b.seq[:350] and len(a.seq) == 350
