@@ -30,7 +30,7 @@ for s in $STEPS; do
   case $s in
     tests)
       step tests
-      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread \
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --durations=30 --timeout 400 --timeout-method thread \
         > "$O/gpu_tests.log" 2>&1; rc=$?
       tail -5 "$O/gpu_tests.log"; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
