@@ -104,7 +104,9 @@ struct DevEpoch {
   std::shared_ptr<DevImage> pool;       // journal pool of that base (d_hdr unused; append-only)
   uint32_t jhdr = 0;                    // this epoch's JournalHdr in the pool (0: base only)
   std::shared_ptr<DevImage> svc;        // Service image (d_hdr unused), shared until Services change
-  std::shared_ptr<DevImage> v6;         // IPv6 image (ipv6_enabled), shared until rules change
+  std::shared_ptr<DevImage> v6;         // IPv6 base image (ipv6_enabled), shared by its delta epochs
+  std::shared_ptr<DevImage> v6_pool;    // journal pool of that base (append-only)
+  uint32_t v6_jhdr = 0;                 // this epoch's IPv6 JournalHdr (0: base only)
   uint32_t v6_lpm = 0;                  // its ImageHdr.v6_lpm
   int32_t v6_bit = 0;                   // grouping key of IPv6 batches (v6_group_bit)
   uint64_t epoch = 0;
@@ -183,8 +185,10 @@ struct gpc_ctx {
   uint64_t svc_gen = ~0ull;              // FeatureService generation the image was built from
   SlotMap slots;
   HostImage last;    // base image of the current epoch: shadow state for re-upload + debug export
-  HostImage last6;   // IPv6 image (ipv6_enabled): rebuilt in full by every commit that changes rules
+  HostImage last6;   // IPv6 base image (ipv6_enabled)
   Journal journal;   // delta epochs over `last` (host mirror of the device pools)
+  Journal journal6;  // IPv6 delta epochs over `last6`
+  uint64_t n_full6 = 0, n_delta6 = 0;
   std::vector<DevState> dev;             // device slots (gpc_create: one, cfg.device)
   uint64_t cur_epoch = 0;                // epoch every slot currently publishes (0: nothing committed)
   uint32_t group_key = GPC_GROUP_KEY_AUTO;                            // gpc_group_key (gpc_create)
@@ -206,8 +210,11 @@ struct gpc_ctx {
   bool comp_pending = false;             // a background compaction was requested, not installed yet
   std::vector<std::pair<uint64_t, FeatureNP::Dirty>> dirty_hist;  // per commit since the request
   Compactor comp;
+  void* stage6 = nullptr;                // pinned staging buffer of IPv6 journal uploads
+  size_t stage6_bytes = 0;
   gpc_ctx(const gpc_config& c, const std::vector<int>& devices) : cfg(c), np(c), svc(c), dev(devices.size()) {
     for (size_t k = 0; k < devices.size(); k++) dev[k].device = devices[k];
+    journal6.set_family(6);
   }
 };
 
@@ -577,6 +584,7 @@ void gpc_destroy(gpc_ctx* ctx) {
     }
   }
   if (ctx->stage) (void)hipHostFree(ctx->stage);
+  if (ctx->stage6) (void)hipHostFree(ctx->stage6);
   delete ctx;
 }
 
@@ -920,6 +928,14 @@ int gpc_replay(gpc_ctx* ctx) {
       rc = upload_image(ctx->last6, D.device, us, &ne[k].v6);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
       ne[k].v6_bit = v6_group_bit(ctx->last6);
+      const Journal& j6 = ctx->journal6;
+      if (!rc && j6.active()) {
+        rc = alloc_pool(D.device, us, &ne[k].v6_pool);
+        if (!rc && hip_ok(hipMemcpyAsync(ne[k].v6_pool->d_blob, j6.pool.data(), j6.pool.size() * 4,
+                                         hipMemcpyHostToDevice, us)))
+          rc = -GPC_EDEV;
+        ne[k].v6_jhdr = j6.hdr_off;
+      }
     }
     if (!rc && !ctx->svc_blob.empty()) rc = upload_words(ctx->svc_blob, D.device, us, &ne[k].svc);
     if (!rc && (hip_ok(hipMalloc(&nc[k], cap * kCounterBytes * copies)) ||
@@ -936,6 +952,7 @@ int gpc_replay(gpc_ctx* ctx) {
     return rc;
   }
   if (jn.active()) jn.uploaded = jn.pool.size();
+  if (ctx->journal6.active()) ctx->journal6.uploaded = ctx->journal6.pool.size();
   const uint64_t epoch = ++ctx->epoch;
   std::lock_guard<std::mutex> d(ctx->data);
   for (size_t k = 0; k < ctx->dev.size(); k++) {
@@ -1141,8 +1158,8 @@ int gpc_classify6_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t 
   DevState& D = ctx->dev[slot];
   if (!D.cur.v6) return -GPC_EINVAL;  // IPv6 disabled or nothing committed yet
   if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
-  EpochArgs ep{D.cur.v6->d_hdr, D.cur.v6->d_blob, nullptr, 0u, nullptr, D.cur.v6_lpm, {0, 0},
-               uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1};
+  EpochArgs ep{D.cur.v6->d_hdr, D.cur.v6->d_blob, D.cur.v6_jhdr ? D.cur.v6_pool->d_blob : nullptr, D.cur.v6_jhdr,
+               nullptr, D.cur.v6_lpm, {0, 0}, uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
   GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, D.cur.v6_bit, ctx->group_unpermute};
   if (ctx->group_v6 && group_batch(ctx, n, D.cur.v6->bytes))
@@ -1320,6 +1337,10 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   out->n_full_builds = ctx->n_full;
   out->n_delta_builds = ctx->n_delta;
   out->n_background_builds = ctx->n_bg;
+  out->v6_full_builds = ctx->n_full6;
+  out->v6_delta_builds = ctx->n_delta6;
+  out->v6_overlay_rules = ctx->journal6.n_live;
+  out->v6_prefixes = ctx->last6.v6_prefixes;
   if (cur.base) {
     out->group_key = group_key(ctx);
     out->lane_sort = cur.base->sort_table[0] | uint32_t(cur.base->sort_table[1]) << 8;
@@ -1453,6 +1474,16 @@ int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uin
   return GPC_OK;
 }
 
+int gpc_debug_epoch6(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr) {
+  if (!ctx) return -GPC_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->ctl);
+  const bool has = ctx->journal6.active();
+  if (pool) *pool = has ? ctx->journal6.pool.data() : nullptr;
+  if (pool_words) *pool_words = has ? ctx->journal6.pool.size() : 0;
+  if (jhdr) *jhdr = has ? ctx->journal6.hdr_off : 0;
+  return GPC_OK;
+}
+
 }  // extern "C"
 
 // Builds the next epoch (full or delta) on the host, uploads it and publishes it atomically.
@@ -1549,22 +1580,47 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     }
     ctx->comp.cv.notify_one();
   }
-  const bool v6_changed = ctx->cfg.ipv6_enabled &&
-                          (full || installed || !dirty.conj.empty() || dirty.hard_tables || ctx->last6.blob.empty());
-  if (v6_changed) {  // an IPv6 rule set the image cannot take leaves IPv6 unpublished, not IPv4
-    HostImage img6;
-    int r6;
-    try {
-      r6 = build_image6(ctx->np, ctx->slots, &img6);
-    } catch (...) {
-      r6 = -GPC_ENOMEM;
+  // IPv6: a delta epoch over the IPv6 base (new prefixes interned in place, changed rules appended
+  // to journal6) when possible, else a full rebuild. v6_full: a new base; v6_changed: a new epoch.
+  bool v6_changed = false, v6_full = false;
+  const bool rules_changed = !dirty.conj.empty() || dirty.hard_tables || classifier_changed;
+  if (ctx->cfg.ipv6_enabled && (rules_changed || force_full || ctx->last6.blob.empty())) {
+    Journal& j6 = ctx->journal6;
+    v6_full = force_full || classifier_changed || ctx->np.foreign() || ctx->last6.blob.empty() || !ctx->last6.codes6 ||
+              j6.any_noact || j6.n_live > std::max(kDeltaMinRules, ctx->last6.conj_rid.size() / kDeltaFraction) ||
+              j6.pool.size() > kPoolWords * 7 / 8;
+    if (!v6_full) {
+      std::string err;
+      try {
+        if (extend_image6(ctx->np, dirty.conj, dirty.hard_tables, &ctx->last6, &j6) != GPC_OK) err = "prefix not internable";
+        else if (j6.apply(ctx->np, ctx->slots, dirty.conj, dirty.hard_tables, &err) != GPC_OK || j6.pool.size() > kPoolWords)
+          err = err.empty() ? "journal full" : err;
+      } catch (...) {
+        err = "out of memory";
+      }
+      v6_full = !err.empty();
+      if (v6_full && std::getenv("GPC_IMAGE_DEBUG")) std::fprintf(stderr, "IPv6 delta -> full build: %s\n", err.c_str());
     }
-    if (r6) {
-      std::string e = img6.error.empty() ? "IPv6 image build failed" : img6.error;
-      img6 = HostImage();
-      img6.error = e;
+    if (v6_full) {  // an IPv6 rule set the image cannot take leaves IPv6 unpublished, not IPv4
+      HostImage img6;
+      int r6;
+      try {
+        r6 = build_image6(ctx->np, ctx->slots, &img6);
+      } catch (...) {
+        r6 = -GPC_ENOMEM;
+      }
+      if (r6) {
+        std::string e = img6.error.empty() ? "IPv6 image build failed" : img6.error;
+        img6 = HostImage();
+        img6.error = e;
+      }
+      ctx->last6 = std::move(img6);
+      j6.reset(&ctx->last6);
+      ctx->n_full6++;
+    } else {
+      ctx->n_delta6++;
     }
-    ctx->last6 = std::move(img6);
+    v6_changed = true;
   }
   const bool svc_changed = ctx->svc.generation() != ctx->svc_gen;
   if (svc_changed) {
@@ -1640,6 +1696,27 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     std::memcpy(ctx->stage, jn.pool.data() + jn.uploaded, tail_bytes);
   }
   const uint32_t jhdr = jn.active() ? jn.hdr_off : 0;
+  // the IPv6 journal tail (delta epochs), staged the same way; a new pool on every slot when the
+  // IPv6 base is new or its journal starts (lockstep: every slot has the same IPv6 base)
+  Journal& j6 = ctx->journal6;
+  const bool j6_active = v6_changed && !v6_full && j6.active();
+  if (j6_active && !ctx->dev[0].cur.v6_pool) j6.uploaded = 0;
+  const size_t j6_from = j6.uploaded;
+  const bool tail6 = j6_active && j6.pool.size() > j6.uploaded;
+  size_t copy6_bytes = 0;
+  if (tail6) {
+    const size_t t6 = (j6.pool.size() - j6.uploaded) * 4;
+    copy6_bytes = std::min(std::max(t6, kMinUploadBytes), kPoolWords * 4 - j6.uploaded * 4);
+    if (ctx->stage6_bytes < copy6_bytes) {
+      if (ctx->stage6) (void)hipHostFree(ctx->stage6);
+      ctx->stage6 = nullptr;
+      ctx->stage6_bytes = 0;
+      const size_t cap = std::max(copy6_bytes, size_t(4) << 20);
+      if (hip_ok(hipHostMalloc(&ctx->stage6, cap, hipHostMallocPortable))) return fail(-GPC_EDEV);
+      ctx->stage6_bytes = cap;
+    }
+    std::memcpy(ctx->stage6, j6.pool.data() + j6.uploaded, t6);
+  }
   const uint64_t epoch = ctx->epoch + 1;
   const size_t need = ctx->slots.size() ? ctx->slots.size() : 1;
   for (size_t k = 0; k < nd; k++) {
@@ -1649,10 +1726,21 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (tail && hip_ok(hipMemcpyAsync(ne[k].pool->d_blob + jn.uploaded, ctx->stage, copy_bytes, hipMemcpyHostToDevice, us)))
       return fail(-GPC_EDEV);
     ne[k].jhdr = jhdr;
-    if (!v6_changed) {
+    if (!v6_full) {  // the IPv6 base stays; a delta extends its journal (new prefixes' LPM entries included)
       ne[k].v6 = D.cur.v6;
       ne[k].v6_lpm = D.cur.v6_lpm;
       ne[k].v6_bit = D.cur.v6_bit;
+      ne[k].v6_pool = D.cur.v6_pool;
+      ne[k].v6_jhdr = D.cur.v6_jhdr;
+      if (v6_changed && ne[k].v6) {
+        if (j6_active && !ne[k].v6_pool) {
+          if ((rc = alloc_pool(D.device, us, &ne[k].v6_pool))) return fail(rc);
+        }
+        if (tail6 && hip_ok(hipMemcpyAsync(ne[k].v6_pool->d_blob + j6_from, ctx->stage6, copy6_bytes,
+                                           hipMemcpyHostToDevice, us)))
+          return fail(-GPC_EDEV);
+        ne[k].v6_jhdr = j6_active ? ctx->journal6.hdr_off : 0u;
+      }
     } else if (!ctx->last6.blob.empty()) {
       if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
@@ -1677,6 +1765,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (hip_ok(hipSetDevice(ctx->dev[k].device)) || hip_ok(hipStreamSynchronize(ctx->dev[k].ustream)))
       return fail(-GPC_EDEV);
   if (tail) jn.uploaded = jn.pool.size();
+  if (tail6) j6.uploaded = j6.pool.size();
   ctx->epoch = epoch;
   std::vector<DevEpoch> old(nd);
   std::vector<unsigned long long*> old_counters(nd, nullptr);

@@ -48,16 +48,33 @@ __device__ __forceinline__ void v6_load(const uint8_t* col, uint64_t i, uint32_t
   a[2] = __builtin_bswap32(v.z);
   a[3] = __builtin_bswap32(v.w);
 }
+// kDelta: an IPv6 delta epoch; the journal header's overflow table (if any) is probed too.
+template <bool kDelta>
 __device__ __forceinline__ void v6_code_pair(const EpochArgs& ep, const uint8_t* c0, const uint8_t* c1, uint64_t i,
                                              uint32_t* code) {
   uint32_t a[2][4];
   v6_load(c0, i, a[0]);
   v6_load(c1, i, a[1]);
+  if (kDelta) {
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
+    if (jh->v6_ovf_off) {
+      v6_codes<2, true>(ep.blob, ep.v6_lpm, a, code, ep.pool + jh->v6_ovf_off, jh->v6_ovf_log2);
+      return;
+    }
+  }
   v6_codes<2>(ep.blob, ep.v6_lpm, a, code);
 }
+template <bool kDelta>
 __device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_t* col, uint64_t i) {
   uint32_t a[1][4], c;
   v6_load(col, i, a[0]);
+  if (kDelta) {
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
+    if (jh->v6_ovf_off) {
+      v6_codes<1, true>(ep.blob, ep.v6_lpm, a, &c, ep.pool + jh->v6_ovf_off, jh->v6_ovf_log2);
+      return c;
+    }
+  }
   v6_codes<1>(ep.blob, ep.v6_lpm, a, &c);
   return c;
 }
@@ -356,18 +373,18 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
       dst = code_d;
     } else {
       uint32_t sd[2];
-      v6_code_pair(ep, pk.src6, pk.dst6, i, sd);
+      v6_code_pair<kDelta>(ep, pk.src6, pk.dst6, i, sd);
       src = sd[0];
       dst = sd[1];
     }
     if (pk.ct_src6 && pk.ct_dst6) {
       uint32_t cd[2];
-      v6_code_pair(ep, pk.ct_src6, pk.ct_dst6, i, cd);
+      v6_code_pair<kDelta>(ep, pk.ct_src6, pk.ct_dst6, i, cd);
       ct_src = cd[0];
       ct_dst = cd[1];
     } else {
-      ct_src = pk.ct_src6 ? v6_code_at(ep, pk.ct_src6, i) : src;
-      ct_dst = pk.ct_dst6 ? v6_code_at(ep, pk.ct_dst6, i) : dst;
+      ct_src = pk.ct_src6 ? v6_code_at<kDelta>(ep, pk.ct_src6, i) : src;
+      ct_dst = pk.ct_dst6 ? v6_code_at<kDelta>(ep, pk.ct_dst6, i) : dst;
     }
   } else {
     src = pk.src[i];
@@ -731,12 +748,21 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
     p = &g;
   }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  uint4* const o = reinterpret_cast<uint4*>(out);
   launch_mark(marks, kLaunchEgress, stream);
-  hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, nullptr);
+  if (ep.pool)  // an IPv6 delta epoch: base + journal
+    hipLaunchKernelGGL((classify_kernel<true, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
+                       nullptr, counters, count, orig, mid, xo, nullptr);
+  else
+    hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
+                       nullptr, counters, count, orig, mid, xo, nullptr);
   launch_mark(marks, kLaunchIngress, stream);
-  hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n,
-                     reinterpret_cast<uint4*>(out), nullptr, counters, count, orig, mid, xo, gout);
+  if (ep.pool)
+    hipLaunchKernelGGL((classify_kernel<true, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
+                       nullptr, counters, count, orig, mid, xo, gout);
+  else
+    hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
+                       nullptr, counters, count, orig, mid, xo, gout);
   if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), nullptr, nullptr, stream, marks);
   launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;

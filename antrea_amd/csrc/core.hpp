@@ -297,10 +297,15 @@ GPC_HD uint64_t v6_hkey(const uint32_t* m, uint32_t len) {
 // code(a_k) for K addresses at once (a[k][0..3], [0] = most significant): the K binary searches run
 // in lock step (the step count is the same for every address up to one), so each step issues the
 // 2K bucket loads before any compare -- K independent dependency chains per lane instead of K in a row.
-template <int K>
-GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)[4], uint32_t* code) {
+// kOvf (IPv6 delta epochs): the journal's overflow table `ovf` (2^ovf_log2 buckets, the LPM entries
+// of prefixes interned since the base) is probed in the same step, its 2K loads issued with the
+// base's: no extra dependent round.
+template <int K, bool kOvf = false>
+GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)[4], uint32_t* code,
+                     const uint32_t* ovf = nullptr, uint32_t ovf_log2 = 0) {
   const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
   const uint32_t mask = (1u << L->hash_log2) - 1u;
+  const uint32_t omask = (1u << ovf_log2) - 1u;
   int lo[K], hi[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
@@ -314,7 +319,7 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
     for (int k = 0; k < K; k++) any |= lo[k] <= hi[k];
     if (!any) break;
     uint32_t len[K], m[K][4];
-    const uint32_t* b[K][2];
+    const uint32_t* b[K][kOvf ? 4 : 2];
 #pragma unroll
     for (int k = 0; k < K; k++) {  // finished addresses re-probe their last length (result unused)
       const int mid = lo[k] <= hi[k] ? (lo[k] + hi[k]) >> 1 : 0;
@@ -323,6 +328,10 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       const uint64_t hk = v6_hkey(m[k], len[k]);
       b[k][0] = blob + L->hash_off + size_t(hash_b1(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
       b[k][1] = blob + L->hash_off + size_t(hash_b2(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
+      if constexpr (kOvf) {
+        b[k][2] = ovf + size_t(hash_b1(hk, omask)) * (kV6SlotWords * kV6BucketSlots);
+        b[k][3] = ovf + size_t(hash_b2(hk, omask)) * (kV6SlotWords * kV6BucketSlots);
+      }
       if (lo[k] <= hi[k]) {
         GPC_TOUCH(b[k][0], 64);
         GPC_TOUCH(b[k][1], 64);
@@ -334,7 +343,7 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       const int mid = (lo[k] + hi[k]) >> 1;
       bool hit = false;
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
+      for (int c = 0; c < (kOvf ? 8 : 4); c++) {
         const uint32_t* w = b[k][c >> 1] + (c & 1) * kV6SlotWords;
         if (w[4] == (len[k] | kV6Valid) && w[0] == m[k][0] && w[1] == m[k][1] && w[2] == m[k][2] && w[3] == m[k][3]) {
           hit = true;
@@ -346,9 +355,11 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
     }
   }
 }
-GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a) {
+GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a, const uint32_t* ovf = nullptr,
+                        uint32_t ovf_log2 = 0) {
   uint32_t aa[1][4] = {{a[0], a[1], a[2], a[3]}}, c;
-  v6_codes<1>(blob, lpm_off, aa, &c);
+  if (ovf) v6_codes<1, true>(blob, lpm_off, aa, &c, ovf, ovf_log2);
+  else v6_codes<1>(blob, lpm_off, aa, &c);
   return c;
 }
 // 16 network-order bytes -> 4 host words, most significant first.
@@ -404,6 +415,9 @@ struct JournalHdr {
   uint32_t bdead_off;      // base tombstones: page table (0: none), see rule_dead
   uint32_t odead_off;      // journal tombstones: page table (0: none)
   uint32_t bloom_axes;     // as ImageHdr.bloom_axes, over every journal entry so far
+  // IPv6 journals: LPM entries of the prefixes interned since the base (image.cpp extend_image6),
+  // a hash laid out like V6Lpm's (2^v6_ovf_log2 buckets) probed next to the base's; 0: none
+  uint32_t v6_ovf_off, v6_ovf_log2;
   JournalTable t[6];
 };
 constexpr uint32_t kJEntWords = 8;

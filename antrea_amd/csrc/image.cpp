@@ -104,6 +104,8 @@ inline u128 v6_value(const IPAddr& a) {
 }
 inline u128 v6_prefix_mask(int len) { return len <= 0 ? u128(0) : len >= 128 ? ~u128(0) : ~((u128(1) << (128 - len)) - 1); }
 
+}  // namespace
+
 class V6Codes {
  public:
   struct Node {
@@ -113,9 +115,15 @@ class V6Codes {
     uint32_t code = 0;
     int clen = 0;
     std::vector<int> kids;
+    // Free code space for prefixes added after the build (add_leaf): the "none" leaf of the node
+    // (addresses in no child) is its code padded with zeros, at depth none_clen; every other code
+    // of that all-zero subtree, [code + 1, code + 2^(32 - none_clen)), is unused. -1: no room.
+    int none_clen = -1;
+    uint64_t next_free = 1;
   };
   std::vector<Node> nodes;  // nodes[0] = ::/0
   int max_clen = 0;
+  std::set<int> lens;       // distinct node lengths (root excluded)
 
   int build(const FeatureNP& np, std::string* err) {
     std::vector<std::pair<u128, int>> pf;
@@ -149,6 +157,7 @@ class V6Codes {
       nodes[st.back()].kids.push_back(id);
       st.push_back(id);
       index_[{p.first, p.second}] = id;
+      lens.insert(p.second);
     }
     // Codes. The children of a node (plus a "none of them" leaf unless they tile the node) get a
     // prefix-free code built like a minimax Huffman tree: merge the two leaves / subtrees needing
@@ -185,10 +194,55 @@ class V6Codes {
           K.clen = N.clen + depth;
           K.code = N.code | (depth ? path << (32 - K.clen) : 0u);
           max_clen = std::max(max_clen, K.clen);
+        } else {
+          nodes[n].none_clen = N.clen + depth;
         }
       }
     }
+    for (Node& N : nodes)
+      if (N.kids.empty()) N.none_clen = N.len < 128 ? N.clen : -1;  // a /128 has no sub-prefixes
     return GPC_OK;
+  }
+
+  // Interns a prefix that appeared after the build (a delta commit) without changing any existing
+  // code: it must be a leaf (no interned prefix below it) and gets an exact code from the free
+  // space of its deepest containing node. Every rule term of that node (a code prefix) and of its
+  // ancestors still covers it, so no other rule changes. Returns the node id, or -1 when the tree
+  // has to be rebuilt (not a leaf, no free code, or a prefix length the LPM does not search).
+  int add_leaf(u128 v, int len) {
+    if (len <= 0 || !lens.count(len)) return -1;
+    v &= v6_prefix_mask(len);
+    auto hit = index_.find({v, len});
+    if (hit != index_.end()) return hit->second;
+    const u128 last = len >= 128 ? v : v | ~v6_prefix_mask(len);
+    auto it = index_.upper_bound({v, len});
+    if (it != index_.end() && it->first.first <= last) return -1;  // an interned prefix lies below it
+    int P = 0;
+    for (auto l = lens.rbegin(); l != lens.rend() && !P; ++l) {
+      if (*l >= len) continue;
+      auto a = index_.find({v & v6_prefix_mask(*l), *l});
+      if (a != index_.end()) P = a->second;
+    }
+    Node& p = nodes[size_t(P)];
+    if (p.none_clen < 0 || p.none_clen >= 32 || p.next_free >= (uint64_t(1) << (32 - p.none_clen))) return -1;
+    Node k{v, len};
+    k.parent = P;
+    k.code = p.code + uint32_t(p.next_free++);
+    k.clen = 32;  // exact: nothing can be added below it without a rebuild
+    const int id = int(nodes.size());
+    nodes.push_back(k);
+    nodes[size_t(P)].kids.push_back(id);
+    index_[{v, len}] = id;
+    n_added++;
+    return id;
+  }
+  uint32_t n_added = 0;  // prefixes interned by add_leaf since the build
+  const char* why_not(u128 v, int len) const {  // the reason add_leaf refused (debug output)
+    if (!lens.count(len)) return "new prefix length";
+    const u128 last = len >= 128 ? v : v | ~v6_prefix_mask(len);
+    auto it = index_.upper_bound({v, len});
+    if (it != index_.end() && it->first.first <= last) return "an interned prefix lies below it";
+    return "no free code in its containing prefix";
   }
   static constexpr int kInternal = -1, kNone = -2;
   struct MergeNode {
@@ -239,16 +293,23 @@ class V6Codes {
     auto it = index_.find({v6_value(a) & v6_prefix_mask(len), len});
     if (it == index_.end()) return false;
     const Node& N = nodes[it->second];
-    // a leaf prefix (no prefix below it): every address in it has exactly the code N.code, so
-    // the term is an exact value (host addresses stay points: exact band, point hash)
-    *mask = N.kids.empty() ? 0xffffffffu : prefix_mask(N.clen);
+    // a /128 (no prefix can lie below it): every address in it has exactly the code N.code, so
+    // the term is an exact value (host addresses stay points: exact band, point hash); any other
+    // prefix is its code prefix, so a leaf added below it later (add_leaf) is still covered
+    *mask = (N.kids.empty() && N.len >= 128) || N.clen >= 32 ? 0xffffffffu : prefix_mask(N.clen);
     *val = N.code & *mask;
     return true;
+  }
+  int find(u128 v, int len) const {
+    auto it = index_.find({v & v6_prefix_mask(len), len});
+    return it == index_.end() ? -1 : it->second;
   }
 
  private:
   std::map<std::pair<u128, int>, int> index_;
 };
+
+namespace {
 
 // Flow match -> atom over the packet axes of a `fam` image (IPv6: addresses as V6Codes codes).
 // Returns 0 ok, 1 never matches a packet of that family, -1 unsupported.
@@ -989,11 +1050,57 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc)
   return emit(G, np, slots, out, alloc);
 }
 
+// A 2-choice hash of V6Lpm slots (core.hpp v6_codes) at most `load` full: 2^lg buckets of
+// kV6BucketSlots slots; cuckoo placement, a larger table when it does not converge.
+static bool v6_hash_build(const std::vector<std::array<uint32_t, 8>>& slots6, double load, std::vector<uint32_t>* tab,
+                          uint32_t* lg_out) {
+  const size_t nk = slots6.size();
+  const uint32_t S = kV6BucketSlots, W = kV6SlotWords;
+  uint32_t lg = 0;
+  while (double(S << lg) * load < double(nk + 1)) lg++;
+  for (int attempt = 0; attempt < 8; attempt++, lg++) {
+    const uint32_t nb = 1u << lg, mask = nb - 1;
+    tab->assign(size_t(nb) * S * W, 0u);
+    std::mt19937 rng(4321 + attempt);
+    bool ok = true;
+    for (size_t n = 0; n < slots6.size() && ok; n++) {
+      uint32_t cur[8];
+      std::memcpy(cur, slots6[n].data(), sizeof cur);
+      bool placed = false;
+      for (int kick = 0; kick < 1000 && !placed; kick++) {
+        const uint64_t hk = v6_hkey(cur, cur[4] & 0xffu);
+        const uint32_t bs[2] = {hash_b1(hk, mask), hash_b2(hk, mask)};
+        for (uint32_t b : bs) {
+          for (uint32_t i = 0; i < S && !placed; i++) {
+            uint32_t* sl = tab->data() + (size_t(b) * S + i) * W;
+            if (!(sl[4] & kV6Valid)) {
+              std::memcpy(sl, cur, sizeof cur);
+              placed = true;
+            }
+          }
+          if (placed) break;
+        }
+        if (!placed) {
+          uint32_t* sl = tab->data() + (size_t(bs[rng() & 1]) * S + rng() % S) * W;
+          for (uint32_t w = 0; w < W; w++) std::swap(cur[w], sl[w]);
+        }
+      }
+      ok = placed;
+    }
+    if (ok) {
+      *lg_out = lg;
+      return true;
+    }
+  }
+  return false;
+}
+
 // IPv6 image: the same build over the IPv6 half of the flows (addresses interned as codes), plus
 // the LPM table the kernel maps packet addresses through (appended to the blob, hdr.v6_lpm).
 int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc) {
   *out = HostImage();
-  V6Codes codes;
+  out->codes6 = std::make_shared<V6Codes>();
+  V6Codes& codes = *out->codes6;
   int rc = codes.build(np, &out->error);
   if (rc) return rc;
   Gather G;
@@ -1047,43 +1154,9 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     slots6.push_back({uint32_t(v >> 96), uint32_t(v >> 64), uint32_t(v >> 32), uint32_t(v), kv.first.second | kV6Valid,
                       kv.second, 0u, 0u});
   }
-  const size_t nk = slots6.size();
-  const uint32_t S = kV6BucketSlots, W = kV6SlotWords;
-  uint32_t lg = 0;
-  while (double(S << lg) * 0.7 < double(nk + 1)) lg++;
   std::vector<uint32_t> tab;
-  bool ok = false;
-  for (int attempt = 0; attempt < 8 && !ok; attempt++, lg++) {
-    const uint32_t nb = 1u << lg, mask = nb - 1;
-    tab.assign(size_t(nb) * S * W, 0u);
-    std::mt19937 rng(4321 + attempt);
-    ok = true;
-    for (size_t n = 0; n < slots6.size() && ok; n++) {
-      uint32_t cur[8];
-      std::memcpy(cur, slots6[n].data(), sizeof cur);
-      bool placed = false;
-      for (int kick = 0; kick < 1000 && !placed; kick++) {
-        const uint64_t hk = v6_hkey(cur, cur[4] & 0xffu);
-        const uint32_t bs[2] = {hash_b1(hk, mask), hash_b2(hk, mask)};
-        for (uint32_t b : bs) {
-          for (uint32_t i = 0; i < S && !placed; i++) {
-            uint32_t* sl = tab.data() + (size_t(b) * S + i) * W;
-            if (!(sl[4] & kV6Valid)) {
-              std::memcpy(sl, cur, sizeof cur);
-              placed = true;
-            }
-          }
-          if (placed) break;
-        }
-        if (!placed) {
-          uint32_t* sl = tab.data() + (size_t(bs[rng() & 1]) * S + rng() % S) * W;
-          for (uint32_t w = 0; w < W; w++) std::swap(cur[w], sl[w]);
-        }
-      }
-      ok = placed;
-    }
-  }
-  if (!ok) {
+  uint32_t lg = 0;
+  if (!v6_hash_build(slots6, 0.7, &tab, &lg)) {
     out->error = "IPv6 LPM table construction failed";
     return -GPC_ENOMEM;
   }
@@ -1091,7 +1164,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
   while (b.size() % 16) b.push_back(0u);
   const uint32_t lpm = uint32_t(b.size());
   V6Lpm L{};
-  L.hash_log2 = lg - 1;  // the loop advanced lg past the successful attempt
+  L.hash_log2 = lg;
   L.n_lens = uint32_t(lens.size());
   for (size_t i = 0; i < lens.size(); i++) L.lens[i] = lens[i];
   const size_t lw = (sizeof(V6Lpm) / 4 + 15) / 16 * 16;
@@ -1103,6 +1176,100 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
   out->bytes_hash += 4ull * tab.size();
   out->v6_code_bits = uint32_t(codes.max_clen);
   out->v6_prefixes = uint32_t(codes.nodes.size() - 1);
+  return GPC_OK;
+}
+
+int extend_image6(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t hard_tables, HostImage* img, Journal* j6) {
+  if (!img->codes6 || !img->hdr.v6_lpm) return -GPC_EINVAL;
+  V6Codes& codes = *img->codes6;
+  const std::vector<uint32_t>& b = img->blob;
+  const V6Lpm L = *reinterpret_cast<const V6Lpm*>(b.data() + img->hdr.v6_lpm);
+  const uint32_t mask = (1u << L.hash_log2) - 1u, S = kV6BucketSlots, W = kV6SlotWords;
+  auto words = [](u128 v, uint32_t len, uint32_t* m) {
+    const uint32_t a[4] = {uint32_t(v >> 96), uint32_t(v >> 64), uint32_t(v >> 32), uint32_t(v)};
+    v6_mask(a, len, m);
+  };
+  auto in_base = [&](const uint32_t* m, uint32_t len) {
+    const uint64_t hk = v6_hkey(m, len);
+    for (uint32_t bi : {hash_b1(hk, mask), hash_b2(hk, mask)})
+      for (uint32_t i = 0; i < S; i++) {
+        const uint32_t* w = b.data() + L.hash_off + (size_t(bi) * S + i) * W;
+        if (w[4] == (len | kV6Valid) && w[0] == m[0] && w[1] == m[1] && w[2] == m[2] && w[3] == m[3]) return true;
+      }
+    return false;
+  };
+  // new LPM entries go to the overflow table of the IPv6 journal (never into the published base)
+  const size_t before = img->v6_ovf.size();
+  auto put = [&](u128 v, uint32_t len, uint32_t code) {
+    std::array<uint32_t, 5> key;
+    words(v, len, key.data());
+    key[4] = len;
+    if (in_base(key.data(), len) || img->v6_ovf.count(key)) return;
+    img->v6_ovf[key] = code;
+  };
+  std::vector<uint32_t> lens(L.lens, L.lens + L.n_lens);
+  auto take = [&](const IPMatch& f) -> int {
+    if (!f.set || f.addr.fam != 6) return GPC_OK;
+    const int len = f.plen < 0 ? 128 : f.plen;
+    if (len <= 0) return GPC_OK;
+    const u128 v = v6_value(f.addr) & v6_prefix_mask(len);
+    if (codes.find(v, len) >= 0) return GPC_OK;
+    const int id = codes.add_leaf(v, len);
+    if (id < 0) {
+      if (std::getenv("GPC_IMAGE_DEBUG"))
+        std::fprintf(stderr, "IPv6 prefix %016llx%016llx/%d: %s\n", (unsigned long long)(v >> 64), (unsigned long long)v, len,
+                     codes.why_not(v, len));
+      return -GPC_EINVAL;
+    }
+    const V6Codes::Node& N = codes.nodes[size_t(id)];
+    // the prefix itself, then a marker at every shorter length its binary search passes through
+    // (build_image6), carrying the code of its deepest ancestor no longer than that length
+    const int t = int(std::lower_bound(lens.begin(), lens.end(), uint32_t(len)) - lens.begin());
+    if (t >= int(lens.size()) || lens[size_t(t)] != uint32_t(len)) return -GPC_EINVAL;
+    put(v, uint32_t(len), N.code);
+    int lo = 0, hi = int(lens.size()) - 1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) / 2;
+      if (mid == t) break;
+      if (mid > t) {
+        hi = mid - 1;
+        continue;
+      }
+      const uint32_t M = lens[size_t(mid)];
+      int a = N.parent;
+      while (a > 0 && codes.nodes[size_t(a)].len > int(M)) a = codes.nodes[size_t(a)].parent;
+      put(v & v6_prefix_mask(int(M)), M, a > 0 ? codes.nodes[size_t(a)].code : 0u);
+      lo = mid + 1;
+    }
+    return GPC_OK;
+  };
+  int rc = GPC_OK;
+  auto scan = [&](const Flow& f) {
+    if (f.table < TB_AP_EGRESS || f.table > TB_INGRESS_DEFAULT || rc) return;
+    for (const IPMatch* m : {&f.m.nw_src, &f.m.nw_dst, &f.m.ct_nw_src, &f.m.ct_nw_dst})
+      if (!rc) rc = take(*m);
+  };
+  for (uint32_t c : conj) {
+    auto it = np.policies().find(c);
+    if (it == np.policies().end()) continue;
+    for (Clause* cl : it->second->clauses())
+      for (auto& kv : cl->matches)
+        if (kv.second->flow) scan(*kv.second->flow);
+  }
+  for (auto& kv : np.hard_flows())
+    if ((hard_tables >> (kv.second.table - 1)) & 1u) scan(kv.second);
+  if (rc) return rc;
+  img->v6_prefixes = uint32_t(codes.nodes.size() - 1);
+  if (img->v6_ovf.size() != before) {  // a new overflow table for this epoch's journal header
+    std::vector<std::array<uint32_t, 8>> sl;
+    sl.reserve(img->v6_ovf.size());
+    for (auto& kv : img->v6_ovf)
+      sl.push_back({kv.first[0], kv.first[1], kv.first[2], kv.first[3], kv.first[4] | kV6Valid, kv.second, 0u, 0u});
+    std::vector<uint32_t> tab;
+    uint32_t lg = 0;
+    if (!v6_hash_build(sl, 0.5, &tab, &lg)) return -GPC_ENOMEM;
+    j6->set_v6_overflow(std::move(tab), lg);
+  }
   return GPC_OK;
 }
 
@@ -1181,6 +1348,9 @@ void Journal::reset(const HostImage* base, uint32_t lg) {
     hard_offs_[t].clear();
   }
   std::memset(tables_, 0, sizeof tables_);
+  ovf_table_.clear();
+  ovf_off_ = ovf_log2_ = 0;
+  ovf_dirty_ = false;
 }
 
 uint32_t Journal::n_tombstones() const {
@@ -1219,6 +1389,12 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
   }
   // 2. current versions
   Gather G;
+  G.fam = fam_;
+  G.codes = fam_ == 6 ? base_->codes6.get() : nullptr;
+  if (fam_ == 6 && !G.codes) {
+    *err = "IPv6 journal without a prefix tree";
+    return -GPC_EINVAL;
+  }
   int rc = gather_rules(np, conj, hard_tables, &G);
   if (rc) {
     *err = G.error;
@@ -1362,6 +1538,12 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     return append(pt.data(), pt.size(), 16);
   };
   h.bloom_axes = bloom_axes_;
+  if (ovf_dirty_) {
+    ovf_off_ = append(ovf_table_.data(), ovf_table_.size(), 16);
+    ovf_dirty_ = false;
+  }
+  h.v6_ovf_off = ovf_off_;
+  h.v6_ovf_log2 = ovf_log2_;
   h.bdead_off = publish(bdead_, bpt_, bdirty_, base_->n_rids);
   h.odead_off = publish(odead_, opt_, odirty_, n_versions);
   for (int t = 0; t < 6; t++) {

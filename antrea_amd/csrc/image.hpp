@@ -1,7 +1,9 @@
 // Builds the device classification image (core.hpp layout) from the realized flow table.
 #pragma once
 
+#include <array>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <unordered_map>
@@ -12,6 +14,8 @@
 #include "core.hpp"
 
 namespace gpc {
+
+class V6Codes;  // IPv6 prefix tree and codes (image.cpp)
 
 struct HostImage {
   ImageHdr hdr{};
@@ -26,6 +30,10 @@ struct HostImage {
   std::vector<uint32_t> hard_rids[6];                // hard pseudo-rules per table
   bool any_noact = false;  // a soft rule without an IPv4 conj_id flow (delta combine needs none)
   uint32_t v6_code_bits = 0, v6_prefixes = 0;  // IPv6 image: deepest code, interned prefixes
+  std::shared_ptr<V6Codes> codes6;             // IPv6 image: its prefix tree (delta commits extend it)
+  // IPv6 image: LPM entries of the prefixes delta commits interned ({masked address, len} -> code),
+  // published through the IPv6 journal's overflow table (extend_image6)
+  std::map<std::array<uint32_t, 5>, uint32_t> v6_ovf;
 };
 
 // Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
@@ -58,8 +66,15 @@ class SlotMap {
 
 // alloc = false (background compactor): counter slots are looked up, never allocated.
 int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true);
-// The IPv6 image (core.hpp "IPv6 interning"): full build, no journal.
+// The IPv6 image (core.hpp "IPv6 interning"): full build.
 int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true);
+class Journal;
+// IPv6 delta commits: interns the prefixes of the changed rules `conj` (and of the hard flows of
+// `hard_tables`) that the image's tree lacks (V6Codes::add_leaf: no existing code changes) and
+// adds their LPM entries and markers to img->v6_ovf; when that grew, the journal gets a new
+// overflow table (probed next to the base LPM hash by delta-epoch kernels). Nothing published is
+// rewritten. -GPC_EINVAL when a prefix cannot be interned (rebuild the IPv6 image instead).
+int extend_image6(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t hard_tables, HostImage* img, Journal* j6);
 // Append-only delta store over one base image (core.hpp "journal"). apply() appends the current
 // versions of the changed rules (records, driver-bucket entries, copied-on-write head pages) and a
 // new epoch header with the cumulative tombstones; nothing published earlier is rewritten, so the
@@ -67,6 +82,14 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
 class Journal {
  public:
   void reset(const HostImage* base, uint32_t lg = 16);
+  // IPv6 journal: rules gathered as an IPv6 image over the base's codes (base->codes6)
+  void set_family(int fam) { fam_ = fam; }
+  // IPv6: the overflow LPM table the next epoch header points at (appended by the next apply)
+  void set_v6_overflow(std::vector<uint32_t> table, uint32_t log2) {
+    ovf_table_ = std::move(table);
+    ovf_log2_ = log2;
+    ovf_dirty_ = true;
+  }
   void set_base(const HostImage* base) { base_ = base; }  // the base image object moved
   int apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, std::string* err,
             bool alloc = true);
@@ -88,6 +111,10 @@ class Journal {
   std::vector<uint32_t> hard_orids_[6], hard_offs_[6];
   JournalTable tables_[6];
   uint32_t bloom_axes_ = 0;  // JournalHdr.bloom_axes
+  int fam_ = 4;
+  std::vector<uint32_t> ovf_table_;
+  uint32_t ovf_off_ = 0, ovf_log2_ = 0;
+  bool ovf_dirty_ = false;
 };
 
 }  // namespace gpc

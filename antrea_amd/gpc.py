@@ -101,7 +101,8 @@ class gpc_image_stats(C.Structure):
                 ("bytes_entries", C.c_uint64), ("bytes_hash", C.c_uint64), ("overlay_bytes", C.c_uint64),
                 ("n_overlay_rules", C.c_uint32), ("n_tombstones", C.c_uint32), ("n_full_builds", C.c_uint64),
                 ("n_delta_builds", C.c_uint64), ("n_background_builds", C.c_uint64), ("group_key", C.c_uint32),
-                ("lane_sort", C.c_uint32)]
+                ("lane_sort", C.c_uint32), ("v6_full_builds", C.c_uint64), ("v6_delta_builds", C.c_uint64),
+                ("v6_overlay_rules", C.c_uint32), ("v6_prefixes", C.c_uint32)]
 
 
 class gpc_endpoint(C.Structure):
@@ -126,7 +127,7 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
            "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay",
            "gpc_set_launch_timing", "gpc_launch_times", "gpc_create_multi", "gpc_n_devices", "gpc_classify_on",
-           "gpc_classify6_on", "gpc_classify_host_on", "gpc_counters_on"]
+           "gpc_classify6_on", "gpc_classify_host_on", "gpc_counters_on", "gpc_debug_epoch6"]
 
 _lib = None
 
@@ -169,6 +170,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_get_image_stats.argtypes = [vp, C.POINTER(gpc_image_stats)]
     lib.gpc_debug_image.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(vp), C.POINTER(sz)]
     lib.gpc_debug_epoch.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(C.c_uint32)]
+    lib.gpc_debug_epoch6.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(sz), C.POINTER(C.c_uint32)]
     lib.gpc_load_flows.argtypes = [vp, C.c_char_p, sz, i32, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
     u8p = C.POINTER(C.c_uint8)
     lib.gpc_install_service_group.argtypes = [vp, C.c_uint32, i32, C.POINTER(gpc_endpoint), sz]
@@ -659,6 +661,14 @@ class Classifier:
         _check(self.lib.gpc_debug_epoch(self.h, C.byref(p), C.byref(n), C.byref(h)), "gpc_debug_epoch")
         return C.cast(p, C.c_void_p).value, n.value, h.value
 
+    def debug_epoch6(self):
+        """debug_epoch for the IPv6 image's journal."""
+        p = C.POINTER(C.c_uint32)()
+        n = C.c_size_t()
+        h = C.c_uint32()
+        _check(self.lib.gpc_debug_epoch6(self.h, C.byref(p), C.byref(n), C.byref(h)), "gpc_debug_epoch6")
+        return C.cast(p, C.c_void_p).value, n.value, h.value
+
     def image_stats(self) -> dict:
         st = gpc_image_stats()
         _check(self.lib.gpc_get_image_stats(self.h, C.byref(st)), "gpc_get_image_stats")
@@ -669,4 +679,6 @@ class Classifier:
                 "overlay_bytes": st.overlay_bytes, "n_overlay_rules": st.n_overlay_rules,
                 "n_tombstones": st.n_tombstones, "n_full_builds": st.n_full_builds,
                 "n_delta_builds": st.n_delta_builds, "n_background_builds": st.n_background_builds,
-                "group_key": st.group_key, "lane_sort": [st.lane_sort & 0xff, st.lane_sort >> 8]}
+                "group_key": st.group_key, "lane_sort": [st.lane_sort & 0xff, st.lane_sort >> 8],
+                "v6_full_builds": st.v6_full_builds, "v6_delta_builds": st.v6_delta_builds,
+                "v6_overlay_rules": st.v6_overlay_rules, "v6_prefixes": st.v6_prefixes}

@@ -312,6 +312,10 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint64_t n_background_builds;  /* full rebuilds done by the background compactor and installed */
   uint32_t group_key;            /* gpc_group_key grouped IPv4 batches of this epoch use (ADDR/SCAN) */
   uint32_t lane_sort;            /* lane-regrouping table per policy stage: egress | ingress << 8   */
+  /* IPv6 image (ipv6_enabled): full rebuilds, delta epochs, its journal */
+  uint64_t v6_full_builds, v6_delta_builds;
+  uint32_t v6_overlay_rules;     /* live rules in the IPv6 journal                               */
+  uint32_t v6_prefixes;          /* interned IPv6 prefixes (incl. those added by delta commits)  */
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */
@@ -479,6 +483,8 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
 /* Host mirror of the journal pool and the current epoch's journal header offset (NULL / 0 when
  * the epoch is the base image alone). */
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
+/* The same for the IPv6 image's journal (IPv6 delta epochs). */
+int gpc_debug_epoch6(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
 /* The epoch (gpc_image_stats.epoch) the last gpc_classify* launch on `stream` was bound to: with
  * classification concurrent to commits, every launch sees exactly this one committed epoch. */
 int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch);

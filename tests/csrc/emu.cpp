@@ -113,20 +113,32 @@ extern "C" int emu_trace(const uint32_t* blob, const void* hdr, const uint32_t* 
 }
 
 // IPv6 batch over the IPv6 image (gpc_debug_image6): addresses mapped to codes as the kernel does.
-extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out,
-                             unsigned long long* counters) {
+extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const uint32_t* pool, uint32_t jhdr,
+                             const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, unsigned long long* counters) {
   const ImageHdr* h = static_cast<const ImageHdr*>(hdr);
-  View im{{blob, h, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}, 1u, 0u};
+  View im{{blob, h, nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr};
+  const uint32_t* ovf = nullptr;
+  uint32_t ovf_log2 = 0;
+  if (pool) {  // an IPv6 delta epoch (gpc_debug_epoch6)
+    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + jhdr);
+    if (jh->bdead_off) im.base.dead = pool + jh->bdead_off;
+    im.n_img = 2u;
+    if (jh->v6_ovf_off) {
+      ovf = pool + jh->v6_ovf_off;
+      ovf_log2 = jh->v6_ovf_log2;
+    }
+  }
   auto code = [&](const uint8_t* col, size_t i) {
     uint32_t a[4];
     v6_words(col + 16 * i, a);
-    return v6_code(blob, h->v6_lpm, a);
+    return v6_code(blob, h->v6_lpm, a, ovf, ovf_log2);
   };
   auto code2 = [&](const uint8_t* c0, const uint8_t* c1, size_t i, uint32_t* c) {  // the kernel's paired LPM
     uint32_t a[2][4];
     v6_words(c0 + 16 * i, a[0]);
     v6_words(c1 + 16 * i, a[1]);
-    v6_codes<2>(blob, h->v6_lpm, a, c);
+    if (ovf) v6_codes<2, true>(blob, h->v6_lpm, a, c, ovf, ovf_log2);
+    else v6_codes<2>(blob, h->v6_lpm, a, c);
   };
   for (size_t i = 0; i < n; i++) {
     g_lines.clear();
@@ -141,7 +153,8 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const gpc_pk
     make_pkt(p, src, dst, pk->sport[i], pk->dport[i], pk->proto[i], pk->out_port[i], pk->in_port ? pk->in_port[i] : 0u,
              pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst,
              pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK), view_bloom_axes(im));
-    PacketOut o = classify_packet<false, 0>(im, p, dest, pk->ct_mark ? pk->ct_mark[i] : 0u);
+    const uint32_t cm = pk->ct_mark ? pk->ct_mark[i] : 0u;
+    PacketOut o = pool ? classify_packet<true, 0>(im, p, dest, cm) : classify_packet<false, 0>(im, p, dest, cm);
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;

@@ -31,8 +31,8 @@ def load():
                                   C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
     _lib.emu_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(gpc.gpc_pkt_soa), C.c_void_p,
                                C.POINTER(gpc.gpc_trace_step), C.POINTER(C.c_uint32)]
-    _lib.emu_classify6.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p,
-                                   C.c_void_p]
+    _lib.emu_classify6.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(gpc.gpc_pkt_soa),
+                                   C.c_size_t, C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -46,7 +46,8 @@ def classify6(clf: "gpc.Classifier", cols, counters=None):
     if counters is not None:
         assert counters.dtype == np.uint64 and counters.flags.c_contiguous
         cptr = counters.ctypes.data
-    load().emu_classify6(blob, hdr, C.byref(soa), n, out.ctypes.data, cptr)
+    pool, _, jhdr = clf.debug_epoch6()
+    load().emu_classify6(blob, hdr, pool, jhdr, C.byref(soa), n, out.ctypes.data, cptr)
     return out.reshape(n, 2)
 
 

@@ -1,0 +1,62 @@
+"""GPU tier: IPv6 delta epochs on the device. A dual-stack context replays
+the seeded churn log (tests/test_ipv6_delta.py: address adds / deletes, uninstall / reinstall,
+priority reassignment, mapped into fd00:10::/96 next to the IPv4 addresses) through delta
+commits. After each commit the device's IPv6 verdicts (gpc_classify6 over the base image + the
+IPv6 journal + its overflow LPM table) equal the host emulation of the same epoch, which the CPU
+tier pins to the IPv4 image and to the oracle; at the end the device is checked against the
+Python oracle directly, and after a compaction again."""
+import copy
+
+import numpy as np
+import pytest
+
+from antrea_amd import gpc, workload
+from tests import emu
+from tests.golden import make_churn_fixture as mcf
+from tests.test_emu_parity import _cmp
+from tests.test_ipv6_delta import _map_log, _oracle_after, _packets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    from antrea_amd.build import build
+    build()
+    import torch
+    assert torch.cuda.is_available(), "GPU tier needs a HIP device"
+
+
+@pytest.mark.parametrize("size", ["small", "C3-10k"])
+def test_gpu_ipv6_delta_epochs_dual_stack(size):
+    wl = (workload.config3(seed=11, n_policies_per_dir=6, rules_per_policy=8) if size == "small"
+          else workload.config3(n_policies_per_dir=50, rules_per_policy=100))
+    n_ops = 600 if size == "small" else 1500
+    log4 = mcf.ops(wl, seed=0x6D)[:n_ops] + [{"op": "commit"}]
+    log6 = _map_log(log4, dual=True)
+    cols = _packets(wl, log4, 20000 if size == "small" else 100_000, seed=13)
+    cols6 = workload.packets_to_v6(cols)
+    c = gpc.Classifier(ipv4=True, ipv6=True, compact_after=-1)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(workload.to_ipv6(wl, dual=True).rules))
+    c.commit()
+    checked = 0
+    for k, o in enumerate(log6):
+        if o["op"] != "commit":
+            mcf.apply(c, [o])
+            continue
+        c.commit()
+        if checked < 4 or o is log6[-1]:
+            _cmp(c.classify6_host(cols6), emu.classify6(c, cols6), cols)
+            _cmp(c.classify_host(cols), emu.classify(c, cols), cols)
+            checked += 1
+    st = c.image_stats()
+    assert st["v6_delta_builds"] >= 5 and st["v6_overlay_rules"] > 0, st
+    got = c.classify6_host(cols6)
+    if size == "small":  # the Python oracle over C3-10k's flows would take minutes; the emulation stands in
+        n = 300
+        sub = {k: v[:n] for k, v in cols6.items()}
+        _cmp(got[:n], _oracle_after(workload.to_ipv6(wl, dual=True).rules, log6, sub, n, True), sub)
+    c.compact()
+    assert c.image_stats()["v6_overlay_rules"] == 0
+    _cmp(c.classify6_host(cols6), got, cols)
