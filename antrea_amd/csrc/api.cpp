@@ -70,17 +70,6 @@ static StreamKey stream_key(hipStream_t s) {
   return StreamKey{s, s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id()};
 }
 
-// IPv6 grouping key: the 8 address bits just above the shortest prefix length of the image's prefix
-// tree (the bits in which its shortest prefixes differ; fd00:10::/96 embedding: the embedded IPv4
-// address's top byte).
-static int32_t v6_group_bit(const HostImage& h) {
-  if (!h.hdr.v6_lpm || h.blob.size() * 4 < size_t(h.hdr.v6_lpm) * 4 + sizeof(V6Lpm)) return 0;
-  const V6Lpm* L = reinterpret_cast<const V6Lpm*>(h.blob.data() + h.hdr.v6_lpm);
-  const int32_t shortest = L->n_lens ? int32_t(L->lens[0]) : 8;
-  return std::min<int32_t>(120, std::max<int32_t>(0, shortest - 8));
-}
-
-
 struct DevImage {  // one uploaded image (freed when the last epoch using it retires)
   ImageHdr* d_hdr = nullptr;
   uint32_t* d_blob = nullptr;
@@ -108,7 +97,6 @@ struct DevEpoch {
   std::shared_ptr<DevImage> v6_pool;    // journal pool of that base (append-only)
   uint32_t v6_jhdr = 0;                 // this epoch's IPv6 JournalHdr (0: base only)
   uint32_t v6_lpm = 0;                  // its ImageHdr.v6_lpm
-  int32_t v6_bit = 0;                   // grouping key of IPv6 batches (v6_group_bit)
   uint64_t epoch = 0;
   std::map<StreamKey, hipEvent_t> last_use;  // last launch on each stream that used this epoch
 };
@@ -199,8 +187,8 @@ struct gpc_ctx {
   // ingress verdicts of a grouped batch stored in grouped order, then put in caller order by
   // unpermute_kernel (1) or stored at the caller index by the ingress launch (0)
   uint32_t group_unpermute = env_u32("GPC_GROUP_UNPERMUTE", 1, 0, 1);
-  // IPv6 grouping: opt in with GPC_GROUP_V6=1 (C3 in IPv6, 64M packets: 31.57 ms plain, 31.69 grouped)
-  uint32_t group_v6 = env_u32("GPC_GROUP_V6", 0, 0, 1);
+  // IPv6 batches are grouped like IPv4 ones, over their code columns (GPC_GROUP_V6=0: never)
+  uint32_t group_v6 = env_u32("GPC_GROUP_V6", 1, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;
   std::vector<uint32_t> released_slots;
@@ -927,7 +915,6 @@ int gpc_replay(gpc_ctx* ctx) {
     if (!rc && !ctx->last6.blob.empty()) {
       rc = upload_image(ctx->last6, D.device, us, &ne[k].v6);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
-      ne[k].v6_bit = v6_group_bit(ctx->last6);
       const Journal& j6 = ctx->journal6;
       if (!rc && j6.active()) {
         rc = alloc_pool(D.device, us, &ne[k].v6_pool);
@@ -1070,10 +1057,10 @@ int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n
   // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
   // the next batch on that stream (launches of one stream run in order), so callers on different
   // streams never share one and the data path does no allocation once warm
-  GroupArgs ga{nullptr, group_key(ctx), D.cur.base->axes, ctx->group_src_bits, ctx->group_xcd, 0, ctx->group_unpermute,
+  GroupArgs ga{nullptr, group_key(ctx), D.cur.base->axes, ctx->group_src_bits, ctx->group_xcd, ctx->group_unpermute,
                D.cur.svc && lb_out && ctx->group_unpermute};
   if (group_batch(ctx, n, D.cur.base->bytes))
-    if (const int e = group_scratch_for(ctx, D, st, group_scratch_bytes(*pk, n, false, ga.lb), &ga.scratch)) return e;
+    if (const int e = group_scratch_for(ctx, D, st, group_scratch_bytes(*pk, n, ga.lb), &ga.scratch)) return e;
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), D.d_counters, count,
                            ga.scratch ? &ga : nullptr, st, n ? next_marks(D) : nullptr);
   if (!rc && ga.scratch) rc = group_scratch_used(D, st);
@@ -1161,12 +1148,25 @@ int gpc_classify6_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t 
   EpochArgs ep{D.cur.v6->d_hdr, D.cur.v6->d_blob, D.cur.v6_jhdr ? D.cur.v6_pool->d_blob : nullptr, D.cur.v6_jhdr,
                nullptr, D.cur.v6_lpm, {0, 0}, uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1};
   hipStream_t st = (hipStream_t)stream;
-  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, D.cur.v6_bit, ctx->group_unpermute};
-  if (ctx->group_v6 && group_batch(ctx, n, D.cur.v6->bytes))
-    if (const int e = group_scratch_for(ctx, D, st, group_scratch_bytes(*pk, n, true, false), &ga.scratch)) return e;
-  int rc = launch_classify6(ep, *pk, n, out, D.d_counters, count, ga.scratch ? &ga : nullptr, st,
-                            n ? next_marks(D) : nullptr);
-  if (!rc && ga.scratch) rc = group_scratch_used(D, st);
+  // per-stream scratch: the code columns of the batch (v6_code_kernel), then, for a grouped batch,
+  // the grouping scratch of the IPv4-shaped batch over those columns (address key: the top byte of
+  // the source code, i.e. the batch's source prefixes in tree order)
+  GroupArgs ga{nullptr, GPC_GROUP_KEY_ADDR, 0u, 8u, ctx->group_xcd, ctx->group_unpermute, 0u};
+  const size_t code_bytes = (size_t(v6_code_columns(*pk)) * n * 4 + 255) & ~size_t(255);
+  gpc_pkt_soa shape = *pk;  // which columns the code batch has (group_scratch_bytes reads presence only)
+  shape.src = shape.dst = reinterpret_cast<const uint32_t*>(pk->src6);
+  shape.ct_src = pk->ct_src6 ? shape.src : nullptr;
+  shape.ct_dst = pk->ct_dst6 ? shape.src : nullptr;
+  uint8_t* scratch = nullptr;
+  if (n && ctx->group_v6 && group_batch(ctx, n, D.cur.v6->bytes)) {
+    if (const int e = group_scratch_for(ctx, D, st, code_bytes + group_scratch_bytes(shape, n, false), &scratch)) return e;
+    if (scratch) ga.scratch = scratch + code_bytes;
+  }
+  if (n && !scratch)
+    if (const int e = group_scratch(D, st, code_bytes, &scratch)) return e;
+  int rc = launch_classify6(ep, *pk, n, out, D.d_counters, count, ga.scratch ? &ga : nullptr,
+                            reinterpret_cast<uint32_t*>(scratch), st, n ? next_marks(D) : nullptr);
+  if (!rc && scratch) rc = group_scratch_used(D, st);
   if (rc || n == 0) return rc;
   return note_launch(ctx, D, st);
 }
@@ -1411,7 +1411,7 @@ int gpc_set_launch_timing(gpc_ctx* ctx, uint32_t slots) {
 int gpc_launch_times(gpc_ctx* ctx, gpc_launch_time* out, size_t cap, size_t* n) {
   if (!ctx || !n || (!out && cap)) return -GPC_EINVAL;
   static const char* const names[kLaunchKinds] = {"group_tiles", "classify_egress", "classify_ingress", "classify_both",
-                                                  "unpermute"};
+                                                  "unpermute",   "v6_codes"};
   double ms[kLaunchKinds] = {};
   uint32_t cnt[kLaunchKinds] = {};
   size_t dropped = 0;
@@ -1729,7 +1729,6 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (!v6_full) {  // the IPv6 base stays; a delta extends its journal (new prefixes' LPM entries included)
       ne[k].v6 = D.cur.v6;
       ne[k].v6_lpm = D.cur.v6_lpm;
-      ne[k].v6_bit = D.cur.v6_bit;
       ne[k].v6_pool = D.cur.v6_pool;
       ne[k].v6_jhdr = D.cur.v6_jhdr;
       if (v6_changed && ne[k].v6) {
@@ -1744,7 +1743,6 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     } else if (!ctx->last6.blob.empty()) {
       if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
-      ne[k].v6_bit = v6_group_bit(ctx->last6);
     }
     if (!svc_changed) ne[k].svc = D.cur.svc;
     else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, D.device, us, &ne[k].svc))) return fail(rc);

@@ -38,45 +38,40 @@ constexpr int block_threads() { return kSort ? kSortBlock : kBlock; }
 // stage, measured 8 % faster on C3 than one launch walking both stages (kStage = 0; lanes leave the
 // egress stage at different times). With Services one launch (0) does both stages: a second
 // launch would have to repeat the Service lookup, which costs more than the split saves (C4).
-// IPv6 address columns (16 network-order bytes per packet, 16-B aligned) -> the addresses' codes in
-// the IPv6 image (core.hpp v6_codes): one coalesced 128-bit load per address, byte swaps, then K
-// longest-prefix matches in lock step.
-__device__ __forceinline__ void v6_load(const uint8_t* col, uint64_t i, uint32_t* a) {
-  const uint4 v = reinterpret_cast<const uint4*>(col)[i];
-  a[0] = __builtin_bswap32(v.x);
-  a[1] = __builtin_bswap32(v.y);
-  a[2] = __builtin_bswap32(v.z);
-  a[3] = __builtin_bswap32(v.w);
-}
-// kDelta: an IPv6 delta epoch; the journal header's overflow table (if any) is probed too.
+// IPv6 batches: a first launch maps every IPv6 address of the batch to its code in
+// the IPv6 image (core.hpp v6_codes), one address per lane, into 32-bit code columns; the batch is
+// then an IPv4-shaped batch over the codes and takes the IPv4 launches (grouping, both policy
+// stages, un-permute) against the IPv6 image unchanged. The length descriptors of the binary search
+// are copied to LDS once per block, so a step's only memory access is its two bucket loads.
+constexpr int kCodeBlock = 256;
+struct V6Cols {
+  const uint8_t* c[4];  // src6, dst6, ct_src6, ct_dst6 (16 network-order bytes per packet, 16-B aligned)
+};
+// kDelta: an IPv6 delta epoch, whose journal header may carry an overflow table (probed in the same step).
 template <bool kDelta>
-__device__ __forceinline__ void v6_code_pair(const EpochArgs& ep, const uint8_t* c0, const uint8_t* c1, uint64_t i,
-                                             uint32_t* code) {
-  uint32_t a[2][4];
-  v6_load(c0, i, a[0]);
-  v6_load(c1, i, a[1]);
+__global__ __launch_bounds__(kCodeBlock) void v6_code_kernel(EpochArgs ep, V6Cols cols, uint64_t n,
+                                                             uint32_t* __restrict__ codes) {
+  __shared__ V6Len desc[kV6MaxLens];
+  const V6Lpm* L = reinterpret_cast<const V6Lpm*>(ep.blob + ep.v6_lpm);
+  const uint32_t words = L->n_lens * uint32_t(sizeof(V6Len) / 4);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(L->d);
+  for (uint32_t j = threadIdx.x; j < words; j += kCodeBlock) reinterpret_cast<uint32_t*>(desc)[j] = src[j];
+  __syncthreads();
+  const uint64_t i = uint64_t(blockIdx.x) * kCodeBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint4 v = reinterpret_cast<const uint4*>(cols.c[blockIdx.y])[i];
+  const uint32_t a[1][4] = {{__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z), __builtin_bswap32(v.w)}};
+  uint32_t code;
   if (kDelta) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
     if (jh->v6_ovf_off) {
-      v6_codes<2, true>(ep.blob, ep.v6_lpm, a, code, ep.pool + jh->v6_ovf_off, jh->v6_ovf_log2);
+      v6_codes<1, true>(ep.blob, ep.v6_lpm, a, &code, ep.pool + jh->v6_ovf_off, jh->v6_ovf_log2, desc);
+      codes[uint64_t(blockIdx.y) * n + i] = code;
       return;
     }
   }
-  v6_codes<2>(ep.blob, ep.v6_lpm, a, code);
-}
-template <bool kDelta>
-__device__ __forceinline__ uint32_t v6_code_at(const EpochArgs& ep, const uint8_t* col, uint64_t i) {
-  uint32_t a[1][4], c;
-  v6_load(col, i, a[0]);
-  if (kDelta) {
-    const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
-    if (jh->v6_ovf_off) {
-      v6_codes<1, true>(ep.blob, ep.v6_lpm, a, &c, ep.pool + jh->v6_ovf_off, jh->v6_ovf_log2);
-      return c;
-    }
-  }
-  v6_codes<1>(ep.blob, ep.v6_lpm, a, &c);
-  return c;
+  v6_codes<1>(ep.blob, ep.v6_lpm, a, &code, nullptr, 0, desc);
+  codes[uint64_t(blockIdx.y) * n + i] = code;
 }
 
 // Lane regrouping for a policy stage launch: the candidate scan of a wavefront runs as long as its
@@ -156,26 +151,6 @@ __device__ __forceinline__ void group_column(const T* __restrict__ in, T* __rest
   for (uint32_t k = threadIdx.x; k < m; k += kGroupThreads) outc[base + k] = buf[from[k]];
 }
 
-// An IPv6 address column (16 network-order bytes per packet) as four word columns.
-__device__ __forceinline__ void group_column16(const uint8_t* __restrict__ in, const uint8_t* outc, uint64_t base, uint32_t m,
-                                               const uint16_t* from, void* stage) {
-  const uint32_t* iw = reinterpret_cast<const uint32_t*>(in);
-  uint32_t* ow = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(outc));
-  uint32_t* buf = reinterpret_cast<uint32_t*>(stage);
-  for (uint32_t w = 0; w < 4; w++) {
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < m; j += kGroupThreads) buf[j] = iw[(base + j) * 4 + w];
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < m; k += kGroupThreads) ow[(base + k) * 4 + w] = buf[from[k]];
-  }
-}
-
-// Grouping key of an IPv6 packet: the 8 bits of ipv6_src from bit `bit` (0 = most significant).
-__device__ __forceinline__ uint32_t group_key6(const uint8_t* a, uint32_t bit) {
-  const uint32_t b0 = a[bit >> 3], b1 = (bit >> 3) < 15u ? a[(bit >> 3) + 1] : 0u;
-  return (((b0 << 8) | b1) >> (8u - (bit & 7u))) & 0xffu;
-}
-
 // Grouping key of a packet: the top src_bits of nw_src followed by the top 8 - src_bits of nw_dst.
 __device__ __forceinline__ uint32_t group_key(uint32_t src, uint32_t dst, uint32_t src_bits) {
   const uint32_t db = 8u - src_bits;
@@ -215,12 +190,10 @@ __device__ __forceinline__ uint32_t scan_key(const EpochArgs& ep, const gpc_pkt_
   return scan_bin(e) << 4 | scan_bin(g);
 }
 
-// v6_bit >= 0: an IPv6 batch, keyed by 8 bits of ipv6_src from that bit (api.cpp picks the bits
-// just above the shortest prefix of the IPv6 image). Else key_mode GPC_GROUP_KEY_SCAN: scan_key;
-// GPC_GROUP_KEY_ADDR: group_key.
+// key_mode GPC_GROUP_KEY_SCAN: scan_key; GPC_GROUP_KEY_ADDR: group_key (IPv6 batches: over the codes).
 __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(EpochArgs ep, gpc_pkt_soa in, uint64_t n,
                                                                     uint32_t key_mode, uint32_t axes, uint32_t src_bits,
-                                                                    int32_t v6_bit, gpc_pkt_soa g, uint32_t* __restrict__ orig) {
+                                                                    gpc_pkt_soa g, uint32_t* __restrict__ orig) {
   __shared__ uint32_t stage[kGroupTile];  // the tile's keys, then one column of the tile
   __shared__ uint16_t from[kGroupTile];   // grouped position -> tile position
   __shared__ uint32_t cur[kGroupBins];
@@ -229,10 +202,8 @@ __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(EpochArgs ep
   const uint64_t base = uint64_t(blockIdx.x) * kGroupTile;
   const uint32_t m = uint32_t(n - base < kGroupTile ? n - base : kGroupTile);
   if (tid < kGroupBins) cur[tid] = 0;
-  if (v6_bit < 0 && key_mode == GPC_GROUP_KEY_SCAN) {
+  if (key_mode == GPC_GROUP_KEY_SCAN) {
     for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = scan_key(ep, in, base + j, axes, axl + tid);
-  } else if (v6_bit >= 0) {
-    for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = group_key6(in.src6 + (base + j) * 16, uint32_t(v6_bit));
   } else if (src_bits == 8u) {
     for (uint32_t j = tid; j < m; j += kGroupThreads) stage[j] = in.src[base + j] >> 24;
   } else {
@@ -278,10 +249,6 @@ __global__ __launch_bounds__(kGroupThreads) void group_tiles_kernel(EpochArgs ep
   GPC_GROUP_COL(len, uint16_t);
   GPC_GROUP_COL(ct_mark, uint8_t);
 #undef GPC_GROUP_COL
-  if (in.src6) group_column16(in.src6, g.src6, base, m, from, stage);
-  if (in.dst6) group_column16(in.dst6, g.dst6, base, m, from, stage);
-  if (in.ct_src6) group_column16(in.ct_src6, g.ct_src6, base, m, from, stage);
-  if (in.ct_dst6) group_column16(in.ct_dst6, g.ct_dst6, base, m, from, stage);
 }
 
 // Logical block of this workgroup for a grouped batch: workgroups are dispatched round-robin over
@@ -311,44 +278,24 @@ __device__ __forceinline__ uint64_t logical_block(uint32_t mode) {
   return uint64_t(b % T) * kTileBlocks + b / T;
 }
 
-// kV6: an IPv6 batch (src6 / dst6 / ct_*6 columns) against the IPv6 image (base only, no Services).
 // orig != null: a grouped batch (group_tiles_kernel): pk holds the grouped columns, lane i of the
-// logical block order classifies grouped packet i, whose caller index is orig[i].
-template <bool kDelta, bool kSvc, int kStage, bool kV6 = false, bool kSort = false>
+// logical block order classifies grouped packet i, whose caller index is orig[i]. IPv6 batches come
+// here as code columns (v6_code_kernel) against the IPv6 image.
+template <bool kDelta, bool kSvc, int kStage, bool kSort = false>
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
-    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, void* __restrict__ midv,
+    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
     uint32_t xcd_order, uint2* __restrict__ gout) {
-  // grouped batches: the egress launch's result in grouped order (IPv6: 16 B, the address codes too)
-  uint2* const mid = reinterpret_cast<uint2*>(midv);
-  uint4* const mid6 = reinterpret_cast<uint4*>(midv);
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
   const uint64_t block_base = logical_block<kGroupTile / block_threads<kSort>()>(xcd_order) * block_threads<kSort>();
   uint64_t i = block_base + threadIdx.x;
   if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
   if (i >= n) return;
-  uint32_t src, dst, ct_src, ct_dst;
-  // Ingress launch: only the egress action (and, IPv6, the parked address codes) of the egress
-  // half is read here; nothing of it is held over the walk (the result is stored as a half).
-  uint32_t ea = 0, code_s = 0, code_d = 0;
-  if (kStage == 2) {
-    uint4 prev;
-    if (orig && kV6) {
-      prev = mid6[i];
-    } else if (orig) {
-      const uint2 v = mid[i];
-      prev = make_uint4(v.x, v.y, 0u, 0u);
-    } else if (kV6) {
-      prev = out[i];
-    } else {
-      const uint2 v = reinterpret_cast<const uint2*>(out)[2 * i];
-      prev = make_uint4(v.x, v.y, 0u, 0u);
-    }
-    ea = prev.y & 0xffu;
-    code_s = prev.z;
-    code_d = prev.w;
-  }
+  // Ingress launch: only the egress action of the egress half is read here; nothing of it is held
+  // over the walk (the result is stored as a half).
+  uint32_t ea = 0;
+  if (kStage == 2) ea = (orig ? mid[i].y : reinterpret_cast<const uint2*>(out)[2 * i].y) & 0xffu;
   // caller index of this packet (loaded where a result is stored: no register held over the walk)
   auto at = [&]() -> uint64_t { return orig ? uint64_t(orig[i]) : i; };
   // the ingress launch's result: its half of the verdict pair in grouped order into gout
@@ -359,39 +306,15 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     if (gout) {
       gout[i] = make_uint2(conj, packed);
     } else if (orig) {
-      const uint2 e = kV6 ? make_uint2(mid6[i].x, mid6[i].y) : mid[i];
+      const uint2 e = mid[i];
       out[at()] = make_uint4(e.x, e.y, conj, packed);
     } else {
       reinterpret_cast<uint2*>(out)[2 * i + 1] = make_uint2(conj, packed);
     }
   };
-  if (kV6) {
-    // The egress launch computes the src / dst codes (both LPMs in lock step) and parks them in the
-    // still empty ingress half of the verdict pair; the ingress launch takes them from there.
-    if (kStage == 2) {
-      src = code_s;
-      dst = code_d;
-    } else {
-      uint32_t sd[2];
-      v6_code_pair<kDelta>(ep, pk.src6, pk.dst6, i, sd);
-      src = sd[0];
-      dst = sd[1];
-    }
-    if (pk.ct_src6 && pk.ct_dst6) {
-      uint32_t cd[2];
-      v6_code_pair<kDelta>(ep, pk.ct_src6, pk.ct_dst6, i, cd);
-      ct_src = cd[0];
-      ct_dst = cd[1];
-    } else {
-      ct_src = pk.ct_src6 ? v6_code_at<kDelta>(ep, pk.ct_src6, i) : src;
-      ct_dst = pk.ct_dst6 ? v6_code_at<kDelta>(ep, pk.ct_dst6, i) : dst;
-    }
-  } else {
-    src = pk.src[i];
-    dst = pk.dst[i];
-    ct_src = pk.ct_src ? pk.ct_src[i] : src;
-    ct_dst = pk.ct_dst ? pk.ct_dst[i] : dst;  // pre-NAT destination
-  }
+  uint32_t src = pk.src[i], dst = pk.dst[i];
+  const uint32_t ct_src = pk.ct_src ? pk.ct_src[i] : src;
+  const uint32_t ct_dst = pk.ct_dst ? pk.ct_dst[i] : dst;  // pre-NAT destination
   uint32_t dport = pk.dport[i];
   const uint32_t sport = pk.sport[i], proto = pk.proto[i];
   uint32_t out_port = pk.out_port[i];
@@ -418,7 +341,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   }
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
-      if (kV6 || orig) store2(0u, 0u);  // ingress NONE (over the parked codes)
+      if (orig) store2(0u, 0u);  // ingress NONE
       return;
     }
     if (const uint32_t b = ingress_bypass(ep.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
@@ -471,8 +394,6 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   count_one(s);
   const VerdictOut e = s.v, g = s.v;
   if (kStage == 2) store2(g.conj, g.packed);
-  else if (kV6 && kStage == 1 && orig) mid6[i] = make_uint4(e.conj, e.packed, src, dst);  // codes parked for launch 2
-  else if (kV6 && kStage == 1) out[i] = make_uint4(e.conj, e.packed, src, dst);
   else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
   else out[i] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
 }
@@ -560,7 +481,7 @@ static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* g
 
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
-                   unsigned long long* counters, int count, const uint32_t* orig, void* mid, uint32_t xo, uint2* gout,
+                   unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, uint32_t xo, uint2* gout,
                    hipStream_t stream, LaunchMarks* marks) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   uint4* const o = reinterpret_cast<uint4*>(out);
@@ -573,14 +494,14 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
   const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
   launch_mark(marks, kLaunchEgress, stream);
   if (ep.sort_table[0])
-    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
                        ep, pk, n, o, lb_out, counters, count, orig, mid, xo, nullptr);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
                        lb_out, counters, count, orig, mid, xo, nullptr);
   launch_mark(marks, kLaunchIngress, stream);
   if (ep.sort_table[1])
-    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, false, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
                        ep, pk, n, o, lb_out, counters, count, orig, mid, xo, gout);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
@@ -667,21 +588,19 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
 constexpr uint64_t kMaxPackets = (1ull << 32) - uint64_t(kSortBlock);
 static_assert(kMaxPackets == GPC_MAX_BATCH, "gpc.h GPC_MAX_BATCH mirrors the launch limit");
 
-uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6, bool lb) {
-  uint64_t per = 4 /*orig*/ + (v6 ? 16 : 8) /*mid*/ + 2 + 2 + 1 + 4;  // + sport dport proto out_port
-  per += v6 ? 32 + (pk.ct_src6 ? 16 : 0) + (pk.ct_dst6 ? 16 : 0) : 8 + (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0);
-  per += (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) +
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool lb) {
+  uint64_t per = 4 /*orig*/ + 8 /*mid*/ + 4 + 4 + 2 + 2 + 1 + 4;  // + src dst sport dport proto out_port
+  per += (pk.ct_src ? 4 : 0) + (pk.ct_dst ? 4 : 0) + (pk.in_port ? 4 : 0) + (pk.svc_group ? 4 : 0) + (pk.tun_id ? 4 : 0) +
          (pk.ct_state ? 1 : 0) + (pk.dest ? 1 : 0) + (pk.len ? 2 : 0) + (pk.ct_mark ? 1 : 0);
   per += 8;  // gout: the ingress halves of the verdict pairs in grouped order (GroupArgs.unpermute)
   if (lb) per += 16;  // lbg: the Service launch's LB results in grouped order
-  return per * n + 26 * 256;  // every region 256-B aligned
+  return per * n + 22 * 256;  // every region 256-B aligned
 }
 
 // Carves the grouped columns, orig and mid out of group->scratch and launches group_tiles_kernel.
-static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, bool v6, const GroupArgs& group,
-                        hipStream_t stream, gpc_pkt_soa* g, uint32_t** orig, void** mid, uint2** gout, uint4** lbg,
-                        LaunchMarks* marks) {
-  if (!group.scratch || group.src_bits > 8 || group.v6_bit > 120 || (group.key != GPC_GROUP_KEY_ADDR && group.key != GPC_GROUP_KEY_SCAN)) return -GPC_EINVAL;
+static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, const GroupArgs& group, hipStream_t stream,
+                        gpc_pkt_soa* g, uint32_t** orig, uint2** mid, uint2** gout, uint4** lbg, LaunchMarks* marks) {
+  if (!group.scratch || group.src_bits > 8 || (group.key != GPC_GROUP_KEY_ADDR && group.key != GPC_GROUP_KEY_SCAN)) return -GPC_EINVAL;
   uint8_t* q = group.scratch;
   auto take = [&](uint64_t bytes) {
     uint8_t* r = q;
@@ -689,19 +608,12 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
     return r;
   };
   *g = gpc_pkt_soa{};
-  *mid = take((v6 ? 16 : 8) * n);
+  *mid = reinterpret_cast<uint2*>(take(8 * n));
   *orig = reinterpret_cast<uint32_t*>(take(4 * n));
   *gout = reinterpret_cast<uint2*>(take(8 * n));
   if (lbg) *lbg = group.lb ? reinterpret_cast<uint4*>(take(16 * n)) : nullptr;
-  if (v6) {
-    g->src6 = take(16 * n);
-    g->dst6 = take(16 * n);
-    if (pk.ct_src6) g->ct_src6 = take(16 * n);
-    if (pk.ct_dst6) g->ct_dst6 = take(16 * n);
-  } else {
-    g->src = reinterpret_cast<const uint32_t*>(take(4 * n));
-    g->dst = reinterpret_cast<const uint32_t*>(take(4 * n));
-  }
+  g->src = reinterpret_cast<const uint32_t*>(take(4 * n));
+  g->dst = reinterpret_cast<const uint32_t*>(take(4 * n));
   g->sport = reinterpret_cast<const uint16_t*>(take(2 * n));
   g->dport = reinterpret_cast<const uint16_t*>(take(2 * n));
   g->proto = take(n);
@@ -709,17 +621,14 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
   if (pk.in_port) g->in_port = reinterpret_cast<const uint32_t*>(take(4 * n));
   if (pk.svc_group) g->svc_group = reinterpret_cast<const uint32_t*>(take(4 * n));
   if (pk.tun_id) g->tun_id = reinterpret_cast<const uint32_t*>(take(4 * n));
-  if (!v6 && pk.ct_src) g->ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
-  if (!v6 && pk.ct_dst) g->ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.ct_src) g->ct_src = reinterpret_cast<const uint32_t*>(take(4 * n));
+  if (pk.ct_dst) g->ct_dst = reinterpret_cast<const uint32_t*>(take(4 * n));
   if (pk.ct_state) g->ct_state = take(n);
   if (pk.dest) g->dest = take(n);
   if (pk.len) g->len = reinterpret_cast<const uint16_t*>(take(2 * n));
   if (pk.ct_mark) g->ct_mark = take(n);
-  // the other family's address columns are ignored by the classification launches: never copied
-  // (their grouped regions do not exist)
-  gpc_pkt_soa in = pk;
-  if (v6) in.src = in.dst = in.ct_src = in.ct_dst = nullptr;
-  else in.src6 = in.dst6 = in.ct_src6 = in.ct_dst6 = nullptr;
+  gpc_pkt_soa in = pk;  // the IPv6 address columns are not read (an IPv6 batch comes as code columns)
+  in.src6 = in.dst6 = in.ct_src6 = in.ct_dst6 = nullptr;
   if (!group.unpermute) {
     *gout = nullptr;
     if (lbg) *lbg = nullptr;
@@ -727,45 +636,39 @@ static int launch_group(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, 
   const uint64_t tiles = (n + kGroupTile - 1) / kGroupTile;
   launch_mark(marks, kLaunchGroup, stream);
   hipLaunchKernelGGL(group_tiles_kernel, dim3(uint32_t(tiles)), dim3(kGroupThreads), 0, stream, ep, in, n, group.key,
-                     group.axes, group.src_bits, v6 ? group.v6_bit : -1, *g, *orig);
+                     group.axes, group.src_bits, *g, *orig);
   return 0;
 }
 
+uint32_t v6_code_columns(const gpc_pkt_soa& pk) { return 2u + (pk.ct_src6 ? 1u : 0u) + (pk.ct_dst6 ? 1u : 0u); }
+
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
-                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
+                     unsigned long long* counters, int count, const GroupArgs* group, uint32_t* codes, hipStream_t stream,
                      LaunchMarks* marks) {
   if (n == 0) return 0;
-  if (n > kMaxPackets) return -GPC_EINVAL;
-  gpc_pkt_soa g;
-  const gpc_pkt_soa* p = &pk;
-  uint32_t* orig = nullptr;
-  void* mid = nullptr;
-  uint32_t xo = 0;
-  uint2* gout = nullptr;
-  if (group) {
-    if (const int rc = launch_group(ep, pk, n, true, *group, stream, &g, &orig, &mid, &gout, nullptr, marks)) return rc;
-    xo = group->xcd_order;
-    p = &g;
+  if (n > kMaxPackets || !codes) return -GPC_EINVAL;
+  V6Cols cols{{pk.src6, pk.dst6, nullptr, nullptr}};
+  uint32_t nc = 2;
+  gpc_pkt_soa p4 = pk;  // the batch over code columns: src, dst [, ct_src] [, ct_dst]
+  p4.src6 = p4.dst6 = p4.ct_src6 = p4.ct_dst6 = nullptr;
+  p4.src = codes;
+  p4.dst = codes + n;
+  p4.ct_src = p4.ct_dst = nullptr;
+  if (pk.ct_src6) {
+    cols.c[nc] = pk.ct_src6;
+    p4.ct_src = codes + uint64_t(nc++) * n;
   }
-  const uint64_t blocks = (n + kBlock - 1) / kBlock;
-  uint4* const o = reinterpret_cast<uint4*>(out);
-  launch_mark(marks, kLaunchEgress, stream);
-  if (ep.pool)  // an IPv6 delta epoch: base + journal
-    hipLaunchKernelGGL((classify_kernel<true, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
-                       nullptr, counters, count, orig, mid, xo, nullptr);
+  if (pk.ct_dst6) {
+    cols.c[nc] = pk.ct_dst6;
+    p4.ct_dst = codes + uint64_t(nc++) * n;
+  }
+  launch_mark(marks, kLaunchCodes, stream);
+  const dim3 grid(uint32_t((n + kCodeBlock - 1) / kCodeBlock), nc);
+  if (ep.pool)  // an IPv6 delta epoch: base + journal (its overflow LPM table)
+    hipLaunchKernelGGL(v6_code_kernel<true>, grid, dim3(kCodeBlock), 0, stream, ep, cols, n, codes);
   else
-    hipLaunchKernelGGL((classify_kernel<false, false, 1, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
-                       nullptr, counters, count, orig, mid, xo, nullptr);
-  launch_mark(marks, kLaunchIngress, stream);
-  if (ep.pool)
-    hipLaunchKernelGGL((classify_kernel<true, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
-                       nullptr, counters, count, orig, mid, xo, gout);
-  else
-    hipLaunchKernelGGL((classify_kernel<false, false, 2, true>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, *p, n, o,
-                       nullptr, counters, count, orig, mid, xo, gout);
-  if (gout) launch_unpermute(mid, 4, gout, orig, n, reinterpret_cast<uint4*>(out), nullptr, nullptr, stream, marks);
-  launch_mark(marks, kLaunchEnd, stream);
-  return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
+    hipLaunchKernelGGL(v6_code_kernel<false>, grid, dim3(kCodeBlock), 0, stream, ep, cols, n, codes);
+  return launch_classify(ep, p4, n, out, nullptr, counters, count, group, stream, marks);
 }
 
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
@@ -776,12 +679,12 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   gpc_pkt_soa g;
   const gpc_pkt_soa* p = &pk;
   uint32_t* orig = nullptr;
-  void* mid = nullptr;
+  uint2* mid = nullptr;
   uint32_t xo = 0;
   uint2* gout = nullptr;
   uint4* lbg = nullptr;  // grouped Service batch with the un-permute: LB results in grouped order
   if (group) {
-    if (const int rc = launch_group(ep, pk, n, false, *group, stream, &g, &orig, &mid, &gout, &lbg, marks)) return rc;
+    if (const int rc = launch_group(ep, pk, n, *group, stream, &g, &orig, &mid, &gout, &lbg, marks)) return rc;
     xo = group->xcd_order;
     p = &g;
   }

@@ -275,14 +275,36 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 // whole IPv4 machinery (bands, Bloom bits, intervals) applies unchanged. code(a) is found on the
 // device by a longest-prefix match: binary search on the distinct prefix lengths (Waldvogel), one
 // hash probe per step -- prefixes and markers, each carrying the code of its best matching prefix.
+//
+// One hash table per prefix length, keyed by the prefix right-aligned: kv = a >> (128 - L) (4 words,
+// [0] most significant). Its slots hold only the low kw words of kv (kw = 1, 2 or 4) and the code:
+// the other 4 - kw words are the same for every entry of the length (the tag, kept in the length's
+// descriptor), so an address whose tag differs misses without a load. Rule sets whose prefixes of
+// one length share their upper bits (C3 in fd00:10::/96: every length) get 8-B slots, 8 per 64-B
+// bucket: the table is a quarter of a 32-B-slot table with the length in every slot (C3: 29 MB ->
+// ~5 MB, mostly L2-resident instead of Infinity-Cache traffic). Two choices, both loaded per probe.
 constexpr uint32_t kV6MaxLens = 64;
-struct V6Lpm {
-  uint32_t hash_off, hash_log2, n_lens, reserved;
-  uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
+struct V6Len {
+  uint32_t meta;     // prefix length | key words kw << 8 | log2(buckets) << 16
+  uint32_t tab_off;  // word offset of its buckets
+  uint32_t seed;     // hash state after the length and the tag (v6_seed)
+  uint32_t reserved;
+  uint32_t pat[4];  // kv words 0 .. 3 - kw: the tag every entry shares; words 4 - kw .. 3: the key of an
+                    // empty slot (no entry of the length has it)
 };
-// hash slot (8 words): masked address (4 words, most significant first), len | kV6Valid, code, 2 pad;
-// bucket = 2 slots (one 64-B line), two choices (both loaded per probe: measured faster on C3 than
-// 128-B single-line buckets with an overflow flag, whose table is larger)
+GPC_HD uint32_t v6_len(const V6Len& d) { return d.meta & 0xffu; }
+GPC_HD uint32_t v6_kw(const V6Len& d) { return (d.meta >> 8) & 0xffu; }
+GPC_HD uint32_t v6_log2(const V6Len& d) { return d.meta >> 16; }
+struct V6Lpm {
+  uint32_t n_lens, reserved[3];
+  uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
+  V6Len d[kV6MaxLens];        // d[i]: the table of lens[i]
+};
+// Bucket: 16 words (one 64-B line); slot = key (kw words), code, padding to 2 / 4 / 8 words.
+constexpr uint32_t kV6BucketWords = 16;
+GPC_HD uint32_t v6_slot_words(uint32_t kw) { return kw == 4u ? 8u : 2u * kw; }
+// Wide slot of the delta epochs' overflow table (journal): masked address (4 words), len | kV6Valid,
+// code, 2 pad; 2 slots per 64-B bucket, two choices.
 constexpr uint32_t kV6SlotWords = 8, kV6BucketSlots = 2, kV6Valid = 0x100u;
 GPC_HD void v6_mask(const uint32_t* a, uint32_t len, uint32_t* m) {
   for (int w = 0; w < 4; w++) {
@@ -294,17 +316,127 @@ GPC_HD uint64_t v6_hkey(const uint32_t* m, uint32_t len) {
   const uint64_t h = mix64(((uint64_t(m[0]) << 32) | m[1]) ^ (uint64_t(len + 1) * 0x9e3779b97f4a7c15ull));
   return mix64(h ^ ((uint64_t(m[2]) << 32) | m[3]));
 }
+// kv = a >> (128 - len): the top len bits of a, right-aligned (len 1..128).
+GPC_HD void v6_key(const uint32_t* a, uint32_t len, uint32_t* r) {
+  const uint64_t hi = (uint64_t(a[0]) << 32) | a[1], lo = (uint64_t(a[2]) << 32) | a[3];
+  const uint32_t s = 128u - len;
+  uint64_t rh, rl;
+  if (s >= 64u) {
+    rh = 0;
+    rl = hi >> (s - 64u);
+  } else if (s == 0u) {
+    rh = hi;
+    rl = lo;
+  } else {
+    rh = hi >> s;
+    rl = (lo >> s) | (hi << (64u - s));
+  }
+  r[0] = uint32_t(rh >> 32);
+  r[1] = uint32_t(rh);
+  r[2] = uint32_t(rl >> 32);
+  r[3] = uint32_t(rl);
+}
+// Bucket hash of a per-length table: 32-bit mixing only (no 64-bit multiplies: the hash is a
+// large part of a step's ALU work). seed = hash of the length and of the tag words (the same for
+// every key of the table, so kept in its descriptor); then one mix per key word.
+GPC_HD uint32_t v6_seed(uint32_t len, uint32_t kw, const uint32_t* r) {
+  uint32_t h = mix32(len * 0x9e3779b9u + 0x7f4a7c15u);
+  for (uint32_t w = 0; w + kw < 4u; w++) h = mix32(h ^ r[w]);
+  return h;
+}
+GPC_HD void v6_buckets(const V6Len& d, const uint32_t* r, uint32_t* b1, uint32_t* b2) {
+  const uint32_t kw = v6_kw(d);
+  uint32_t h = d.seed;
+  if (kw == 1u) {
+    h = mix32(h ^ r[3]);
+  } else {
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++)
+      if (w + kw >= 4u) h = mix32(h ^ r[w]);
+  }
+  const uint32_t mask = (1u << v6_log2(d)) - 1u;
+  *b1 = h & mask;
+  *b2 = mix32(h ^ 0x85ebca6bu) & mask;
+}
+// Does the length's table have to be probed for key kv: its tag matches and it is not the empty key.
+GPC_HD bool v6_probe_needed(const V6Len& d, const uint32_t* r) {
+  bool tag = true, empty = true;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) {
+    if (w + v6_kw(d) < 4u) tag = tag && r[w] == d.pat[w];
+    else empty = empty && r[w] == d.pat[w];
+  }
+  return tag && !empty;
+}
+// Key kv in one bucket (16 words): slot s of a kw-word table holds kv's low kw words, then the code.
+// Keys are unique in a table, so at most one slot matches: its code is OR-accumulated under a mask
+// (no data-dependent slot index, which the compiler would turn into a private-memory array).
+GPC_HD bool v6_bucket_find(const uint32_t* w, uint32_t kw, const uint32_t* r, uint32_t* code) {
+  uint32_t c = 0, any = 0;
+  if (kw == 1u) {
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const uint32_t mt = 0u - uint32_t(w[2 * s] == r[3]);
+      c |= w[2 * s + 1] & mt;
+      any |= mt;
+    }
+  } else if (kw == 2u) {
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint32_t mt = 0u - uint32_t(w[4 * s] == r[2] && w[4 * s + 1] == r[3]);
+      c |= w[4 * s + 2] & mt;
+      any |= mt;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const uint32_t mt = 0u - uint32_t(w[8 * s] == r[0] && w[8 * s + 1] == r[1] && w[8 * s + 2] == r[2] && w[8 * s + 3] == r[3]);
+      c |= w[8 * s + 4] & mt;
+      any |= mt;
+    }
+  }
+  if (any) *code = c;
+  return any != 0;
+}
+// A wide (overflow-table) bucket: masked address m of length len.
+GPC_HD bool v6_wide_find(const uint32_t* w, const uint32_t* m, uint32_t len, uint32_t* code) {
+  uint32_t c = 0, any = 0;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const uint32_t* x = w + s * kV6SlotWords;
+    const uint32_t mt = 0u - uint32_t(x[4] == (len | kV6Valid) && x[0] == m[0] && x[1] == m[1] && x[2] == m[2] && x[3] == m[3]);
+    c |= x[5] & mt;
+    any |= mt;
+  }
+  if (any) *code = c;
+  return any != 0;
+}
+// 16 words from a 64-B aligned bucket (four 128-bit loads).
+GPC_HD void v6_load_bucket(const uint32_t* p, uint32_t* w) {
+#if defined(__HIPCC__)
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint4 v = q[j];
+    w[4 * j] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+  }
+#else
+  for (uint32_t j = 0; j < kV6BucketWords; j++) w[j] = p[j];
+#endif
+}
 // code(a_k) for K addresses at once (a[k][0..3], [0] = most significant): the K binary searches run
-// in lock step (the step count is the same for every address up to one), so each step issues the
-// 2K bucket loads before any compare -- K independent dependency chains per lane instead of K in a row.
-// kOvf (IPv6 delta epochs): the journal's overflow table `ovf` (2^ovf_log2 buckets, the LPM entries
-// of prefixes interned since the base) is probed in the same step, its 2K loads issued with the
-// base's: no extra dependent round.
+// in lock step, so each step issues every bucket load before any compare. `desc`: the length
+// descriptors (the kernel's LDS copy; null: those of the image). kOvf (IPv6 delta epochs): the
+// journal's overflow table `ovf` (2^ovf_log2 wide buckets, the LPM entries of prefixes interned since
+// the base) is probed in the same step, its loads issued with the base's: no extra dependent round.
 template <int K, bool kOvf = false>
 GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)[4], uint32_t* code,
-                     const uint32_t* ovf = nullptr, uint32_t ovf_log2 = 0) {
+                     const uint32_t* ovf = nullptr, uint32_t ovf_log2 = 0, const V6Len* desc = nullptr) {
   const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
-  const uint32_t mask = (1u << L->hash_log2) - 1u;
+  const V6Len* D = desc ? desc : L->d;
   const uint32_t omask = (1u << ovf_log2) - 1u;
   int lo[K], hi[K];
 #pragma unroll
@@ -318,23 +450,35 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
 #pragma unroll
     for (int k = 0; k < K; k++) any |= lo[k] <= hi[k];
     if (!any) break;
-    uint32_t len[K], m[K][4];
-    const uint32_t* b[K][kOvf ? 4 : 2];
+    uint32_t r[K][4], kw[K], w[K][2][kV6BucketWords];
+    bool probe[K];
+    uint32_t m[K][kOvf ? 4 : 1], len[K], ow[K][kOvf ? 2 : 1][kOvf ? kV6BucketWords : 1];
 #pragma unroll
-    for (int k = 0; k < K; k++) {  // finished addresses re-probe their last length (result unused)
-      const int mid = lo[k] <= hi[k] ? (lo[k] + hi[k]) >> 1 : 0;
-      len[k] = L->lens[mid];
-      v6_mask(a[k], len[k], m[k]);
-      const uint64_t hk = v6_hkey(m[k], len[k]);
-      b[k][0] = blob + L->hash_off + size_t(hash_b1(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
-      b[k][1] = blob + L->hash_off + size_t(hash_b2(hk, mask)) * (kV6SlotWords * kV6BucketSlots);
-      if constexpr (kOvf) {
-        b[k][2] = ovf + size_t(hash_b1(hk, omask)) * (kV6SlotWords * kV6BucketSlots);
-        b[k][3] = ovf + size_t(hash_b2(hk, omask)) * (kV6SlotWords * kV6BucketSlots);
+    for (int k = 0; k < K; k++) {
+      const bool live = lo[k] <= hi[k];
+      const V6Len& d = D[live ? (lo[k] + hi[k]) >> 1 : 0];
+      len[k] = v6_len(d);
+      kw[k] = v6_kw(d);
+      v6_key(a[k], len[k], r[k]);
+      probe[k] = live && v6_probe_needed(d, r[k]);
+      uint32_t bk[2];
+      v6_buckets(d, r[k], &bk[0], &bk[1]);
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const uint32_t* b = blob + d.tab_off + size_t(bk[c]) * kV6BucketWords;
+        if (probe[k]) {
+          GPC_TOUCH(b, 64);
+          v6_load_bucket(b, w[k][c]);
+        }
       }
-      if (lo[k] <= hi[k]) {
-        GPC_TOUCH(b[k][0], 64);
-        GPC_TOUCH(b[k][1], 64);
+      if constexpr (kOvf) {
+        v6_mask(a[k], len[k], m[k]);
+        const uint64_t ok = v6_hkey(m[k], len[k]);
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+          const uint32_t* b = ovf + size_t(c ? hash_b2(ok, omask) : hash_b1(ok, omask)) * (kV6SlotWords * kV6BucketSlots);
+          if (live) v6_load_bucket(b, ow[k][c]);
+        }
       }
     }
 #pragma unroll
@@ -342,13 +486,13 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       if (lo[k] > hi[k]) continue;
       const int mid = (lo[k] + hi[k]) >> 1;
       bool hit = false;
-#pragma unroll
-      for (int c = 0; c < (kOvf ? 8 : 4); c++) {
-        const uint32_t* w = b[k][c >> 1] + (c & 1) * kV6SlotWords;
-        if (w[4] == (len[k] | kV6Valid) && w[0] == m[k][0] && w[1] == m[k][1] && w[2] == m[k][2] && w[3] == m[k][3]) {
-          hit = true;
-          code[k] = w[5];
-        }
+      if (probe[k]) {
+        hit = v6_bucket_find(w[k][0], kw[k], r[k], &code[k]);
+        hit = v6_bucket_find(w[k][1], kw[k], r[k], &code[k]) || hit;
+      }
+      if constexpr (kOvf) {
+        hit = v6_wide_find(ow[k][0], m[k], len[k], &code[k]) || hit;
+        hit = v6_wide_find(ow[k][1], m[k], len[k], &code[k]) || hit;
       }
       if (hit) lo[k] = mid + 1;
       else hi[k] = mid - 1;
@@ -361,6 +505,24 @@ GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* 
   if (ovf) v6_codes<1, true>(blob, lpm_off, aa, &c, ovf, ovf_log2);
   else v6_codes<1>(blob, lpm_off, aa, &c);
   return c;
+}
+// Is the (masked address m, len) entry in the base LPM (host: which delta entries go to the overflow).
+GPC_HD bool v6_base_has(const uint32_t* blob, uint32_t lpm_off, const uint32_t* m, uint32_t len) {
+  const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
+  for (uint32_t i = 0; i < L->n_lens; i++) {
+    const V6Len& d = L->d[i];
+    if (v6_len(d) != len) continue;
+    uint32_t r[4], w[kV6BucketWords], c = 0, bk[2];
+    v6_key(m, len, r);
+    if (!v6_probe_needed(d, r)) return false;
+    v6_buckets(d, r, &bk[0], &bk[1]);
+    for (int j = 0; j < 2; j++) {
+      v6_load_bucket(blob + d.tab_off + size_t(bk[j]) * kV6BucketWords, w);
+      if (v6_bucket_find(w, v6_kw(d), r, &c)) return true;
+    }
+    return false;
+  }
+  return false;
 }
 // 16 network-order bytes -> 4 host words, most significant first.
 GPC_HD void v6_words(const uint8_t* p, uint32_t* a) {

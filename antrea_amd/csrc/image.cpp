@@ -1095,8 +1095,81 @@ static bool v6_hash_build(const std::vector<std::array<uint32_t, 8>>& slots6, do
   return false;
 }
 
+// The LPM table of one prefix length (core.hpp V6Len): entries (kv = prefix right-aligned, code).
+// Key words kw = the fewest of 1 / 2 / 4 whose complement (the tag) all entries share; the empty-slot
+// key is one no entry has. 2-choice cuckoo placement over 64-B buckets, a larger table when it does
+// not converge. Fills d (except tab_off) and tab.
+static bool v6_len_table_build(uint32_t len, const std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>& ents,
+                               V6Len* d, std::vector<uint32_t>* tab) {
+  *d = V6Len{};
+  uint32_t kw = 4;
+  for (uint32_t k : {1u, 2u}) {
+    bool same = true;
+    for (auto& e : ents)
+      for (uint32_t w = 0; w + k < 4 && same; w++) same = e.first[w] == ents[0].first[w];
+    if (same) {
+      kw = k;
+      break;
+    }
+  }
+  const uint32_t sw = v6_slot_words(kw), ns = kV6BucketWords / sw;
+  std::set<std::array<uint32_t, 4>> used;
+  for (auto& e : ents) {
+    std::array<uint32_t, 4> k = e.first;
+    for (uint32_t w = 0; w + kw < 4; w++) k[w] = 0;
+    used.insert(k);
+  }
+  std::array<uint32_t, 4> empty{0u, 0u, 0u, 0u};
+  for (uint32_t w = 4 - kw; w < 4; w++) empty[w] = ~0u;
+  while (used.count(empty)) empty[3]--;  // at most |ents| tries
+  for (uint32_t w = 0; w < 4; w++) d->pat[w] = w + kw < 4 ? (ents.empty() ? 0u : ents[0].first[w]) : empty[w];
+  d->seed = v6_seed(len, kw, d->pat);
+  const double load = kw == 4 ? 0.7 : 0.85;
+  uint32_t lg = 0;
+  while (double(ns << lg) * load < double(ents.size() + 1)) lg++;
+  for (int attempt = 0; attempt < 8; attempt++, lg++) {
+    const uint32_t nb = 1u << lg;
+    d->meta = len | kw << 8 | lg << 16;
+    tab->assign(size_t(nb) * kV6BucketWords, 0u);
+    std::vector<uint8_t> full(size_t(nb) * ns, 0);
+    for (size_t s = 0; s < size_t(nb) * ns; s++)
+      for (uint32_t w = 0; w < kw; w++) (*tab)[s * sw + w] = empty[4 - kw + w];
+    std::mt19937 rng(4321 + attempt);
+    bool ok = true;
+    for (size_t n = 0; n < ents.size() && ok; n++) {
+      std::array<uint32_t, 4> cur = ents[n].first;
+      uint32_t code = ents[n].second;
+      bool placed = false;
+      for (int kick = 0; kick < 1000 && !placed; kick++) {
+        uint32_t bs[2];
+        v6_buckets(*d, cur.data(), &bs[0], &bs[1]);
+        for (uint32_t bk : bs) {
+          for (uint32_t i = 0; i < ns && !placed; i++) {
+            const size_t s = size_t(bk) * ns + i;
+            if (!full[s]) {
+              for (uint32_t w = 0; w < kw; w++) (*tab)[s * sw + w] = cur[4 - kw + w];
+              (*tab)[s * sw + kw] = code;
+              full[s] = 1;
+              placed = true;
+            }
+          }
+          if (placed) break;
+        }
+        if (!placed) {  // evict a random resident of one of the two buckets
+          const size_t s = size_t(bs[rng() & 1]) * ns + rng() % ns;
+          for (uint32_t w = 0; w < kw; w++) std::swap(cur[4 - kw + w], (*tab)[s * sw + w]);
+          std::swap(code, (*tab)[s * sw + kw]);
+        }
+      }
+      ok = placed;
+    }
+    if (ok) return true;
+  }
+  return false;
+}
+
 // IPv6 image: the same build over the IPv6 half of the flows (addresses interned as codes), plus
-// the LPM table the kernel maps packet addresses through (appended to the blob, hdr.v6_lpm).
+// the LPM tables the kernel maps packet addresses through (appended to the blob, hdr.v6_lpm).
 int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc) {
   *out = HostImage();
   out->codes6 = std::make_shared<V6Codes>();
@@ -1148,32 +1221,38 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
       lo = mid + 1;
     }
   }
-  std::vector<std::array<uint32_t, 8>> slots6;
+  // one table per length (core.hpp V6Len), appended after the V6Lpm block
+  std::vector<std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>> per_len(lens.size());
   for (auto& kv : lpm_map) {
     const u128 v = kv.first.first;
-    slots6.push_back({uint32_t(v >> 96), uint32_t(v >> 64), uint32_t(v >> 32), uint32_t(v), kv.first.second | kV6Valid,
-                      kv.second, 0u, 0u});
-  }
-  std::vector<uint32_t> tab;
-  uint32_t lg = 0;
-  if (!v6_hash_build(slots6, 0.7, &tab, &lg)) {
-    out->error = "IPv6 LPM table construction failed";
-    return -GPC_ENOMEM;
+    const uint32_t a[4] = {uint32_t(v >> 96), uint32_t(v >> 64), uint32_t(v >> 32), uint32_t(v)};
+    const size_t li = size_t(std::lower_bound(lens.begin(), lens.end(), kv.first.second) - lens.begin());
+    std::array<uint32_t, 4> r;
+    v6_key(a, kv.first.second, r.data());
+    per_len[li].push_back({r, kv.second});
   }
   auto& b = out->blob;
   while (b.size() % 16) b.push_back(0u);
   const uint32_t lpm = uint32_t(b.size());
   V6Lpm L{};
-  L.hash_log2 = lg;
   L.n_lens = uint32_t(lens.size());
-  for (size_t i = 0; i < lens.size(); i++) L.lens[i] = lens[i];
   const size_t lw = (sizeof(V6Lpm) / 4 + 15) / 16 * 16;
-  L.hash_off = lpm + uint32_t(lw);
   b.resize(b.size() + lw, 0u);
+  size_t tab_words = 0;
+  for (size_t i = 0; i < lens.size(); i++) {
+    L.lens[i] = lens[i];
+    std::vector<uint32_t> tab;
+    if (!v6_len_table_build(lens[i], per_len[i], &L.d[i], &tab)) {
+      out->error = "IPv6 LPM table construction failed";
+      return -GPC_ENOMEM;
+    }
+    L.d[i].tab_off = uint32_t(b.size());
+    b.insert(b.end(), tab.begin(), tab.end());
+    tab_words += tab.size();
+  }
   std::memcpy(b.data() + lpm, &L, sizeof L);
-  b.insert(b.end(), tab.begin(), tab.end());
   out->hdr.v6_lpm = lpm;
-  out->bytes_hash += 4ull * tab.size();
+  out->bytes_hash += 4ull * tab_words;
   out->v6_code_bits = uint32_t(codes.max_clen);
   out->v6_prefixes = uint32_t(codes.nodes.size() - 1);
   return GPC_OK;
@@ -1183,21 +1262,12 @@ int extend_image6(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t h
   if (!img->codes6 || !img->hdr.v6_lpm) return -GPC_EINVAL;
   V6Codes& codes = *img->codes6;
   const std::vector<uint32_t>& b = img->blob;
-  const V6Lpm L = *reinterpret_cast<const V6Lpm*>(b.data() + img->hdr.v6_lpm);
-  const uint32_t mask = (1u << L.hash_log2) - 1u, S = kV6BucketSlots, W = kV6SlotWords;
+  const V6Lpm& L = *reinterpret_cast<const V6Lpm*>(b.data() + img->hdr.v6_lpm);
   auto words = [](u128 v, uint32_t len, uint32_t* m) {
     const uint32_t a[4] = {uint32_t(v >> 96), uint32_t(v >> 64), uint32_t(v >> 32), uint32_t(v)};
     v6_mask(a, len, m);
   };
-  auto in_base = [&](const uint32_t* m, uint32_t len) {
-    const uint64_t hk = v6_hkey(m, len);
-    for (uint32_t bi : {hash_b1(hk, mask), hash_b2(hk, mask)})
-      for (uint32_t i = 0; i < S; i++) {
-        const uint32_t* w = b.data() + L.hash_off + (size_t(bi) * S + i) * W;
-        if (w[4] == (len | kV6Valid) && w[0] == m[0] && w[1] == m[1] && w[2] == m[2] && w[3] == m[3]) return true;
-      }
-    return false;
-  };
+  auto in_base = [&](const uint32_t* m, uint32_t len) { return v6_base_has(b.data(), img->hdr.v6_lpm, m, len); };
   // new LPM entries go to the overflow table of the IPv6 journal (never into the published base)
   const size_t before = img->v6_ovf.size();
   auto put = [&](u128 v, uint32_t len, uint32_t code) {

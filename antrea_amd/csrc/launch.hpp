@@ -30,19 +30,18 @@ int launch_merge_counters(unsigned long long* dst, const unsigned long long* src
                           uint64_t n_words, hipStream_t stream);
 // Packet grouping of a batch (classify.hip group_tiles_kernel): the batch is classified in the
 // order of an 8-bit key (scan lengths or address bits) within every tile of 16384 packets, from a grouped copy in
-// `scratch` (group_scratch_bytes(pk, n, v6, lb) bytes of device memory, live until the launches have run:
+// `scratch` (group_scratch_bytes(pk, n, lb) bytes of device memory, live until the launches have run:
 // stream-ordered).
 struct GroupArgs {
   uint8_t* scratch;
-  uint32_t key;        // GPC_GROUP_KEY_ADDR or GPC_GROUP_KEY_SCAN (IPv4 batches)
+  uint32_t key;        // GPC_GROUP_KEY_ADDR or GPC_GROUP_KEY_SCAN
   uint32_t axes;       // SCAN: bit a = axis a is read by a sub-index of the image (group_axes)
   uint32_t src_bits;   // ADDR: key = top src_bits of nw_src, then the top 8 - src_bits of nw_dst
   uint32_t xcd_order;  // block order (classify.hip logical_block): 1 = the blocks of one tile run on one XCD
-  int32_t v6_bit;      // IPv6 batches: key = 8 bits of ipv6_src from this bit (0 = most significant)
   uint32_t unpermute;  // 1: the ingress launch stores in grouped order, unpermute_kernel restores caller order
   uint32_t lb;         // 1: a Service batch with lb_out: its LB results are un-permuted too (scratch for them)
 };
-uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool v6, bool lb);
+uint64_t group_scratch_bytes(const gpc_pkt_soa& pk, uint64_t n, bool lb);
 // Launch timing (gpc_set_launch_timing): an event is recorded on the launch stream before every
 // kernel of one gpc_classify* call and after the last, named by the kernel that follows it.
 struct LaunchMarks {
@@ -51,7 +50,9 @@ struct LaunchMarks {
   uint8_t kind[kMax];  // LaunchKind of the kernel starting at ev[i] (kLaunchEnd: the closing event)
   int n;
 };
-enum LaunchKind : uint8_t { kLaunchGroup, kLaunchEgress, kLaunchIngress, kLaunchBoth, kLaunchUnpermute, kLaunchKinds, kLaunchEnd };
+enum LaunchKind : uint8_t {
+  kLaunchGroup, kLaunchEgress, kLaunchIngress, kLaunchBoth, kLaunchUnpermute, kLaunchCodes, kLaunchKinds, kLaunchEnd
+};
 inline void launch_mark(LaunchMarks* m, uint8_t kind, hipStream_t s) {
   if (!m || m->n >= LaunchMarks::kMax) return;
   if (hipEventRecord(m->ev[m->n], s) == hipSuccess) m->kind[m->n++] = kind;
@@ -59,8 +60,12 @@ inline void launch_mark(LaunchMarks* m, uint8_t kind, hipStream_t s) {
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
                     LaunchMarks* marks = nullptr);
-// IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base only).
+// IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base or delta
+// epoch): v6_code_kernel maps the addresses to codes in `codes` (v6_code_columns(pk) * n words of
+// device memory, live until the launches have run), then launch_classify runs over the code columns
+// (`group`: sized by group_scratch_bytes of that IPv4-shaped batch).
+uint32_t v6_code_columns(const gpc_pkt_soa& pk);
 int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out,
-                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
+                     unsigned long long* counters, int count, const GroupArgs* group, uint32_t* codes, hipStream_t stream,
                      LaunchMarks* marks = nullptr);
 }

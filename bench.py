@@ -160,7 +160,7 @@ def _pmc_pass(counters, args):
     if not shutil.which("rocprofv3"):
         return None
     d = tempfile.mkdtemp(prefix="gpc_pmc_")
-    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel|group_tiles|unpermute", "-d", d, "-o", "pmc",
+    cmd = ["rocprofv3", "--pmc"] + list(counters) + ["--kernel-include-regex", "classify_kernel|group_tiles|unpermute|v6_code_kernel", "-d", d, "-o", "pmc",
                                                        "--output-format", "csv", "--", sys.executable,
                                                        os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
                                                        "--no-cpu-baseline", "--no-traffic", "--no-parity", "--config",
@@ -177,7 +177,7 @@ def _pmc_pass(counters, args):
                 shutil.copy(f, os.path.join(args.keep_pmc, "pmc_%s_%s.csv" % (args.config, "_".join(counters))))
             with open(f) as fh:
                 rows += [r for r in csv.DictReader(fh)
-                         if re.search(r"classify_kernel|group_tiles|unpermute", r.get("Kernel_Name", ""))]
+                         if re.search(r"classify_kernel|group_tiles|unpermute|v6_code_kernel", r.get("Kernel_Name", ""))]
         # one step = the grouping launch (if grouped) + two classify launches without Services
         # (egress stage, ingress stage) or one with them (+ the un-permute launch of a grouped batch
         # without Services): steps = dispatches of the first classify stage
@@ -221,8 +221,8 @@ KIND_STAGE = {"classify_egress": "1", "classify_ingress": "2", "classify_both": 
 def _pmc_kernel(by_kernel, kind):
     """PMC means per dispatch of one launch kind (pmc_by_kernel keys are kernel names)."""
     for k, cs in by_kernel.items():
-        if kind in ("group_tiles", "unpermute"):
-            if kind in k:
+        if kind in ("group_tiles", "unpermute", "v6_codes"):
+            if {"v6_codes": "v6_code_kernel"}.get(kind, kind) in k:
                 return cs
         else:
             m = re.search(r"classify_kernel<\w+, \w+, (\d)", k)

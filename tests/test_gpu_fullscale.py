@@ -72,13 +72,11 @@ def test_device_vs_oracle_fullscale(config, group):
 
 
 @pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
-def test_device_ipv6_vs_oracle_fullscale_c3(group, monkeypatch):
+def test_device_ipv6_vs_oracle_fullscale_c3(group):
     """gpc_classify6 on full C3 embedded in fd00:10::/96 (IPv6 image, device LPM) equals the C
     oracle's IPv4 verdicts of the same packets (the embedding preserves every match), with the
-    grouping pre-pass off and on (IPv6 key: the 8 ipv6_src bits above the shortest prefix; IPv6
-    grouping is opt-in, GPC_GROUP_V6=1 read at gpc_create)."""
-    if group == 1:
-        monkeypatch.setenv("GPC_GROUP_V6", "1")
+    grouping pre-pass off and on (IPv6 batches are grouped over their code columns: the top byte
+    of the source address's code)."""
     f, wl, cols = _inputs("C3")
     c = _classifier(wl, ipv6=True, rules=workload.to_ipv6(wl).rules, group=group)
     got = c.classify6_host(workload.packets_to_v6(cols), count=True)

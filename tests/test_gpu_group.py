@@ -184,10 +184,9 @@ def test_grouped_many_streams():
 
 
 @pytest.mark.parametrize("n", [1, 16383, 16385, 3 * 16384 + 5])
-def test_grouped_ipv6_equals_plain(n, monkeypatch):
-    """IPv6 batches (gpc_classify6): grouped == plain, verdicts and counters, with ct_*6 columns.
-    IPv6 grouping is opt-in (GPC_GROUP_V6=1, read at gpc_create): measured no faster on C3 in IPv6."""
-    monkeypatch.setenv("GPC_GROUP_V6", "1")
+def test_grouped_ipv6_equals_plain(n):
+    """IPv6 batches (gpc_classify6): grouped == plain, verdicts and counters, with ct_*6 columns
+    (the code launch maps four address columns; grouping runs over the code columns)."""
     wl = workload.config1(seed=9)
     w6 = workload.to_ipv6(wl, dual=True)
     rng = np.random.default_rng(n)

@@ -11,9 +11,9 @@ for l in sys.stdin:
     m = re.search(r"Function Name: (\S+)", l)
     if m:
         name = m.group(1)
-        t = re.search(r"classify_kernelIL(b\d)EL(b\d)ELi(\d)EL(b\d)EL(b\d)E", name)
-        cur = {"kernel": "classify<delta=%s,svc=%s,stage=%s,v6=%s,sort=%s>" % (t.group(1)[1], t.group(2)[1], t.group(3),
-               t.group(4)[1], t.group(5)[1]) if t else re.sub(r"^_ZN3gpc\d+", "", name)[:40]}
+        t = re.search(r"classify_kernelIL(b\d)EL(b\d)ELi(\d)EL(b\d)E", name)
+        cur = {"kernel": "classify<delta=%s,svc=%s,stage=%s,sort=%s>" % (t.group(1)[1], t.group(2)[1], t.group(3),
+               t.group(4)[1]) if t else re.sub(r"^_ZN3gpc\d+", "", name)[:40]}
         rows.append(cur)
         continue
     for key, pat in (("vgpr", r"\sVGPRs: (\d+)"), ("vgpr_spill", r"VGPRs Spill: (\d+)"), ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
