@@ -280,9 +280,10 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 // [0] most significant). Its slots hold only the low kw words of kv (kw = 1, 2 or 4) and the code:
 // the other 4 - kw words are the same for every entry of the length (the tag, kept in the length's
 // descriptor), so an address whose tag differs misses without a load. Rule sets whose prefixes of
-// one length share their upper bits (C3 in fd00:10::/96: every length) get 8-B slots, 8 per 64-B
-// bucket: the table is a quarter of a 32-B-slot table with the length in every slot (C3: 29 MB ->
-// ~5 MB, mostly L2-resident instead of Infinity-Cache traffic). Two choices, both loaded per probe.
+// one length share their upper bits (C3 in fd00:10::/96: every length) get 8-B slots: a bucket of
+// two slots is one 16-B load, so a probe of both choices is two 128-bit loads per lane (the table
+// is a quarter of a 32-B-slot table with the length in every slot: C3 29 MB -> 5 MB, mostly
+// L2-resident instead of Infinity-Cache traffic).
 constexpr uint32_t kV6MaxLens = 64;
 struct V6Len {
   uint32_t meta;     // prefix length | key words kw << 8 | log2(buckets) << 16
@@ -300,9 +301,10 @@ struct V6Lpm {
   uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
   V6Len d[kV6MaxLens];        // d[i]: the table of lens[i]
 };
-// Bucket: 16 words (one 64-B line); slot = key (kw words), code, padding to 2 / 4 / 8 words.
-constexpr uint32_t kV6BucketWords = 16;
+// Bucket: two slots; slot = key (kw words), code, padding to 2 / 4 / 8 words: 16 / 32 / 64-B buckets.
+constexpr uint32_t kV6BucketWords = 16;  // the largest bucket (and the overflow table's)
 GPC_HD uint32_t v6_slot_words(uint32_t kw) { return kw == 4u ? 8u : 2u * kw; }
+GPC_HD uint32_t v6_bucket_words(uint32_t kw) { return 2u * v6_slot_words(kw); }
 // Wide slot of the delta epochs' overflow table (journal): masked address (4 words), len | kV6Valid,
 // code, 2 pad; 2 slots per 64-B bucket, two choices.
 constexpr uint32_t kV6SlotWords = 8, kV6BucketSlots = 2, kV6Valid = 0x100u;
@@ -375,14 +377,14 @@ GPC_HD bool v6_bucket_find(const uint32_t* w, uint32_t kw, const uint32_t* r, ui
   uint32_t c = 0, any = 0;
   if (kw == 1u) {
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
+    for (int s = 0; s < 2; s++) {
       const uint32_t mt = 0u - uint32_t(w[2 * s] == r[3]);
       c |= w[2 * s + 1] & mt;
       any |= mt;
     }
   } else if (kw == 2u) {
 #pragma unroll
-    for (int s = 0; s < 4; s++) {
+    for (int s = 0; s < 2; s++) {
       const uint32_t mt = 0u - uint32_t(w[4 * s] == r[2] && w[4 * s + 1] == r[3]);
       c |= w[4 * s + 2] & mt;
       any |= mt;
@@ -411,20 +413,22 @@ GPC_HD bool v6_wide_find(const uint32_t* w, const uint32_t* m, uint32_t len, uin
   if (any) *code = c;
   return any != 0;
 }
-// 16 words from a 64-B aligned bucket (four 128-bit loads).
-GPC_HD void v6_load_bucket(const uint32_t* p, uint32_t* w) {
+// The first `words` (4, 8 or 16) words of a bucket (128-bit loads; w is 16 words).
+GPC_HD void v6_load_bucket(const uint32_t* p, uint32_t words, uint32_t* w) {
 #if defined(__HIPCC__)
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint4 v = q[j];
-    w[4 * j] = v.x;
-    w[4 * j + 1] = v.y;
-    w[4 * j + 2] = v.z;
-    w[4 * j + 3] = v.w;
+  for (uint32_t j = 0; j < 4; j++) {
+    if (4u * j < words) {
+      const uint4 v = q[j];
+      w[4 * j] = v.x;
+      w[4 * j + 1] = v.y;
+      w[4 * j + 2] = v.z;
+      w[4 * j + 3] = v.w;
+    }
   }
 #else
-  for (uint32_t j = 0; j < kV6BucketWords; j++) w[j] = p[j];
+  for (uint32_t j = 0; j < words; j++) w[j] = p[j];
 #endif
 }
 // code(a_k) for K addresses at once (a[k][0..3], [0] = most significant): the K binary searches run
@@ -465,10 +469,11 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       v6_buckets(d, r[k], &bk[0], &bk[1]);
 #pragma unroll
       for (int c = 0; c < 2; c++) {
-        const uint32_t* b = blob + d.tab_off + size_t(bk[c]) * kV6BucketWords;
+        const uint32_t bw = v6_bucket_words(kw[k]);
+        const uint32_t* b = blob + d.tab_off + size_t(bk[c]) * bw;
         if (probe[k]) {
-          GPC_TOUCH(b, 64);
-          v6_load_bucket(b, w[k][c]);
+          GPC_TOUCH(b, bw * 4);
+          v6_load_bucket(b, bw, w[k][c]);
         }
       }
       if constexpr (kOvf) {
@@ -477,7 +482,7 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
 #pragma unroll
         for (int c = 0; c < 2; c++) {
           const uint32_t* b = ovf + size_t(c ? hash_b2(ok, omask) : hash_b1(ok, omask)) * (kV6SlotWords * kV6BucketSlots);
-          if (live) v6_load_bucket(b, ow[k][c]);
+          if (live) v6_load_bucket(b, kV6BucketWords, ow[k][c]);
         }
       }
     }
@@ -516,8 +521,9 @@ GPC_HD bool v6_base_has(const uint32_t* blob, uint32_t lpm_off, const uint32_t* 
     v6_key(m, len, r);
     if (!v6_probe_needed(d, r)) return false;
     v6_buckets(d, r, &bk[0], &bk[1]);
+    const uint32_t bw = v6_bucket_words(v6_kw(d));
     for (int j = 0; j < 2; j++) {
-      v6_load_bucket(blob + d.tab_off + size_t(bk[j]) * kV6BucketWords, w);
+      v6_load_bucket(blob + d.tab_off + size_t(bk[j]) * bw, bw, w);
       if (v6_bucket_find(w, v6_kw(d), r, &c)) return true;
     }
     return false;

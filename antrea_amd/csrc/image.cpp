@@ -1097,8 +1097,8 @@ static bool v6_hash_build(const std::vector<std::array<uint32_t, 8>>& slots6, do
 
 // The LPM table of one prefix length (core.hpp V6Len): entries (kv = prefix right-aligned, code).
 // Key words kw = the fewest of 1 / 2 / 4 whose complement (the tag) all entries share; the empty-slot
-// key is one no entry has. 2-choice cuckoo placement over 64-B buckets, a larger table when it does
-// not converge. Fills d (except tab_off) and tab.
+// key is one no entry has. 2-choice cuckoo placement over buckets of two slots, a larger table when
+// it does not converge. Fills d (except tab_off) and tab.
 static bool v6_len_table_build(uint32_t len, const std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>& ents,
                                V6Len* d, std::vector<uint32_t>* tab) {
   *d = V6Len{};
@@ -1112,7 +1112,7 @@ static bool v6_len_table_build(uint32_t len, const std::vector<std::pair<std::ar
       break;
     }
   }
-  const uint32_t sw = v6_slot_words(kw), ns = kV6BucketWords / sw;
+  const uint32_t sw = v6_slot_words(kw), ns = 2, bw = v6_bucket_words(kw);
   std::set<std::array<uint32_t, 4>> used;
   for (auto& e : ents) {
     std::array<uint32_t, 4> k = e.first;
@@ -1124,13 +1124,13 @@ static bool v6_len_table_build(uint32_t len, const std::vector<std::pair<std::ar
   while (used.count(empty)) empty[3]--;  // at most |ents| tries
   for (uint32_t w = 0; w < 4; w++) d->pat[w] = w + kw < 4 ? (ents.empty() ? 0u : ents[0].first[w]) : empty[w];
   d->seed = v6_seed(len, kw, d->pat);
-  const double load = kw == 4 ? 0.7 : 0.85;
+  const double load = 0.7;
   uint32_t lg = 0;
   while (double(ns << lg) * load < double(ents.size() + 1)) lg++;
   for (int attempt = 0; attempt < 8; attempt++, lg++) {
     const uint32_t nb = 1u << lg;
     d->meta = len | kw << 8 | lg << 16;
-    tab->assign(size_t(nb) * kV6BucketWords, 0u);
+    tab->assign(size_t(nb) * bw, 0u);
     std::vector<uint8_t> full(size_t(nb) * ns, 0);
     for (size_t s = 0; s < size_t(nb) * ns; s++)
       for (uint32_t w = 0; w < kw; w++) (*tab)[s * sw + w] = empty[4 - kw + w];
