@@ -609,6 +609,31 @@ GPC_HD uint32_t jhead(const uint32_t* pool, const JournalHdr* jh, uint32_t b) {
   return page ? pool[page + (b % kJPageHeads)] : 0u;
 }
 
+// Two consecutive words (a bucket's begin / end offsets) as one 8-B load: dword-aligned multi-dword
+// global loads are legal on gfx950, so the pair costs one vector memory instruction, not two.
+GPC_HD void load_pair(const uint32_t* p, uint32_t* a, uint32_t* b) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  *a = uint32_t(v);
+  *b = uint32_t(v >> 32);
+}
+
+// A rule record's 6 header words (records are 64-B aligned): one 16-B and one 8-B load.
+struct RecHdr {
+  uint32_t w[kRecHdrWords];
+};
+GPC_HD RecHdr load_rec_hdr(const uint32_t* rec) {
+  RecHdr h;
+#if defined(__HIPCC__)
+  const uint4 a = *reinterpret_cast<const uint4*>(rec);
+  const uint2 b = *reinterpret_cast<const uint2*>(rec + 4);
+  h.w[0] = a.x, h.w[1] = a.y, h.w[2] = a.z, h.w[3] = a.w, h.w[4] = b.x, h.w[5] = b.y;
+#else
+  for (uint32_t i = 0; i < kRecHdrWords; i++) h.w[i] = rec[i];
+#endif
+  return h;
+}
+
 // Both buckets are loaded before either is compared (two independent 16-B loads).
 GPC_HD bool hash_contains(const Img& im, uint64_t key) {
   const uint64_t* tab = reinterpret_cast<const uint64_t*>(im.blob + im.hdr->hash_off);
@@ -734,7 +759,9 @@ GPC_HD uint32_t scan_estimate(const Img& im, uint32_t table, const Pkt& p) {
       if (uint32_t(i) >= th.n_idx[k]) break;
       const SubIdx& si = th.idx[k][i];
       const uint32_t* o = im.blob + si.off + bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
-      cnt[k] += o[1] - o[0];
+      uint32_t ob, oe;
+      load_pair(o, &ob, &oe);
+      cnt[k] += oe - ob;
     }
   return cnt[0] < cnt[1] ? cnt[0] : cnt[1];
 }
@@ -825,7 +852,8 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     const uint32_t off = hard[h];
     const uint32_t* rec = im.blob + off;
     GPC_TOUCH(rec, 4 * kRecHdrWords);
-    const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
+    const RecHdr hd = load_rec_hdr(rec);
+    const uint32_t w1 = hd.w[1], w2 = hd.w[2], rid = hd.w[4] >> 8;
     if (rule_dead(im, rid)) continue;
     if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
       if ((w1 & 0xffffu) != hprio) break;
@@ -854,8 +882,10 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
       const uint32_t* o = im.blob + si.off;
       GPC_TOUCH(o + b, 8);
-      lo0[i] = si.ent / 4 + o[b];
-      hi0[i] = si.ent / 4 + o[b + 1];
+      uint32_t ob, oe;
+      load_pair(o + b, &ob, &oe);
+      lo0[i] = si.ent / 4 + ob;
+      hi0[i] = si.ent / 4 + oe;
       cnt0 += hi0[i] - lo0[i];
     }
     if (uint32_t(i) < n1) {
@@ -863,8 +893,10 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
       const uint32_t* o = im.blob + si.off;
       GPC_TOUCH(o + b, 8);
-      lo1[i] = si.ent / 4 + o[b];
-      hi1[i] = si.ent / 4 + o[b + 1];
+      uint32_t ob, oe;
+      load_pair(o + b, &ob, &oe);
+      lo1[i] = si.ent / 4 + ob;
+      hi1[i] = si.ent / 4 + oe;
       cnt1 += hi1[i] - lo1[i];
     }
   }
@@ -906,7 +938,8 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       after = off;
       const uint32_t* rec = im.blob + off;
       GPC_TOUCH(rec, 4 * kRecHdrWords);
-      const uint32_t w1 = rec[1], w2 = rec[2];
+      const RecHdr hd = load_rec_hdr(rec);
+      const uint32_t w1 = hd.w[1], w2 = hd.w[2];
       const uint32_t prio = w1 & 0xffffu;
       if (prio != level) {
         if (have) {  // winning level finished
@@ -917,8 +950,8 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
         level_done = 0;
       }
       GPC_STAT(3, 1);
-      const uint32_t rid = rec[4] >> 8;
-      if (rule_dead(im, rid) || !rule_match(im, rec, w2, d, (rec[5] >> (3 * d)) & 7u, p)) {
+      const uint32_t rid = hd.w[4] >> 8;
+      if (rule_dead(im, rid) || !rule_match(im, rec, w2, d, (hd.w[5] >> (3 * d)) & 7u, p)) {
         GPC_STAT(5, 1);
         continue;
       }
@@ -997,16 +1030,16 @@ GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_bl
   res.prio = 0;
   const bool hf = (q.h & kHFound) != 0, have = (q.s & kSHave) != 0;
   if (have && !(q.s & kSNoAct)) {
-    const uint32_t* rec = ((q.s & kSImg) ? ovl_blob : base_blob) + q.win;
-    const uint32_t w2 = rec[2];
-    if (!(hf && (q.h & 0xffffu) > (rec[1] >> 16))) {  // the soft winner's action flow beats the hard match
+    const RecHdr hd = load_rec_hdr(((q.s & kSImg) ? ovl_blob : base_blob) + q.win);
+    const uint32_t w2 = hd.w[2];
+    if (!(hf && (q.h & 0xffffu) > (hd.w[1] >> 16))) {  // the soft winner's action flow beats the hard match
       res.verdict = uint8_t(rec_verdict(w2));
-      res.conj = rec[0];
-      res.tier = uint8_t(rec[4] & 0xffu);
+      res.conj = hd.w[0];
+      res.tier = uint8_t(hd.w[4] & 0xffu);
       res.counted = uint8_t(rec_counted(w2));
-      res.slot = rec[3];
-      res.pin = (rec[5] & kRecPacketIn) ? uint32_t(GPC_VFLAG_PACKETIN) : 0u;
-      res.prio = rec[1] >> 16;
+      res.slot = hd.w[3];
+      res.pin = (hd.w[5] & kRecPacketIn) ? uint32_t(GPC_VFLAG_PACKETIN) : 0u;
+      res.prio = hd.w[1] >> 16;
       if (q.s & kSTie) res.tie = 1;
       return res;
     }
