@@ -30,7 +30,18 @@
 #define GPC_WAVE_ANY(c) (c)
 #endif
 
+// Image words read at wave-uniform addresses (the hard pseudo-rules of a table: the same records for
+// every lane) go through the constant address space, so the compiler issues scalar loads (K$, the
+// scalar-memory counter) that overlap the lanes' vector loads instead of queueing behind them.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GPC_CONST_AS __attribute__((address_space(4)))
+#else
+#define GPC_CONST_AS
+#endif
+
 namespace gpc {
+
+typedef GPC_CONST_AS uint32_t cword;  // an image word read at a wave-uniform address
 
 // Packet axes (all 32-bit; IPv4 image).
 enum Axis : uint8_t {
@@ -646,7 +657,8 @@ GPC_HD bool hash_contains(const Img& im, uint64_t key) {
   return (k0 == key) | (k1 == key) | (k2 == key) | (k3 == key);
 }
 
-GPC_HD bool ival_hit(const uint32_t* iv, uint32_t n, uint32_t v) {
+template <typename W = uint32_t>
+GPC_HD bool ival_hit(const W* iv, uint32_t n, uint32_t v) {
   if (n <= 8) {
     for (uint32_t i = 0; i < n; i++) {
       GPC_TOUCH(iv + 2 * i, 8);
@@ -665,7 +677,8 @@ GPC_HD bool ival_hit(const uint32_t* iv, uint32_t n, uint32_t v) {
   return lo > 0 && v <= iv[2 * (lo - 1) + 1];
 }
 
-GPC_HD bool pts_hit(const uint32_t* pt, uint32_t n, uint32_t v) {
+template <typename W = uint32_t>
+GPC_HD bool pts_hit(const W* pt, uint32_t n, uint32_t v) {
   if (n <= 16) {
     for (uint32_t i = 0; i < n; i++) {
       GPC_TOUCH(pt + i, 4);
@@ -683,7 +696,8 @@ GPC_HD bool pts_hit(const uint32_t* pt, uint32_t n, uint32_t v) {
   return lo < n && pt[lo] == v;
 }
 
-GPC_HD bool box_hit(const uint32_t* bx, uint32_t n, const Pkt& p) {
+template <typename W = uint32_t>
+GPC_HD bool box_hit(const W* bx, uint32_t n, const Pkt& p) {
   for (uint32_t i = 0; i < n; i++, bx += kBoxWords) {
     GPC_TOUCH(bx, kBoxWords * 4);
     const uint32_t meta = bx[6];
@@ -695,11 +709,14 @@ GPC_HD bool box_hit(const uint32_t* bx, uint32_t n, const Pkt& p) {
   return false;
 }
 
-// One clause of the record at word offset `roff` (OR of its segments).
-GPC_HD bool clause_match(const Img& im, uint32_t roff, const uint32_t* c, const Pkt& p) {
+// One clause of the record at word offset `roff` (OR of its segments). W: uint32_t, or cword when
+// the record is read at a wave-uniform address (hard pseudo-rules).
+template <typename W = uint32_t>
+GPC_HD bool clause_match(const Img& im, uint32_t roff, const W* c, const Pkt& p) {
+  const W* blob = (const W*)im.blob;
   GPC_TOUCH(c, 4);
   const uint32_t nseg = c[0];
-  const uint32_t* w = c + 1;
+  const W* w = c + 1;
   for (uint32_t s = 0; s < nseg; s++) {
     GPC_TOUCH(w, 4);
     const uint32_t tag = *w++;
@@ -711,9 +728,9 @@ GPC_HD bool clause_match(const Img& im, uint32_t roff, const uint32_t* c, const 
       case SK_PTS: hit = pts_hit(w, n, p.ax[axis]); w += n; break;
       case SK_HASH: hit = hash_contains(im, point_key(roff, axis, p.ax[axis])); break;
       case SK_BOX: hit = box_hit(w, n, p); w += kBoxWords * n; break;
-      case SK_XIVAL: GPC_TOUCH(w, 4); hit = ival_hit(im.blob + *w, n, p.ax[axis]); w++; break;
-      case SK_XPTS: GPC_TOUCH(w, 4); hit = pts_hit(im.blob + *w, n, p.ax[axis]); w++; break;
-      case SK_XBOX: GPC_TOUCH(w, 4); hit = box_hit(im.blob + *w, n, p); w++; break;
+      case SK_XIVAL: GPC_TOUCH(w, 4); hit = ival_hit(blob + *w, n, p.ax[axis]); w++; break;
+      case SK_XPTS: GPC_TOUCH(w, 4); hit = pts_hit(blob + *w, n, p.ax[axis]); w++; break;
+      case SK_XBOX: GPC_TOUCH(w, 4); hit = box_hit(blob + *w, n, p); w++; break;
       default: hit = false; break;
     }
     if (hit) return true;
@@ -724,8 +741,9 @@ GPC_HD bool clause_match(const Img& im, uint32_t roff, const uint32_t* c, const 
 // All clauses of a record; clause `last` (the driver, already a likely hit) is checked last
 // (last >= n_clauses: natural order). One clause_match call site keeps the code small.
 // `skip`: clauses already decided (the entry's exact interval test).
-GPC_HD bool rule_match(const Img& im, const uint32_t* rec, uint32_t w2, uint32_t last, uint32_t skip, const Pkt& p) {
-  const uint32_t roff = uint32_t(rec - im.blob);
+template <typename W = uint32_t>
+GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, uint32_t last, uint32_t skip, const Pkt& p) {
+  const uint32_t roff = uint32_t(rec - (const W*)im.blob);
   const uint32_t ncl = rec_nclauses(w2);
   const uint32_t first = last < ncl ? last + 1 : 0;
   for (uint32_t j = 0; j < ncl; j++) {
@@ -844,16 +862,17 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   res.h = res.s = res.win = 0;
   uint32_t htie = 0, noact = 0;
   // --- hard pseudo-rules (few): best hard match H
+  // (wave-uniform: the list, the records and their clause data are read with scalar loads)
   uint32_t rH = th.end_off;
   uint32_t hprio = 0, hverdict = RV_MISS;
-  const uint32_t* hard = im.blob + th.hard_off;
+  const cword* cblob = (const cword*)im.blob;
+  const cword* hard = cblob + th.hard_off;
   for (uint32_t h = 0; h < th.n_hard; h++) {
     GPC_TOUCH(&hard[h], 4);
     const uint32_t off = hard[h];
-    const uint32_t* rec = im.blob + off;
+    const cword* rec = cblob + off;
     GPC_TOUCH(rec, 4 * kRecHdrWords);
-    const RecHdr hd = load_rec_hdr(rec);
-    const uint32_t w1 = hd.w[1], w2 = hd.w[2], rid = hd.w[4] >> 8;
+    const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
     if (rule_dead(im, rid)) continue;
     if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
       if ((w1 & 0xffffu) != hprio) break;

@@ -2,6 +2,8 @@
 # One GPU session on the gpurun box (run from the repo root):
 #   tools/gpu_session.sh TAG [STEPS...]
 # STEPS (default "tests smoke bench kt"):
+#   build   python -m antrea_amd.build --force on the box (every object recompiled from source there;
+#           the later steps then load the box-built library)
 #   tests   pytest -m gpu (one process, per-test timeout)
 #   smoke   __graft_entry__.smoke()
 #   bench   python bench.py (default C3 line: PMC passes, parity stamp, CPU baseline)
@@ -28,6 +30,10 @@ pmc() {  # name, config, counters...
 }
 for s in $STEPS; do
   case $s in
+    build)
+      step build
+      timeout -k 10 900 python -u -m antrea_amd.build --force > "$O/build.log" 2>&1 || { tail -20 "$O/build.log"; exit 1; }
+      tail -1 "$O/build.log"; sha256sum antrea_amd/_build/libgpc.so >> "$O/build.log" ;;
     tests)
       step tests
       timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --durations=30 --timeout 400 --timeout-method thread \
