@@ -280,6 +280,19 @@ static void lane_sort_tables(const HostImage& h, uint8_t* sort_table) {
     if (!bt) continue;
     const TableHdr& th = h.hdr.t[bt - 1];
     double mean[2];
+    if (th.n_cidx) {  // the composite driver is the one scanned: its lists decide
+      double s1 = th.always_n[th.cband], s2 = s1 * s1;
+      for (uint32_t i = 0; i < th.n_cidx; i++) {
+        const SubIdx& si = th.cidx[i];
+        const uint32_t* o = h.blob.data() + si.off;
+        for (uint64_t b = 0; b < (1ull << si.bits); b++) {
+          const double len = double(o[b + 1] - o[b]);
+          s1 += len;
+          s2 += len * len;
+        }
+      }
+      mean[0] = mean[1] = s1 > 0 ? s2 / s1 : 1e30;
+    } else {
     for (int k = 0; k < 2; k++) {
       double s1 = th.always_n[k], s2 = double(th.always_n[k]) * th.always_n[k];
       for (uint32_t i = 0; i < th.n_idx[k]; i++) {
@@ -293,6 +306,7 @@ static void lane_sort_tables(const HostImage& h, uint8_t* sort_table) {
       }
       mean[k] = s1 > 0 ? s2 / s1 : 1e30;
     }
+    }
     const char* force = std::getenv("GPC_LANE_SORT");  // experiments: "1" forces regrouping on, "0" off
     if (force ? force[0] == '1' : std::min(mean[0], mean[1]) >= kLaneSortMinList) sort_table[st] = uint8_t(bt);
     if (std::getenv("GPC_IMAGE_DEBUG"))
@@ -305,9 +319,11 @@ static void lane_sort_tables(const HostImage& h, uint8_t* sort_table) {
 // (classify.hip scan_key) needs.
 static uint32_t group_axes(const HostImage& h) {
   uint32_t m = 0;
-  for (const TableHdr& th : h.hdr.t)
+  for (const TableHdr& th : h.hdr.t) {
     for (int k = 0; k < 2; k++)
       for (uint32_t i = 0; i < th.n_idx[k] && i < uint32_t(kIdxPerClause); i++) m |= 1u << th.idx[k][i].axis;
+    for (uint32_t i = 0; i < th.n_cidx && i < uint32_t(kIdxPerClause); i++) m |= 1u << th.cidx[i].axis | 1u << th.cx;
+  }
   return m;
 }
 

@@ -123,6 +123,17 @@ struct TableHdr {
   uint32_t always_off[2], always_n[2];
   uint32_t n_idx[2];
   SubIdx idx[2][kIdxPerClause];
+  // Composite driver (image.cpp build_composite): when every soft rule's clause 1 - cband is a small
+  // set of exact values on one axis cx (AppliedTo ofports, Pod IPs), the driver lists of clause cband
+  // are also kept keyed by (band key, exact value): sub-index i lists the rules whose clause cband
+  // covers the packet's band key AND whose clause 1 - cband holds its cx value. A packet then scans
+  // only those (plus clause cband's always list) -- a subset of either plain driver's candidates
+  // (up to hash collisions). n_cidx = 0: none.
+  uint32_t n_cidx;
+  uint8_t cband, cx, pad[2];
+  uint32_t xmap_off;  // 2^16-bit map of the cx values any soft rule holds (cx_bit): a packet whose
+                      // value is absent has no soft candidate at all (one load, L2-resident)
+  SubIdx cidx[kIdxPerClause];
 };
 
 struct ImageHdr {
@@ -233,6 +244,13 @@ GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t bits, uint32_t 
   }
   if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
   return v & ((1u << bits) - 1u);
+}
+// Bit of exact value x in a composite table's value map (TableHdr xmap_off, 2^16 bits).
+GPC_HD uint32_t cx_bit(uint32_t x) { return mix32(x ^ 0x2545f491u) >> 16; }
+// Composite driver bucket (TableHdr cidx): IP band key of v on (axis, band) with the exact value x.
+GPC_HD uint32_t cbucket_of(uint32_t band, uint32_t bits, uint32_t v, uint32_t x) {
+  const uint32_t key = v >> ip_band_shift(band);
+  return mix32((key * 0x9e3779b1u) ^ mix32(x ^ (band << 28) ^ 0x5bd1e995u)) >> (32 - bits);
 }
 // Point-hash key of value v on `axis` of the record at word offset `off` (16-word aligned, < 2^28):
 // (off / 16) << 4 | axis in the high word. ~0 (empty slot) is never a key.
@@ -769,6 +787,18 @@ GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
 // it): the kernel can group lanes of similar length into the same wavefront (classify.hip).
 GPC_HD uint32_t scan_estimate(const Img& im, uint32_t table, const Pkt& p) {
   const TableHdr& th = im.hdr->t[table - 1];
+  if (th.n_cidx) {  // the composite driver is always taken (eval_part)
+    const uint32_t xb = cx_bit(p.ax[th.cx]);
+    if (!((im.blob[th.xmap_off + (xb >> 5)] >> (xb & 31u)) & 1u)) return 0;
+    uint32_t c = th.always_n[th.cband];
+    for (uint32_t i = 0; i < th.n_cidx && i < uint32_t(kIdxPerClause); i++) {
+      const SubIdx& si = th.cidx[i];
+      uint32_t ob, oe;
+      load_pair(im.blob + si.off + cbucket_of(si.band, si.bits, p.ax[si.axis], p.ax[th.cx]), &ob, &oe);
+      c += oe - ob;
+    }
+    return c;
+  }
   uint32_t cnt[2] = {th.always_n[0], th.always_n[1]};
 #pragma unroll
   for (int k = 0; k < 2; k++)
@@ -886,51 +916,84 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     }
   }
   const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
-  if (n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
+  if (th.n_cidx == 0 && n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
     if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
     return res;
   }
-  // --- driver clause: the one with fewer candidate records
+  // --- driver clause: the composite driver when the table has one (a subset of either plain
+  // driver's candidates, table-uniform branch), else the clause with fewer candidate records
   uint32_t lo0[kIdxPerClause], hi0[kIdxPerClause], lo1[kIdxPerClause], hi1[kIdxPerClause];
-  uint32_t cnt0 = th.always_n[0], cnt1 = th.always_n[1];
+  const uint32_t nc = th.n_cidx;
+  bool d1 = false;
+  uint32_t d = 0;
+  uint32_t always_n = 0;  // entries of the driver's always list to scan
+  if (nc) {
+    d = th.cband;
+    const uint32_t xv = p.ax[th.cx];
+    const uint32_t xb = cx_bit(xv);
+    GPC_TOUCH(im.blob + th.xmap_off + (xb >> 5), 4);
+    const bool xin = (im.blob[th.xmap_off + (xb >> 5)] >> (xb & 31u)) & 1u;  // else no soft rule can match
+    always_n = xin ? th.always_n[d] : 0u;
+    uint32_t cnt = always_n;
 #pragma unroll
-  for (int i = 0; i < kIdxPerClause; i++) {
-    lo0[i] = hi0[i] = lo1[i] = hi1[i] = 0;
-    if (uint32_t(i) < n0) {
-      const SubIdx& si = th.idx[0][i];
-      const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
-      const uint32_t* o = im.blob + si.off;
-      GPC_TOUCH(o + b, 8);
-      uint32_t ob, oe;
-      load_pair(o + b, &ob, &oe);
-      lo0[i] = si.ent / 4 + ob;
-      hi0[i] = si.ent / 4 + oe;
-      cnt0 += hi0[i] - lo0[i];
+    for (int i = 0; i < kIdxPerClause; i++) {
+      lo0[i] = hi0[i] = lo1[i] = hi1[i] = 0;
+      if (uint32_t(i) < nc && xin) {
+        const SubIdx& si = th.cidx[i];
+        const uint32_t b = cbucket_of(si.band, si.bits, p.ax[si.axis], xv);
+        const uint32_t* o = im.blob + si.off;
+        GPC_TOUCH(o + b, 8);
+        uint32_t ob, oe;
+        load_pair(o + b, &ob, &oe);
+        lo0[i] = si.ent / 4 + ob;
+        hi0[i] = si.ent / 4 + oe;
+        cnt += hi0[i] - lo0[i];
+      }
     }
-    if (uint32_t(i) < n1) {
-      const SubIdx& si = th.idx[1][i];
-      const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
-      const uint32_t* o = im.blob + si.off;
-      GPC_TOUCH(o + b, 8);
-      uint32_t ob, oe;
-      load_pair(o + b, &ob, &oe);
-      lo1[i] = si.ent / 4 + ob;
-      hi1[i] = si.ent / 4 + oe;
-      cnt1 += hi1[i] - lo1[i];
+    GPC_STAT(0, 1);
+    GPC_STAT(1, cnt);
+  } else {
+    uint32_t cnt0 = th.always_n[0], cnt1 = th.always_n[1];
+#pragma unroll
+    for (int i = 0; i < kIdxPerClause; i++) {
+      lo0[i] = hi0[i] = lo1[i] = hi1[i] = 0;
+      if (uint32_t(i) < n0) {
+        const SubIdx& si = th.idx[0][i];
+        const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
+        const uint32_t* o = im.blob + si.off;
+        GPC_TOUCH(o + b, 8);
+        uint32_t ob, oe;
+        load_pair(o + b, &ob, &oe);
+        lo0[i] = si.ent / 4 + ob;
+        hi0[i] = si.ent / 4 + oe;
+        cnt0 += hi0[i] - lo0[i];
+      }
+      if (uint32_t(i) < n1) {
+        const SubIdx& si = th.idx[1][i];
+        const uint32_t b = bucket_of(si.axis, si.band, si.bits, p.ax[si.axis]);
+        const uint32_t* o = im.blob + si.off;
+        GPC_TOUCH(o + b, 8);
+        uint32_t ob, oe;
+        load_pair(o + b, &ob, &oe);
+        lo1[i] = si.ent / 4 + ob;
+        hi1[i] = si.ent / 4 + oe;
+        cnt1 += hi1[i] - lo1[i];
+      }
     }
+    d1 = cnt1 < cnt0;
+    d = d1 ? 1u : 0u;
+    always_n = th.always_n[d];
+    GPC_STAT(0, 1);
+    GPC_STAT(1, d1 ? cnt1 : cnt0);
+    GPC_STAT(2, d1 ? cnt0 : cnt1);
   }
-  const bool d1 = cnt1 < cnt0;
-  const uint32_t d = d1 ? 1u : 0u;
-  GPC_STAT(0, 1);
-  GPC_STAT(1, d1 ? cnt1 : cnt0);
-  GPC_STAT(2, d1 ? cnt0 : cnt1);
   // Candidate scan. The driver lists (0 = always list, 1.. = sub-index buckets) are walked as one
   // flattened sequence (scan_lists), keeping the two best-ranked prefilter survivors. They are then
   // verified in rank order; if more candidates passed and no decision was reached, the lists are
   // rescanned above the last verified offset. Same result as a k-way merge in rank order.
   uint32_t dl[kLists], upto[kLists];  // entry index offset per list; cumulative end in the flattened scan
   dl[0] = th.always_off[d] / 4;
-  upto[0] = th.always_n[d];
+  upto[0] = always_n;
 #pragma unroll
   for (int i = 0; i < kIdxPerClause; i++) {
     const uint32_t lo = d1 ? lo1[i] : lo0[i], hi = d1 ? hi1[i] : hi0[i];
@@ -938,7 +1001,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     upto[i + 1] = upto[i] + (hi - lo);
   }
   const uint32_t total = upto[kLists - 1];
-  const bool one_idx = n0 <= 1 && n1 <= 1;  // table-uniform: every driver clause has <= 1 sub-index
+  const bool one_idx = nc ? nc <= 1 : n0 <= 1 && n1 <= 1;  // table-uniform: every driver list set has <= 1 sub-index
   uint32_t after = 0;       // rescan bound (exclusive); record offsets are > 0
   int have = 0;             // result found
   uint32_t level = 0xffffffffu;

@@ -867,6 +867,113 @@ bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vect
   return false;
 }
 
+// Composite driver (core.hpp TableHdr cidx): built when every soft rule of the table has, in clause
+// 1 - cb, at most kCompositeMaxValues exact values on one common axis (AppliedTo ofports, Pod IPs)
+// and, in clause cb, only IP atoms the driver index can key. Each rule is listed under (band key,
+// value) for every band key its clause-cb atoms cover and every value of its other clause, with the
+// same entry (prefilter) as clause cb's plain index. GPC_COMPOSITE=0 / 1 turns it off / on.
+constexpr size_t kCompositeMaxValues = 16;
+constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 26;
+void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>& rec_off, const uint64_t* span, int t,
+                     TableHdr& th, Blob& B, HostImage* out) {
+  th.n_cidx = 0;
+  th.cband = th.cx = 0;
+  th.xmap_off = 0;
+  const char* on = std::getenv("GPC_COMPOSITE");  // GPC_COMPOSITE=0 / 1 (read at every build)
+  if (!on || on[0] != '1') return;
+  struct CE {
+    AtomKey key;
+    uint32_t xi;  // index of the rule's value list in xsets
+    std::array<uint32_t, 4> ent;
+  };
+  for (int cb = 0; cb < 2; cb++) {
+    const int ce = 1 - cb;
+    int X = -1;
+    bool ok = true;
+    size_t nsoft = 0;
+    std::vector<std::vector<uint32_t>> xsets;
+    std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>> sub;
+    for (size_t rank = 0; rank < rs.size() && ok; rank++) {
+      const RuleB& r = *rs[rank];
+      if (r.hard) continue;
+      nsoft++;
+      if (r.n < 2 || r.clause[ce].empty() || r.clause[ce].size() > kCompositeMaxValues) {
+        ok = false;
+        break;
+      }
+      std::vector<uint32_t> xs;
+      for (auto& a : r.clause[ce]) {
+        if (a.t.size() != 1 || a.t[0].mask != 0xffffffffu || a.t[0].axis > AX_TUN || (X >= 0 && a.t[0].axis != X)) {
+          ok = false;
+          break;
+        }
+        X = a.t[0].axis;
+        xs.push_back(a.t[0].val);
+      }
+      if (!ok) break;
+      std::sort(xs.begin(), xs.end());
+      xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+      const std::array<uint32_t, 4> ent = entry_of(r, cb, rec_off[rank], span);
+      for (auto& a : r.clause[cb]) {
+        AtomKey key;
+        if (!atom_key(a, &key) || key.axis > AX_CTDST) {
+          ok = false;
+          break;
+        }
+        sub[{key.axis, key.band}].push_back({key, uint32_t(xsets.size()), ent});
+      }
+      xsets.push_back(std::move(xs));
+    }
+    if (!ok || nsoft == 0 || X < 0 || sub.size() > size_t(kIdxPerClause)) continue;
+    uint64_t total = 0;
+    for (auto& kv : sub)
+      for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size();
+    if (total > kCompositeMaxEntries) continue;
+    std::vector<std::pair<uint32_t, std::array<uint32_t, 4>>> be;
+    const char* xe = std::getenv("GPC_COMPOSITE_EXTRA_BITS");  // experiments: 2^extra buckets per entry
+    const uint32_t extra = xe ? uint32_t(std::min(3, std::max(0, std::atoi(xe)))) : 0u;
+    for (auto& kv : sub) {
+      const uint8_t axis = kv.first.first, band = kv.first.second;
+      uint64_t n = 0;
+      for (auto& e : kv.second) n += atom_span(e.key) * xsets[e.xi].size();
+      uint32_t bits = 10;
+      while (bits < 22 && (1ull << bits) < n) bits++;
+      bits = std::min(24u, bits + extra);
+      const uint32_t sh = ip_band_shift(band);
+      be.clear();
+      for (auto& e : kv.second)
+        for (uint64_t k = e.key.lo >> sh; k <= (e.key.hi >> sh); k++)
+          for (uint32_t x : xsets[e.xi]) be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), e.ent});
+      std::sort(be.begin(), be.end());
+      be.erase(std::unique(be.begin(), be.end()), be.end());
+      const uint32_t nb = 1u << bits;
+      std::vector<uint32_t> offs(size_t(nb) + 1, 0), ents;
+      ents.reserve(4 * be.size());
+      for (auto& e : be) offs[e.first + 1]++;
+      for (uint32_t b = 0; b < nb; b++) offs[b + 1] += offs[b];
+      for (auto& e : be) ents.insert(ents.end(), e.second.begin(), e.second.end());
+      SubIdx& si = th.cidx[th.n_cidx++];
+      si.axis = axis;
+      si.band = band;
+      si.bits = uint8_t(bits);
+      si.off = B.put(offs.data(), offs.size(), 16);
+      si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
+      out->bytes_bucket_offsets += 4ull * offs.size();
+      out->bytes_entries += 4ull * ents.size();
+      if (std::getenv("GPC_IMAGE_DEBUG"))
+        std::fprintf(stderr, "table %d composite clause %d x axis %d: axis %u band %u bits %u entries %zu\n", t, cb, X, axis,
+                     band, bits, be.size());
+    }
+    std::vector<uint32_t> xmap(1u << 11, 0u);  // 2^16 bits
+    for (auto& xs : xsets)
+      for (uint32_t x : xs) xmap[cx_bit(x) >> 5] |= 1u << (cx_bit(x) & 31u);
+    th.xmap_off = B.put(xmap.data(), xmap.size(), 16);
+    th.cband = uint8_t(cb);
+    th.cx = uint8_t(X);
+    return;
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -1759,6 +1866,10 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
     th.n_hard = uint32_t(hard_offs.size());
     th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
     T_.lap(1);
+    // composite driver first: a table that has one never scans the plain sub-indexes, so they are
+    // not emitted (only the always lists, which the composite driver scans too)
+    build_composite(rs, rec_off, span, t, th, B, out);
+    const bool composite = th.n_cidx != 0;
     // driver indexes for clauses 0 and 1 of the soft rules; entries carry the non-driver filter
     for (int k = 0; k < 2; k++) {
       std::vector<std::array<uint32_t, 4>> always;
@@ -1796,6 +1907,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         sub.erase(h);
       }
       std::vector<std::pair<size_t, std::pair<uint8_t, uint8_t>>> order;
+      if (composite) sub.clear();  // keyed atoms are all in the composite sub-indexes
       for (auto& kv : sub) order.push_back({kv.second.size(), kv.first});
       std::sort(order.rbegin(), order.rend());
       th.n_idx[k] = 0;

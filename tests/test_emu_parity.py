@@ -58,7 +58,9 @@ def _cmp(got, want, cols):
 
 @pytest.mark.parametrize("name", sorted(WORKLOADS))
 @pytest.mark.parametrize("seed", [1, 2])
-def test_emu_vs_oracle(name, seed):
+@pytest.mark.parametrize("composite", ["0", "1"])
+def test_emu_vs_oracle(name, seed, composite, monkeypatch):
+    monkeypatch.setenv("GPC_COMPOSITE", composite)
     wl = WORKLOADS[name](seed)
     n = 400
     cols = workload.gen_packets(wl, n, seed=seed)

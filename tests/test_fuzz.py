@@ -102,6 +102,26 @@ def test_random_rule_sets_product_equals_oracle(rules, cols):
     _cmp(a, b, cols)
 
 
+@settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")) // 2, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(rules=rule_set(), cols=packets())
+def test_random_rule_sets_composite_driver(rules, cols):
+    """The same property with composite driver indexes (GPC_COMPOSITE=1: tables whose rules all
+    hold a few exact AppliedTo values get the (band key, value) index, core.hpp TableHdr cidx)."""
+    import os
+    old = os.environ.get("GPC_COMPOSITE")
+    os.environ["GPC_COMPOSITE"] = "1"
+    try:
+        got, _ = product_verdicts(rules, cols)
+    finally:
+        if old is None:
+            del os.environ["GPC_COMPOSITE"]
+        else:
+            os.environ["GPC_COMPOSITE"] = old
+    want, _ = oracle_verdicts(rules, cols, len(cols["src"]))
+    _cmp(got, want, cols)
+
+
 @st.composite
 def churn(draw):
     """A rule set, then 1-8 control-plane operations on it (the agent's churn path, network_policy.go
@@ -144,6 +164,28 @@ def test_random_churn_product_equals_oracle(case, cols):
     """Random churn in lock step: after every operation the realized flows are identical, and at the
     end the product's committed image (base + journal delta epochs, host emulation of the kernel
     body) gives the Python oracle's verdicts."""
+    _churn_body(case, cols)
+
+
+@settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")) // 2, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(case=churn(), cols=packets())
+def test_random_churn_composite_driver(case, cols):
+    """The churn property over base images with composite driver indexes (GPC_COMPOSITE=1; delta
+    epochs, tombstones and compaction on top of them)."""
+    import os
+    old = os.environ.get("GPC_COMPOSITE")
+    os.environ["GPC_COMPOSITE"] = "1"
+    try:
+        _churn_body(case, cols)
+    finally:
+        if old is None:
+            del os.environ["GPC_COMPOSITE"]
+        else:
+            os.environ["GPC_COMPOSITE"] = old
+
+
+def _churn_body(case, cols):
     from oracle import compiler as oc
     from oracle import ovs_cls
     from tests import emu

@@ -70,7 +70,9 @@ def test_grouped_equals_plain_ragged(n, key):
 
 
 def test_grouped_equals_plain_optional_columns_c3():
-    wl = workload.config3()
+    """C3's rule shapes at a fifth of its size (20k rules: the builds dominate the test time; the
+    full-size grouped path is checked against the oracle in test_gpu_fullscale.py)."""
+    wl = workload.config3(n_policies_per_dir=100)
     rng = np.random.default_rng(12)
     n = 150_000
     cols = _optional_columns(workload.gen_packets(wl, n, seed=12), rng)
@@ -113,9 +115,10 @@ def test_grouped_equals_plain_services_lb():
 
 def test_grouped_device_stream_batch():
     """Device-pointer path on a torch stream with an auto-grouped batch (>= 2^18 packets) equals an
-    ungrouped one (the bench's configuration at a smaller size)."""
+    ungrouped one (the bench's configuration at a smaller size: 20k C3-shaped rules, an image above
+    the auto-grouping threshold)."""
     import torch
-    wl = workload.config3()
+    wl = workload.config3(n_policies_per_dir=100)
     n = 1 << 19
     cols = workload.gen_packets_torch(wl, n, device="cuda")
     outs = []
