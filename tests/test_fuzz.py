@@ -105,12 +105,13 @@ def test_random_rule_sets_product_equals_oracle(rules, cols):
 @settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")) // 2, deadline=None,
           suppress_health_check=[HealthCheck.too_slow])
 @given(rules=rule_set(), cols=packets())
-def test_random_rule_sets_composite_driver(rules, cols):
-    """The same property with composite driver indexes (GPC_COMPOSITE=1: tables whose rules all
-    hold a few exact AppliedTo values get the (band key, value) index, core.hpp TableHdr cidx)."""
+def test_random_rule_sets_plain_driver(rules, cols):
+    """The same property without composite driver indexes (GPC_COMPOSITE=0: every table keeps the
+    plain per-clause driver index; by default tables whose rules all hold a few exact AppliedTo
+    values get the (band key, value) index of core.hpp TableHdr cidx)."""
     import os
     old = os.environ.get("GPC_COMPOSITE")
-    os.environ["GPC_COMPOSITE"] = "1"
+    os.environ["GPC_COMPOSITE"] = "0"
     try:
         got, _ = product_verdicts(rules, cols)
     finally:
@@ -170,12 +171,12 @@ def test_random_churn_product_equals_oracle(case, cols):
 @settings(max_examples=int(__import__("os").environ.get("GPC_FUZZ_EXAMPLES", "100")) // 2, deadline=None,
           suppress_health_check=[HealthCheck.too_slow])
 @given(case=churn(), cols=packets())
-def test_random_churn_composite_driver(case, cols):
-    """The churn property over base images with composite driver indexes (GPC_COMPOSITE=1; delta
-    epochs, tombstones and compaction on top of them)."""
+def test_random_churn_plain_driver(case, cols):
+    """The churn property over base images without composite driver indexes (GPC_COMPOSITE=0;
+    the default property runs over composite bases: delta epochs, tombstones, compaction)."""
     import os
     old = os.environ.get("GPC_COMPOSITE")
-    os.environ["GPC_COMPOSITE"] = "1"
+    os.environ["GPC_COMPOSITE"] = "0"
     try:
         _churn_body(case, cols)
     finally:

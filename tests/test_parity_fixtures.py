@@ -29,8 +29,8 @@ def test_fixture_inputs_stable(config):
 
 @pytest.mark.parametrize("config,composite", [("C2", "0"), ("C3", "0"), ("C3x", "0"), ("C2", "1"), ("C3", "1")])
 def test_emu_vs_oracle_fixture(config, composite, monkeypatch):
-    """composite "1": the image carries composite driver indexes (GPC_COMPOSITE, core.hpp
-    TableHdr cidx) -- C2 and C3 qualify in both directions."""
+    """composite "1" (the default): the image carries composite driver indexes (core.hpp TableHdr
+    cidx; C2 and C3 qualify in both directions), "0": the plain per-clause driver indexes only."""
     monkeypatch.setenv("GPC_COMPOSITE", composite)
     f = fx.load(config)
     wl, cols = fx.packets(config)
