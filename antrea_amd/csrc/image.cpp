@@ -1989,6 +1989,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
   T_.lap(3);
   T_.report("emit");
   B.align(16);
+  for (int i = 0; i < 16; i++) B.w.push_back(0);  // core.hpp rule_match reads 4 words per clause
   out->blob = std::move(B.w);
   return GPC_OK;
 }
