@@ -756,24 +756,11 @@ GPC_HD bool clause_match(const Img& im, uint32_t roff, const W* c, const Pkt& p)
   return false;
 }
 
-// A clause decided from its first four words alone (one segment whose data is inline in them:
-// an ALWAYS, a one-interval or a one/two-point segment): 1 = hit, 0 = miss, -1 = read the clause.
-GPC_HD int clause_fast(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, const Pkt& p) {
-  if (w0 != 1u) return -1;  // nseg
-  const uint32_t kind = w1 & 0xfu, axis = (w1 >> 4) & 0xfu, n = w1 >> 8;
-  if (kind == SK_ALWAYS) return 1;
-  if (axis >= AX_N) return -1;
-  const uint32_t v = p.ax[axis];
-  if (kind == SK_IVAL && n == 1) return (v >= w2 && v <= w3) ? 1 : 0;
-  if (kind == SK_PTS && (n == 1 || n == 2)) return (v == w2 || (n == 2 && v == w3)) ? 1 : 0;
-  return -1;
-}
-
 // All clauses of a record; clause `last` (the driver, already a likely hit) is checked last
-// (last >= n_clauses: natural order). `skip`: clauses already decided (the entry's exact interval
-// test). A clause's first four words are loaded together (one round; clauses are inline and a few
-// words long, and records are followed by more image data, so the reads stay in the blob): most
-// clauses are then decided without the nseg -> tag -> data chain of dependent loads.
+// (last >= n_clauses: natural order). One clause_match call site keeps the code small.
+// `skip`: clauses already decided (the entry's exact interval test). (Loading every clause's first
+// four words in one round and deciding one-segment clauses from them measured slower on MI355X:
+// C2 10.22 -> 10.80 ms, C3 10.12 -> 10.24, profiles/r03k_clause_fast.txt.)
 template <typename W = uint32_t>
 GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, uint32_t last, uint32_t skip, const Pkt& p) {
   const uint32_t roff = uint32_t(rec - (const W*)im.blob);
@@ -783,11 +770,7 @@ GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, uint32_t last, 
     uint32_t k = first + j;
     if (k >= ncl) k -= ncl;
     if ((skip >> k) & 1u) continue;
-    const W* c = rec + rec_off(w2, k);
-    GPC_TOUCH(c, 16);
-    const int f = clause_fast(c[0], c[1], c[2], c[3], p);
-    if (f == 0) return false;
-    if (f < 0 && !clause_match(im, roff, c, p)) return false;
+    if (!clause_match(im, roff, rec + rec_off(w2, k), p)) return false;
   }
   return true;
 }
