@@ -189,6 +189,10 @@ struct gpc_ctx {
   uint32_t group_unpermute = env_u32("GPC_GROUP_UNPERMUTE", 1, 0, 1);
   // IPv6 batches are grouped like IPv4 ones, over their code columns (GPC_GROUP_V6=0: never)
   uint32_t group_v6 = env_u32("GPC_GROUP_V6", 1, 0, 1);
+  // Service batches as two launches with the rewritten fields parked in between (GPC_SVC_SPLIT=1).
+  // Off by default: measured slower than one launch doing the Service stage and both policy stages
+  // (C4, 64M packets: 9.61 vs 9.10 ms; 12.24 vs 11.37 before the two-slot Service hash)
+  uint32_t svc_split = env_u32("GPC_SVC_SPLIT", 0, 0, 1);
   void* stage = nullptr;                 // pinned staging buffer of journal uploads
   size_t stage_bytes = 0;
   std::vector<uint32_t> released_slots;
@@ -1075,11 +1079,22 @@ int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n
   // streams never share one and the data path does no allocation once warm
   GroupArgs ga{nullptr, group_key(ctx), D.cur.base->axes, ctx->group_src_bits, ctx->group_xcd, ctx->group_unpermute,
                D.cur.svc && lb_out && ctx->group_unpermute};
-  if (group_batch(ctx, n, D.cur.base->bytes))
-    if (const int e = group_scratch_for(ctx, D, st, group_scratch_bytes(*pk, n, ga.lb), &ga.scratch)) return e;
+  // Service batches: 16 B per packet to park the fields the Service stage rewrites between the
+  // egress and the ingress launch (classify.hip launch); without it (no memory) one launch does both
+  const size_t park_bytes = D.cur.svc && n && ctx->svc_split ? (16 * n + 255) & ~size_t(255) : 0;
+  uint8_t* scratch = nullptr;
+  if (group_batch(ctx, n, D.cur.base->bytes)) {
+    if (const int e = group_scratch_for(ctx, D, st, park_bytes + group_scratch_bytes(*pk, n, ga.lb), &scratch)) return e;
+    if (scratch) ga.scratch = scratch + park_bytes;
+  }
+  if (park_bytes && !scratch && group_scratch(D, st, park_bytes, &scratch)) {
+    (void)hipGetLastError();
+    scratch = nullptr;  // a performance choice, never a data-path failure
+  }
   int rc = launch_classify(ep, *pk, n, out, reinterpret_cast<uint4*>(lb_out), D.d_counters, count,
-                           ga.scratch ? &ga : nullptr, st, n ? next_marks(D) : nullptr);
-  if (!rc && ga.scratch) rc = group_scratch_used(D, st);
+                           ga.scratch ? &ga : nullptr, st, n ? next_marks(D) : nullptr,
+                           park_bytes && scratch ? reinterpret_cast<uint4*>(scratch) : nullptr);
+  if (!rc && scratch) rc = group_scratch_used(D, st);
   if (rc || n == 0) return rc;
   return note_launch(ctx, D, st);
 }

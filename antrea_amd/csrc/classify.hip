@@ -293,7 +293,7 @@ template <bool kDelta, bool kSvc, int kStage, bool kSort = false>
 __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
-    uint32_t xcd_order, uint2* __restrict__ gout) {
+    uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
   const uint64_t block_base = logical_block<kGroupTile / block_threads<kSort>()>(xcd_order) * block_threads<kSort>();
@@ -329,17 +329,29 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   uint32_t svc_group = pk.svc_group ? pk.svc_group[i] : 0u;
   uint32_t dest = pk.dest ? pk.dest[i] : 0u;
   const uint32_t ct_mark = pk.ct_mark ? pk.ct_mark[i] : 0u;
-  if (kSvc) {  // both launches derive the same Endpoint (the selection is a pure function of the packet)
+  // Service stage. kStage 0: one launch does it and both policy stages. kStage 1 / 2 (Service
+  // batches split like the others): the egress launch runs it and parks the fields it rewrites
+  // (destination, port, reg1 / reg7, destination mark) in park[i]; the ingress launch reads them back
+  // instead of repeating the lookup. NO_ENDPOINT: rejected in EndpointDNAT before the policy
+  // stages, so the ingress launch sees a REJECT egress action and stores ingress NONE.
+  if (kSvc && kStage == 2) {
+    // (read after the egress-action check below)
+  } else if (kSvc) {
     uint32_t lb[4];
     const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
     // grouped with the un-permute (gout): results in grouped order, unpermute_kernel stores them
-    if (kStage != 2 && lb_out) lb_out[gout ? i : at()] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+    if (lb_out) lb_out[gout ? i : at()] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+    if (kStage == 1) park[i] = make_uint4(dst, (dport & 0xffffu) | (dest << 16), out_port, svc_group);
     if (f & GPC_LB_NO_ENDPOINT) {  // EndpointDNAT serviceNoEndpointFlow: rejected before the policy stages
       const uint32_t rj = pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0);
       if (kStage == 0 && gout) {
         mid[i] = make_uint2(0u, rj);
         gout[i] = make_uint2(0u, 0u);
-      } else if (kStage != 2) {
+      } else if (kStage == 1 && orig) {
+        mid[i] = make_uint2(0u, rj);
+      } else if (kStage == 1) {
+        out[i] = make_uint4(0u, rj, 0u, 0u);
+      } else {
         out[at()] = make_uint4(0u, rj, 0u, 0u);
       }
       return;
@@ -351,6 +363,14 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
       if (orig) store2(0u, 0u);  // ingress NONE
       return;
+    }
+    if (kSvc) {  // the fields the egress launch's Service stage rewrote
+      const uint4 pv = park[i];
+      dst = pv.x;
+      dport = pv.y & 0xffffu;
+      dest = pv.y >> 16;
+      out_port = pv.z;
+      svc_group = pv.w;
     }
     if (const uint32_t b = ingress_bypass(ep.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
       store2(0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
@@ -490,30 +510,39 @@ static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* g
 template <bool kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                    unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, uint32_t xo, uint2* gout,
-                   hipStream_t stream, LaunchMarks* marks) {
+                   uint4* park, hipStream_t stream, LaunchMarks* marks) {
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   uint4* const o = reinterpret_cast<uint4*>(out);
+  if (kSvc && park) {  // split like the Service-free batches, the rewritten fields parked in between
+    launch_mark(marks, kLaunchEgress, stream);
+    hipLaunchKernelGGL((classify_kernel<kDelta, true, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
+                       lb_out, counters, count, orig, mid, xo, gout, park);
+    launch_mark(marks, kLaunchIngress, stream);
+    hipLaunchKernelGGL((classify_kernel<kDelta, true, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
+                       lb_out, counters, count, orig, mid, xo, gout, park);
+    return;
+  }
   if (kSvc) {
     launch_mark(marks, kLaunchBoth, stream);
     hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid, xo, gout);
+                       lb_out, counters, count, orig, mid, xo, gout, nullptr);
     return;
   }
   const uint64_t sblocks = (n + kSortBlock - 1) / kSortBlock;
   launch_mark(marks, kLaunchEgress, stream);
   if (ep.sort_table[0])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
-                       ep, pk, n, o, lb_out, counters, count, orig, mid, xo, nullptr);
+                       ep, pk, n, o, lb_out, counters, count, orig, mid, xo, nullptr, nullptr);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid, xo, nullptr);
+                       lb_out, counters, count, orig, mid, xo, nullptr, nullptr);
   launch_mark(marks, kLaunchIngress, stream);
   if (ep.sort_table[1])
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2, true>), dim3(uint32_t(sblocks)), dim3(kSortBlock), 0, stream,
-                       ep, pk, n, o, lb_out, counters, count, orig, mid, xo, gout);
+                       ep, pk, n, o, lb_out, counters, count, orig, mid, xo, gout, nullptr);
   else
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
-                       lb_out, counters, count, orig, mid, xo, gout);
+                       lb_out, counters, count, orig, mid, xo, gout, nullptr);
 }
 
 // gpc_trace: one packet through the same table walk as classify_kernel (Service stage and journal
@@ -681,7 +710,7 @@ int launch_classify6(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc
 
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
-                    LaunchMarks* marks) {
+                    LaunchMarks* marks, uint4* park) {
   if (n == 0) return 0;
   if (n > kMaxPackets) return -GPC_EINVAL;
   gpc_pkt_soa g;
@@ -703,10 +732,10 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   // results) in grouped order for the un-permute, like the two launches without Services
   if (svc && lb_out && gout && !lbg) return -GPC_EINVAL;  // the caller sized the scratch without lb
   uint4* const lbk = lbg ? lbg : lb_out;
-  if (delta && svc) launch<true, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, stream, marks);
-  else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
-  else if (svc) launch<false, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, stream, marks);
-  else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, stream, marks);
+  if (delta && svc) launch<true, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
+  else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
+  else if (svc) launch<false, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
+  else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
   if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), svc ? lbg : nullptr, lb_out, stream, marks);
   launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;

@@ -1245,14 +1245,19 @@ GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
 //   service records {first endpoint, n_ep | slot_log2 << 24, group id, flags};
 //   endpoint records {ip, port | flags << 16, out_port (reg1), destination class}.
 struct SvcHdr {
-  uint32_t hash_off, hash_log2, svc_off, n_svc, ep_off, n_ep, reserved[2];
+  uint32_t hash_off, hash_log2, svc_off, n_svc, ep_off, n_ep;
+  uint32_t map_off, map_log2;  // 2^map_log2-bit map of the keys (svc_map_bit): most packets that
+                               // address no Service are settled by one load
 };
-constexpr uint32_t kSvcBucketWords = 32;
+// Service hash: 2-choice cuckoo, buckets of two 16-B slots {key low, key high, service index, 0}:
+// a lookup is one 128-bit load per slot (four per packet), not a 96-B scan of an 8-way bucket.
+constexpr uint32_t kSvcBucketWords = 8, kSvcSlots = 2, kSvcSlotWords = 4;
 constexpr uint32_t kSvcLoadReg7 = 1u;  // service flag: the ServiceLB flow loads reg7 = group id
 // endpoint flags (port word >> 16): GPC_LB_DNAT / GPC_LB_REMOTE values
 GPC_HD uint64_t svc_key(uint32_t proto, uint32_t ip, uint32_t port) {
   return (1ull << 63) | (uint64_t(proto & 0xffu) << 48) | (uint64_t(port & 0xffffu) << 32) | ip;
 }
+GPC_HD uint32_t svc_map_bit(uint64_t key, uint32_t log2) { return uint32_t(mix64(key ^ 0xa0761d6478bd642full) >> (64 - log2)); }
 // Endpoint selection of the select group. OVS picks a bucket by dp_hash over a symmetric L4 hash
 // with a 64-slot table for equal weights (OVS-internal, not in the reference: parity unpinned);
 // restated: symmetric hash of (src ^ dst, sport ^ dport, proto), slot table of 2^slot_log2 >= 64
@@ -1264,17 +1269,27 @@ GPC_HD uint32_t lb_hash(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dpo
 GPC_HD uint32_t svc_lookup(const uint32_t* sv, uint32_t proto, uint32_t ip, uint32_t port) {
   const SvcHdr* h = reinterpret_cast<const SvcHdr*>(sv);
   const uint64_t key = svc_key(proto, ip, port);
+  const uint32_t mb = svc_map_bit(key, h->map_log2);
+  GPC_TOUCH(sv + h->map_off + (mb >> 5), 4);
+  if (!((sv[h->map_off + (mb >> 5)] >> (mb & 31u)) & 1u)) return 0xffffffffu;
   const uint32_t mask = (1u << h->hash_log2) - 1u;
   const uint32_t bs[2] = {hash_b1(key, mask), hash_b2(key, mask)};
+  const uint32_t klo = uint32_t(key), khi = uint32_t(key >> 32);
   uint32_t r = 0xffffffffu;
 #pragma unroll
   for (int c = 0; c < 2; c++) {
     const uint32_t* b = sv + h->hash_off + size_t(bs[c]) * kSvcBucketWords;
-    GPC_TOUCH(b, 96);
-    const uint64_t* k = reinterpret_cast<const uint64_t*>(b);
+    GPC_TOUCH(b, 4 * kSvcBucketWords);
 #pragma unroll
-    for (int i = 0; i < 8; i++)
-      if (k[i] == key) r = b[16 + i];
+    for (uint32_t i = 0; i < kSvcSlots; i++) {
+#if defined(__HIPCC__)
+      const uint4 v = reinterpret_cast<const uint4*>(b)[i];
+      const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
+#else
+      const uint32_t w0 = b[kSvcSlotWords * i], w1 = b[kSvcSlotWords * i + 1], w2 = b[kSvcSlotWords * i + 2];
+#endif
+      r = (w0 == klo && w1 == khi) ? w2 : r;
+    }
   }
   return r;
 }

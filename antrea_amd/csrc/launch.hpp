@@ -57,9 +57,11 @@ inline void launch_mark(LaunchMarks* m, uint8_t kind, hipStream_t s) {
   if (!m || m->n >= LaunchMarks::kMax) return;
   if (hipEventRecord(m->ev[m->n], s) == hipSuccess) m->kind[m->n++] = kind;
 }
+// park: with Services (ep.svc), 16 B per packet of device scratch for the fields the Service stage
+// rewrites, handed from the egress launch to the ingress launch; null: one launch does both stages.
 int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                     unsigned long long* counters, int count, const GroupArgs* group, hipStream_t stream,
-                    LaunchMarks* marks = nullptr);
+                    LaunchMarks* marks = nullptr, uint4* park = nullptr);
 // IPv6 batch (pk.src6 / dst6 [/ ct_src6 / ct_dst6]) against the IPv6 image `ep` (base or delta
 // epoch): v6_code_kernel maps the addresses to codes in `codes` (v6_code_columns(pk) * n words of
 // device memory, live until the launches have run), then launch_classify runs over the code columns

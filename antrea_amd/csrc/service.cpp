@@ -252,17 +252,18 @@ std::string FeatureService::dump_groups() const {
 // --------------------------------------------------------------------------- device image
 namespace {
 
-struct SvcHash {  // 2-choice, 8-way cuckoo table of (key, value)
+struct SvcHash {  // 2-choice cuckoo table of (key, value), kSvcSlots slots per bucket
   uint32_t log2 = 0;
   std::vector<uint64_t> keys;
   std::vector<uint32_t> vals;
   bool build(const std::vector<std::pair<uint64_t, uint32_t>>& kv) {
-    for (log2 = 1; (8ull << log2) < 2 * kv.size() + 8; log2++) {
+    constexpr uint32_t S = kSvcSlots;
+    for (log2 = 1; double(S << log2) * 0.6 < double(kv.size() + 1); log2++) {
     }
     for (int attempt = 0; attempt < 8; attempt++, log2++) {
       const uint32_t nb = 1u << log2, mask = nb - 1;
-      keys.assign(size_t(nb) * 8, 0);
-      vals.assign(size_t(nb) * 8, 0);
+      keys.assign(size_t(nb) * S, 0);
+      vals.assign(size_t(nb) * S, 0);
       bool ok = true;
       for (auto& e : kv) {
         uint64_t k = e.first;
@@ -271,10 +272,10 @@ struct SvcHash {  // 2-choice, 8-way cuckoo table of (key, value)
         while (true) {
           bool placed = false;
           for (uint32_t b : {hash_b1(k, mask), hash_b2(k, mask)}) {
-            for (int i = 0; i < 8 && !placed; i++)
-              if (!keys[size_t(b) * 8 + i]) {
-                keys[size_t(b) * 8 + i] = k;
-                vals[size_t(b) * 8 + i] = v;
+            for (uint32_t i = 0; i < S && !placed; i++)
+              if (!keys[size_t(b) * S + i]) {
+                keys[size_t(b) * S + i] = k;
+                vals[size_t(b) * S + i] = v;
                 placed = true;
               }
             if (placed) break;
@@ -285,9 +286,9 @@ struct SvcHash {  // 2-choice, 8-way cuckoo table of (key, value)
             break;
           }
           const uint32_t b = (kicks & 1) ? hash_b2(k, mask) : hash_b1(k, mask);
-          const int i = kicks % 8;
-          std::swap(k, keys[size_t(b) * 8 + i]);
-          std::swap(v, vals[size_t(b) * 8 + i]);
+          const uint32_t i = uint32_t(kicks) % S;
+          std::swap(k, keys[size_t(b) * S + i]);
+          std::swap(v, vals[size_t(b) * S + i]);
         }
         if (!ok) break;
       }
@@ -383,8 +384,10 @@ int FeatureService::build_image(std::vector<uint32_t>* blob, std::string* err) c
   }
   const uint32_t nb = 1u << h.log2;
   SvcHdr hdr{};
-  const uint32_t hdr_words = sizeof(SvcHdr) / 4;
-  hdr.hash_off = 32;  // 128-B aligned buckets
+  hdr.map_log2 = 12;  // about 16 map bits per Service: most non-Service packets stop at the map
+  while (hdr.map_log2 < 22 && (1ull << hdr.map_log2) < 16ull * kv.size()) hdr.map_log2++;
+  hdr.map_off = 32;
+  hdr.hash_off = hdr.map_off + (1u << (hdr.map_log2 - 5));  // 128-B aligned
   hdr.hash_log2 = h.log2;
   hdr.svc_off = hdr.hash_off + nb * kSvcBucketWords;
   hdr.n_svc = uint32_t(svc_words.size() / 4);
@@ -392,11 +395,18 @@ int FeatureService::build_image(std::vector<uint32_t>* blob, std::string* err) c
   hdr.n_ep = uint32_t(ep_words.size() / 4);
   blob->assign(hdr.ep_off + ep_words.size(), 0u);
   std::memcpy(blob->data(), &hdr, sizeof hdr);
-  (void)hdr_words;
+  for (auto& e : kv) {
+    const uint32_t mb = svc_map_bit(e.first, hdr.map_log2);
+    (*blob)[hdr.map_off + (mb >> 5)] |= 1u << (mb & 31u);
+  }
   for (uint32_t b = 0; b < nb; b++) {
     uint32_t* w = blob->data() + hdr.hash_off + size_t(b) * kSvcBucketWords;
-    std::memcpy(w, &h.keys[size_t(b) * 8], 64);
-    std::memcpy(w + 16, &h.vals[size_t(b) * 8], 32);
+    for (uint32_t i = 0; i < kSvcSlots; i++) {
+      const uint64_t k = h.keys[size_t(b) * kSvcSlots + i];
+      w[kSvcSlotWords * i] = uint32_t(k);
+      w[kSvcSlotWords * i + 1] = uint32_t(k >> 32);
+      w[kSvcSlotWords * i + 2] = h.vals[size_t(b) * kSvcSlots + i];
+    }
   }
   std::copy(svc_words.begin(), svc_words.end(), blob->begin() + hdr.svc_off);
   std::copy(ep_words.begin(), ep_words.end(), blob->begin() + hdr.ep_off);

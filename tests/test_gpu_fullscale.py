@@ -71,6 +71,19 @@ def test_device_vs_oracle_fullscale(config, group):
     assert {1, 2} <= acts and (3 in acts or 5 in acts), acts
 
 
+@pytest.mark.parametrize("config", ["C2", "C3"])
+def test_device_vs_oracle_fullscale_plain_driver(config, monkeypatch):
+    """The same parity with the composite driver index turned off (GPC_COMPOSITE=0, read at image
+    build): tables then keep the plain per-clause driver indexes, the kernel's other lookup path."""
+    monkeypatch.setenv("GPC_COMPOSITE", "0")
+    f, wl, cols = _inputs(config)
+    c = _classifier(wl, group=1)
+    got = c.classify_host(cols, count=True)
+    res = parity.compare(got, f["verdicts"])
+    assert res["mismatches"] == 0, res
+    assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
+
+
 @pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
 def test_device_ipv6_vs_oracle_fullscale_c3(group):
     """gpc_classify6 on full C3 embedded in fd00:10::/96 (IPv6 image, device LPM) equals the C
