@@ -875,7 +875,7 @@ bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vect
 // MI355X (64M packets, profiles/r03h_*): C1 8.73 -> 8.51 ms, C2 14.00 -> 10.25, C3 10.66 -> 10.12,
 // C4 12.18 -> 11.38.
 constexpr size_t kCompositeMaxValues = 16;
-constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 26;
+constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 24;  // 256 MB of entries at most
 void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>& rec_off, const uint64_t* span, int t,
                      TableHdr& th, Blob& B, HostImage* out) {
   th.n_cidx = 0;
