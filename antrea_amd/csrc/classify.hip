@@ -20,6 +20,9 @@ namespace gpc {
 #ifndef GPC_WAVES_PER_EU
 #define GPC_WAVES_PER_EU 6
 #endif
+#ifndef GPC_DELTA_WAVES_PER_EU  // delta-epoch (journal) kernels
+#define GPC_DELTA_WAVES_PER_EU 6
+#endif
 #ifndef GPC_BLOCK
 #define GPC_BLOCK 64
 #endif
@@ -290,7 +293,7 @@ __device__ __forceinline__ uint64_t logical_block(uint32_t mode) {
 // logical block order classifies grouped packet i, whose caller index is orig[i]. IPv6 batches come
 // here as code columns (v6_code_kernel) against the IPv6 image.
 template <bool kDelta, bool kSvc, int kStage, bool kSort = false>
-__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(GPC_WAVES_PER_EU))) void classify_kernel(
+__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta ? GPC_DELTA_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
     uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {

@@ -1167,16 +1167,29 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
     }
   }
   if (hfound) res.h = hprio | (hverdict << 16) | kHFound | htie;
-  uint32_t cnt[2] = {jt.always[0] >> 24, jt.always[1] >> 24};
+  // Driver clause of the journal walk. A table with a composite base index: its band clause (the
+  // other one holds the AppliedTo values, whose chains list every changed rule of a Pod), chosen
+  // without reading any head; else the clause with the shorter chains (saturating chain lengths).
+  uint32_t d;
+  const TableHdr& bt = v.base.hdr->t[table - 1];
+#if defined(GPC_JOURNAL_COUNT_ALWAYS)  // experiments: the pre-composite choice
+  if (false) {
+#else
+  if (bt.n_cidx) {  // (every soft rule has clauses 0 and 1: one-clause rules compile to plain flows)
+#endif
+    d = bt.cband;
+  } else {
+    uint32_t cnt[2] = {jt.always[0] >> 24, jt.always[1] >> 24};
 #pragma unroll
-  for (uint32_t k = 0; k < 2; k++)
-    for (uint32_t i = 0; i < jt.n_kinds[k]; i++) {
-      const uint32_t axis = jt.kinds[k][i] & 15u, band = jt.kinds[k][i] >> 4;
-      const uint32_t meta = jmeta(table, k, axis, band);
-      cnt[k] += jhead(pool, jh, jbucket(meta, jkey(axis, band, p.ax[axis]), jh->lg)) >> 24;
-    }
-  if (cnt[0] + cnt[1] == 0) return res;
-  const uint32_t d = (jt.n_kinds[1] || jt.always[1]) && cnt[1] < cnt[0] ? 1u : 0u;
+    for (uint32_t k = 0; k < 2; k++)
+      for (uint32_t i = 0; i < jt.n_kinds[k]; i++) {
+        const uint32_t axis = jt.kinds[k][i] & 15u, band = jt.kinds[k][i] >> 4;
+        const uint32_t meta = jmeta(table, k, axis, band);
+        cnt[k] += jhead(pool, jh, jbucket(meta, jkey(axis, band, p.ax[axis]), jh->lg)) >> 24;
+      }
+    if (cnt[0] + cnt[1] == 0) return res;
+    d = (jt.n_kinds[1] || jt.always[1]) && cnt[1] < cnt[0] ? 1u : 0u;
+  }
   uint32_t best = 0, best_prio = 0, best_conj = 0, at_best = 0;
   for (uint32_t i = 0; i <= jt.n_kinds[d]; i++) {
     uint32_t meta = 0, key = 0, e;
@@ -1192,20 +1205,29 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
     while (e & 0xffffffu) {
       const uint32_t* en = pool + size_t(e & 0xffffffu) * kJEntWords;
       GPC_TOUCH(en, 4 * kJEntWords);
-      e = en[0];
-      if (!always && (en[1] != key || (en[2] & kJMetaMask) != meta)) continue;
-      if (rule_dead(im, en[2] >> kJOridShift)) continue;
+      // the 32-B entry as two 16-B loads (entries are 32-B aligned)
+      uint32_t ew[kJEntWords];
+#if defined(__HIPCC__) && !defined(GPC_JOURNAL_WORD_LOADS)
+      const uint4 ea = reinterpret_cast<const uint4*>(en)[0], eb = reinterpret_cast<const uint4*>(en)[1];
+      ew[0] = ea.x, ew[1] = ea.y, ew[2] = ea.z, ew[3] = ea.w, ew[4] = eb.x, ew[5] = eb.y, ew[6] = eb.z, ew[7] = eb.w;
+#else
+      for (uint32_t w = 0; w < kJEntWords; w++) ew[w] = en[w];
+#endif
+      e = ew[0];
+      if (!always && (ew[1] != key || (ew[2] & kJMetaMask) != meta)) continue;
+      if (rule_dead(im, ew[2] >> kJOridShift)) continue;
       Ent f;
-      f.x = en[4];
-      f.y = en[5];
-      f.lo = en[6];
-      f.hi = en[7];
+      f.x = ew[4];
+      f.y = ew[5];
+      f.lo = ew[6];
+      f.hi = ew[7];
       if (!entry_pass(p, f)) continue;
-      const uint32_t off = en[3];
+      const uint32_t off = ew[3];
       const uint32_t* rec = pool + off;
       GPC_TOUCH(rec, 4 * kRecHdrWords);
-      const uint32_t w1 = rec[1], w2 = rec[2];
-      const uint32_t prio = w1 & 0xffffu, conj = rec[0];
+      const RecHdr hd = load_rec_hdr(rec);
+      const uint32_t w1 = hd.w[1], w2 = hd.w[2];
+      const uint32_t prio = w1 & 0xffffu, conj = hd.w[0];
       if (best && prio < best_prio) continue;  // cannot change the decision
       if (!rule_match(im, rec, w2, d, 0, p)) continue;
       if (!best || prio > best_prio) {
