@@ -326,10 +326,23 @@ GPC_HD uint32_t v6_len(const V6Len& d) { return d.meta & 0xffu; }
 GPC_HD uint32_t v6_kw(const V6Len& d) { return (d.meta >> 8) & 0xffu; }
 GPC_HD uint32_t v6_log2(const V6Len& d) { return d.meta >> 16; }
 struct V6Lpm {
-  uint32_t n_lens, reserved[3];
+  uint32_t n_lens;
+  uint32_t l1_off;            // region table (0: none): 2^16 entries of 4 words, see v6_codes
+  uint32_t l1_c;              // its tag length c: regions are the /c+16 blocks under the tag
+  uint32_t reserved;
   uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
   V6Len d[kV6MaxLens];        // d[i]: the table of lens[i]
+  uint32_t l1_tag[4];         // the top c bits every prefix shares, right-aligned (v6_key(a, c))
 };
+// Region table (image.cpp build_image6): when every prefix of the tree lies under one /c (C3 in
+// fd00:10::/96: c = 96), an address under it is first looked up by its next 16 bits (one 16-B load,
+// a 1-MB table): entry {code of the deepest prefix no longer than c + 16 holding the region,
+// number n of the lengths longer than c + 16 present in the region | kV6L1Global, the indexes of
+// those lengths, 8 bits each}; the binary search then runs over those n lengths only (regional
+// markers are in the per-length tables; a marker carries the best match at its length whatever
+// search tree placed it, so extra markers never mislead the global search). kV6L1Global: more
+// than 8 lengths, search them all.
+constexpr uint32_t kV6L1Bits = 16, kV6L1Global = 16u, kV6L1MaxLens = 8;
 // Bucket: two slots; slot = key (kw words), code, padding to 2 / 4 / 8 words: 16 / 32 / 64-B buckets.
 constexpr uint32_t kV6BucketWords = 16;  // the largest bucket (and the overflow table's)
 GPC_HD uint32_t v6_slot_words(uint32_t kw) { return kw == 4u ? 8u : 2u * kw; }
@@ -472,11 +485,35 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
   const V6Len* D = desc ? desc : L->d;
   const uint32_t omask = (1u << ovf_log2) - 1u;
   int lo[K], hi[K];
+  uint32_t rl[K][2];  // regional search: the length indexes (8 bits each); all-ones: global
 #pragma unroll
   for (int k = 0; k < K; k++) {
     code[k] = 0;
     lo[k] = 0;
     hi[k] = int(L->n_lens) - 1;
+    rl[k][0] = rl[k][1] = 0xffffffffu;
+    // (a delta epoch's overflow entries may sit at lengths a region's list omits: global search)
+    if (!kOvf && L->l1_off) {
+      const uint32_t c = L->l1_c;
+      uint32_t t[4] = {0u, 0u, 0u, 0u}, x[4];
+      if (c) v6_key(a[k], c, t);
+      if (t[0] == L->l1_tag[0] && t[1] == L->l1_tag[1] && t[2] == L->l1_tag[2] && t[3] == L->l1_tag[3]) {
+        v6_key(a[k], c + kV6L1Bits, x);
+        const uint32_t* e = blob + L->l1_off + 4 * size_t(x[3] & ((1u << kV6L1Bits) - 1u));
+        GPC_TOUCH(e, 16);
+#if defined(__HIPCC__)
+        const uint4 ev = *reinterpret_cast<const uint4*>(e);
+#else
+        const struct { uint32_t x, y, z, w; } ev = {e[0], e[1], e[2], e[3]};
+#endif
+        if (!(ev.y & kV6L1Global)) {
+          code[k] = ev.x;
+          hi[k] = int(ev.y & 15u) - 1;
+          rl[k][0] = ev.z;
+          rl[k][1] = ev.w;
+        }
+      }
+    }
   }
   while (true) {
     bool any = false;
@@ -489,7 +526,9 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
 #pragma unroll
     for (int k = 0; k < K; k++) {
       const bool live = lo[k] <= hi[k];
-      const V6Len& d = D[live ? (lo[k] + hi[k]) >> 1 : 0];
+      const uint32_t mid = live ? uint32_t(lo[k] + hi[k]) >> 1 : 0u;
+      const uint32_t li = rl[k][0] == 0xffffffffu ? mid : ((mid < 4u ? rl[k][0] >> (8u * mid) : rl[k][1] >> (8u * (mid - 4u))) & 0xffu);
+      const V6Len& d = D[li];
       len[k] = v6_len(d);
       kw[k] = v6_kw(d);
       v6_key(a[k], len[k], r[k]);

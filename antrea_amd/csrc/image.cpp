@@ -1333,6 +1333,89 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
       lo = mid + 1;
     }
   }
+  // Region table (core.hpp kV6L1Bits): when all prefixes share their top c bits (c <= the shortest
+  // length, c + 16 <= 128), every /c+16 region gets the best match no longer than c + 16 and the
+  // list of longer lengths present under it, plus the markers of that shorter search.
+  uint32_t l1_c = 0;
+  bool l1 = codes.nodes.size() > 1;
+  std::vector<uint32_t> l1_tab;
+  u128 tag_v = 0;
+  if (l1) {
+    const u128 v0 = codes.nodes[1].v;
+    int c = 128;
+    for (size_t n = 1; n < codes.nodes.size(); n++) {
+      const auto& N = codes.nodes[n];
+      c = std::min(c, N.len);
+      const u128 x = N.v ^ v0;
+      int lcp = 0;
+      while (lcp < 128 && !((x >> (127 - lcp)) & 1)) lcp++;
+      c = std::min(c, lcp);
+    }
+    l1_c = uint32_t(c);
+    l1 = c + int(kV6L1Bits) <= 128;
+    tag_v = c ? (v0 & v6_prefix_mask(c)) : 0;
+  }
+  if (l1) {
+    const uint32_t s_len = l1_c + kV6L1Bits, nreg = 1u << kV6L1Bits;
+    auto region = [&](u128 v) { return uint32_t(v >> (128 - s_len)) & (nreg - 1u); };
+    std::vector<uint32_t> base(nreg, 0u), base_len(nreg, 0u);
+    std::vector<std::vector<uint32_t>> reg_lens(nreg);  // length indexes > s_len present
+    for (size_t n = 1; n < codes.nodes.size(); n++) {
+      const auto& N = codes.nodes[n];
+      const uint32_t li = uint32_t(std::lower_bound(lens.begin(), lens.end(), uint32_t(N.len)) - lens.begin());
+      if (uint32_t(N.len) > s_len) {
+        reg_lens[region(N.v)].push_back(li);
+        continue;
+      }
+      // a prefix no longer than c + 16 covers 2^(c+16-len) whole regions: the deepest one wins
+      const uint32_t r0 = region(N.v), span = 1u << (s_len - uint32_t(N.len));
+      for (uint32_t r = r0; r < r0 + span; r++)
+        if (uint32_t(N.len) >= base_len[r]) {
+          base[r] = pad(N);
+          base_len[r] = uint32_t(N.len);
+        }
+    }
+    l1_tab.assign(size_t(nreg) * 4, 0u);
+    for (uint32_t r = 0; r < nreg; r++) {
+      auto& L = reg_lens[r];
+      std::sort(L.begin(), L.end());
+      L.erase(std::unique(L.begin(), L.end()), L.end());
+      uint32_t* e = l1_tab.data() + 4 * size_t(r);
+      e[0] = base[r];
+      if (L.size() > kV6L1MaxLens) {
+        e[1] = kV6L1Global;
+        continue;
+      }
+      e[1] = uint32_t(L.size());
+      for (size_t j = 0; j < L.size(); j++) e[2 + j / 4] |= L[j] << (8 * (j % 4));
+    }
+    // markers of the regional searches (nodes longer than c + 16 in regions with a list)
+    for (size_t n = 1; n < codes.nodes.size(); n++) {
+      const auto& P = codes.nodes[n];
+      if (uint32_t(P.len) <= s_len) continue;
+      const auto& L = reg_lens[region(P.v)];
+      if (L.size() > kV6L1MaxLens) continue;
+      const uint32_t li = uint32_t(std::lower_bound(lens.begin(), lens.end(), uint32_t(P.len)) - lens.begin());
+      const int t = int(std::lower_bound(L.begin(), L.end(), li) - L.begin());
+      int lo = 0, hi = int(L.size()) - 1;
+      while (lo <= hi) {
+        const int mid = (lo + hi) / 2;
+        if (mid == t) break;
+        if (mid > t) {
+          hi = mid - 1;
+          continue;
+        }
+        const uint32_t M = lens[L[size_t(mid)]];
+        const std::pair<u128, uint32_t> key{P.v & v6_prefix_mask(int(M)), M};
+        if (!lpm_map.count(key)) {
+          int a = P.parent;
+          while (a > 0 && codes.nodes[size_t(a)].len > int(M)) a = codes.nodes[size_t(a)].parent;
+          lpm_map[key] = a > 0 ? pad(codes.nodes[size_t(a)]) : 0u;
+        }
+        lo = mid + 1;
+      }
+    }
+  }
   // one table per length (core.hpp V6Len), appended after the V6Lpm block
   std::vector<std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>> per_len(lens.size());
   for (auto& kv : lpm_map) {
@@ -1361,6 +1444,15 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     L.d[i].tab_off = uint32_t(b.size());
     b.insert(b.end(), tab.begin(), tab.end());
     tab_words += tab.size();
+  }
+  if (l1) {
+    while (b.size() % 16) b.push_back(0u);
+    L.l1_off = uint32_t(b.size());
+    L.l1_c = l1_c;
+    const uint32_t tg[4] = {uint32_t(tag_v >> 96), uint32_t(tag_v >> 64), uint32_t(tag_v >> 32), uint32_t(tag_v)};
+    if (l1_c) v6_key(tg, l1_c, L.l1_tag);
+    b.insert(b.end(), l1_tab.begin(), l1_tab.end());
+    tab_words += l1_tab.size();
   }
   std::memcpy(b.data() + lpm, &L, sizeof L);
   out->hdr.v6_lpm = lpm;

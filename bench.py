@@ -215,6 +215,20 @@ def _host_sample(cols, idx):
     return out
 
 
+def _grouping_label(st, launches, v6):
+    """How the timed batches were grouped, from the launches that actually ran (gpc_launch_times)."""
+    if "group_tiles" not in (launches or {}):
+        return "off"
+    if v6:
+        key = "key: top 8 bits of the source address code (IPv6 code columns)"
+    elif st["group_key"] == gpc.GROUP_KEY_ADDR:
+        sb = int(os.environ.get("GPC_GROUP_SRC_BITS", "8"))
+        key = "key: top %d bits of nw_src + %d of nw_dst" % (sb, 8 - sb)
+    else:
+        key = "key: egress x ingress scan-length bins"
+    return key + ", 16384-packet tiles" + (", results un-permuted" if "unpermute" in launches else "")
+
+
 KIND_STAGE = {"classify_egress": "1", "classify_ingress": "2", "classify_both": "0"}
 
 
@@ -517,14 +531,7 @@ def main():
                    "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
                    "counters": count, "parallelism": "packet-shard x%d, rules replicated" % world,
                    "verdict_mix": mix, "build_s": round(t_build, 1),
-                   "packet_grouping": (("key: top %s bits of nw_src + %d of nw_dst, 16384-packet tiles" % (
-                       os.environ.get("GPC_GROUP_SRC_BITS", "8"), 8 - int(os.environ.get("GPC_GROUP_SRC_BITS", "8"))))
-                       if st["group_key"] == gpc.GROUP_KEY_ADDR else
-                       "key: egress x ingress scan-length bins, 16384-packet tiles") +
-                   (", ingress verdicts un-permuted" if os.environ.get("GPC_GROUP_UNPERMUTE", "1") != "0"
-                    and not getattr(wl, "services", None) else "")
-                   if not v6 and (args.group > 0 or (args.group == 0 and n >= 1 << 18 and st["device_bytes"] >= 4 << 20))
-                   else "off"},
+                   "packet_grouping": _grouping_label(st, launches, v6)},
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)
         "launches_per_step": round(sum(t["per_step"] for t in launches.values()), 2),
         "kernel_ms_by_launch": {k: round(t["mean_ms"], 3) for k, t in launches.items()},
