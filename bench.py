@@ -217,6 +217,7 @@ def _host_sample(cols, idx):
 
 def _grouping_label(st, launches, v6):
     """How the timed batches were grouped, from the launches that actually ran (gpc_launch_times)."""
+    from antrea_amd import gpc
     if "group_tiles" not in (launches or {}):
         return "off"
     if v6:

@@ -60,3 +60,15 @@ def test_churn_ops_same_seed_same_stream():
     for _ in range(7):
         ob.apply(50)
     assert a.seq == b.seq[:350] and len(a.seq) == 350
+
+
+def test_grouping_label_from_launches():
+    """The bench line's packet_grouping field names what ran (no GPU: launch names only)."""
+    import bench
+    from antrea_amd import gpc
+    st = {"group_key": gpc.GROUP_KEY_ADDR}
+    assert bench._grouping_label(st, {"classify_egress": {}}, False) == "off"
+    lab = bench._grouping_label(st, {"group_tiles": {}, "unpermute": {}}, False)
+    assert lab.startswith("key: top 8 bits of nw_src") and lab.endswith("results un-permuted")
+    assert "IPv6 code columns" in bench._grouping_label(st, {"group_tiles": {}}, True)
+    assert "scan-length" in bench._grouping_label({"group_key": gpc.GROUP_KEY_SCAN}, {"group_tiles": {}}, False)
