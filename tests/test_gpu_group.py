@@ -114,15 +114,15 @@ def test_grouped_equals_plain_services_lb():
 
 
 def test_grouped_device_stream_batch():
-    """Device-pointer path on a torch stream with an auto-grouped batch (>= 2^18 packets) equals an
-    ungrouped one (the bench's configuration at a smaller size: 20k C3-shaped rules, an image above
-    the auto-grouping threshold)."""
+    """Device-pointer path on a torch stream with a grouped batch (>= 2^18 packets) equals an
+    ungrouped one (20k C3-shaped rules; auto mode no longer groups against composite images, so the
+    grouped run is forced)."""
     import torch
     wl = workload.config3(n_policies_per_dir=100)
     n = 1 << 19
     cols = workload.gen_packets_torch(wl, n, device="cuda")
     outs = []
-    for g in (0, -1):
+    for g in (1, -1):
         c = gpc.Classifier(group_packets=g)
         c.initialize()
         c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
