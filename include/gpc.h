@@ -131,9 +131,10 @@ typedef struct gpc_config {
   int32_t ovs_meters;            /* OVS meters supported: packet-in flows carry meter:256/258    */
   int32_t external_node;         /* config.ExternalNode: no IngressSecurityClassifier flows      */
   int32_t group_packets;         /* gpc_classify groups a batch by nw_src before the table walk:
-                                    0 = batches of >= 2^18 packets against an image of >= 4 MB,
-                                    > 0 = always, < 0 = never (gpc_classify6: only with the
-                                    environment GPC_GROUP_V6=1: measured no faster, C3 in IPv6) */
+                                    0 = batches of >= 2^18 packets against an image of >= 4 MB
+                                    without composite driver indexes (with them grouping
+                                    measured slower), > 0 = always, < 0 = never (gpc_classify6:
+                                    the same over the code columns; GPC_GROUP_V6=0: never)      */
   int32_t group_key;             /* grouping key of IPv4 batches (gpc_group_key; environment
                                     GPC_GROUP_KEY overrides): 0 = per image, SCAN when waves' scan
                                     lengths are very unequal (long driver lists), else ADDR       */
