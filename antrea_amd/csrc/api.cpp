@@ -1032,13 +1032,13 @@ static int group_scratch_for(gpc_ctx* ctx, DevState& D, hipStream_t st, size_t n
   return e;
 }
 
-// Auto mode leaves batches against an image with composite driver indexes ungrouped: the short
-// composite lists gain less from grouped lanes than the pre-pass and the un-permute cost (64M
+// Auto mode leaves batches against a base-only image with composite driver indexes ungrouped: the
+// short composite lists gain less from grouped lanes than the pre-pass and the un-permute cost (64M
 // packets, profiles/r03q_grouping_ab.txt: C3 10.13 grouped vs 9.91 ms, C2 10.27 vs 9.79, C4 9.13
-// vs 8.91).
-static bool group_batch(const gpc_ctx* ctx, size_t n, const DevImage& img) {
+// vs 8.91). Delta epochs (journal walks) still gain from it (C5: 13.05 grouped vs 13.58 ms).
+static bool group_batch(const gpc_ctx* ctx, size_t n, const DevImage& img, bool delta) {
   const int gm = ctx->cfg.group_packets;
-  return n && (gm > 0 || (gm == 0 && n >= kGroupMinPackets && img.bytes >= kGroupMinImageBytes && !img.composite));
+  return n && (gm > 0 || (gm == 0 && n >= kGroupMinPackets && img.bytes >= kGroupMinImageBytes && (!img.composite || delta)));
 }
 
 // GPC_GROUP_KEY_AUTO: scan lengths where a wavefront's lanes scan very unequal driver lists (the
@@ -1089,7 +1089,7 @@ int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n
   // egress and the ingress launch (classify.hip launch); without it (no memory) one launch does both
   const size_t park_bytes = D.cur.svc && n && ctx->svc_split ? (16 * n + 255) & ~size_t(255) : 0;
   uint8_t* scratch = nullptr;
-  if (group_batch(ctx, n, *D.cur.base)) {
+  if (group_batch(ctx, n, *D.cur.base, D.cur.jhdr != 0)) {
     if (const int e = group_scratch_for(ctx, D, st, park_bytes + group_scratch_bytes(*pk, n, ga.lb), &scratch)) return e;
     if (scratch) ga.scratch = scratch + park_bytes;
   }
@@ -1195,7 +1195,7 @@ int gpc_classify6_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t 
   shape.ct_src = pk->ct_src6 ? shape.src : nullptr;
   shape.ct_dst = pk->ct_dst6 ? shape.src : nullptr;
   uint8_t* scratch = nullptr;
-  if (n && ctx->group_v6 && group_batch(ctx, n, *D.cur.v6)) {
+  if (n && ctx->group_v6 && group_batch(ctx, n, *D.cur.v6, D.cur.v6_jhdr != 0)) {
     if (const int e = group_scratch_for(ctx, D, st, code_bytes + group_scratch_bytes(shape, n, false), &scratch)) return e;
     if (scratch) ga.scratch = scratch + code_bytes;
   }
