@@ -250,3 +250,26 @@ def test_grouped_per_thread_default_stream_two_threads():
     for k in range(2):
         for o in outs[k]:
             assert torch.equal(o, refs[k])
+
+
+@pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
+def test_service_split_equals_single_launch(group, monkeypatch):
+    """GPC_SVC_SPLIT=1 (read at gpc_create): Service batches as two launches, the DNAT'ed fields
+    parked between them, give the same verdicts, LB results and counters as the one-launch default."""
+    from tests.test_service import _svc_workload
+    wl = _svc_workload("C1", 62)
+    n = 40_000
+    cols = workload.gen_packets(wl, n, seed=15)
+    res = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("GPC_SVC_SPLIT", split)
+        c = gpc.Classifier(group_packets=group)
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+        workload.install_services(c, wl)
+        c.commit()
+        v, lb = c.classify_host(cols, count=True, lb=True)
+        res.append((v, lb, _metrics(c)))
+    assert ((res[0][1]["flags"] & gpc.LB_HIT) != 0).any()
+    assert (res[0][0] == res[1][0]).all() and (res[0][1] == res[1][1]).all()
+    assert res[0][2] == res[1][2]
