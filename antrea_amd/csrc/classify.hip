@@ -17,6 +17,10 @@
 
 namespace gpc {
 
+#if defined(GPC_STAMPS)
+__device__ unsigned long long gpc_stamp_acc[32];  // [16 * (kStage == 2) + region], [.. + 15] = waves
+#endif
+
 #ifndef GPC_WAVES_PER_EU
 #define GPC_WAVES_PER_EU 6
 #endif
@@ -299,6 +303,18 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
   __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
+#if defined(GPC_STAMPS)
+  {
+    uint32_t* st = gpc_stamp_lds();
+    if (threadIdx.x < ST_N + 1) st[threadIdx.x] = threadIdx.x == ST_N ? uint32_t(ST_PRE) : 0u;
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) st[ST_N + 1] = uint32_t(now), st[ST_N + 2] = uint32_t(now >> 32);
+    __syncthreads();
+  }
+  auto body = [&]() {
+#else
+  {
+#endif
   const uint64_t block_base = logical_block<kGroupTile / block_threads<kSort>()>(xcd_order) * block_threads<kSort>();
   uint64_t i = block_base + threadIdx.x;
   if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
@@ -427,6 +443,18 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if (kStage == 2) store2(g.conj, g.packed);
   else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
   else out[i] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
+#if defined(GPC_STAMPS)
+  };
+  body();
+  gpc_mark(ST_POST);
+  __syncthreads();
+  uint32_t* st = gpc_stamp_lds();
+  constexpr uint32_t sb = kStage == 2 ? 16u : 0u;
+  if (threadIdx.x < ST_N) atomicAdd(&gpc_stamp_acc[sb + threadIdx.x], (unsigned long long)st[threadIdx.x]);
+  if (threadIdx.x == 0) atomicAdd(&gpc_stamp_acc[sb + 15], 1ull);
+#else
+  }
+#endif
 }
 
 // Verdict pairs of a grouped batch in caller order: the egress half from mid (grouped order, every
@@ -743,5 +771,17 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
+
+#if defined(GPC_STAMPS)
+// Diagnostic builds: copy (and optionally clear) the region-stamp totals (tools/stamps.py).
+extern "C" int gpc_stamps_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpc_stamp_acc), sizeof(gpc_stamp_acc)) != hipSuccess) return -GPC_EDEV;
+  if (reset) {
+    static const unsigned long long zero[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gpc_stamp_acc), zero, sizeof(zero)) != hipSuccess) return -GPC_EDEV;
+  }
+  return 0;
+}
+#endif
 
 }  // namespace gpc

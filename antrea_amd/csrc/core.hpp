@@ -91,6 +91,22 @@ GPC_HD uint32_t rec_off(uint32_t w2, uint32_t k) { return (w2 >> (8 + 8 * k)) & 
 constexpr uint32_t kRecHdrWords = 6;
 constexpr uint32_t kRecPacketIn = 1u << 8;
 constexpr uint32_t kBoxWords = 7;
+// Fast clause descriptors (round 4): words kRecFcd + 3k .. + 2 of the record's first 64-B line
+// describe clause k in a shape the kernel checks with straight-line code instead of interpreting
+// its segment list (image.cpp fast_clause). A = kind | axis << 4 | n << 8, then B, C by kind:
+//   FK_GENERIC  several segments or multi-field boxes: clause_match at the clause offset
+//   FK_ALWAYS   every packet
+//   FK_IV1      B <= v <= C (one interval, a CIDR, a port range, one point)
+//   FK_MK1      (v & C) == B (one masked term: ct_state, masked tun_id)
+//   FK_HASH     the image-wide point hash holds (record, axis, v)
+//   FK_IVN      n >= 2 sorted disjoint intervals (lo, hi) at word B of the blob
+//   FK_PTN      n >= 2 sorted points at word B
+//   FK_MKN      n single-term boxes (kBoxWords each: value at +0, mask at +3) at word B
+// Clause data (the segment lists) starts at word kRecLine. Arrays a descriptor points at are
+// followed by at least 4 readable words (chunks are read 16 B at a time).
+enum FastKind : uint32_t { FK_GENERIC = 0, FK_ALWAYS = 1, FK_IV1 = 2, FK_MK1 = 3, FK_HASH = 4, FK_IVN = 5, FK_PTN = 6, FK_MKN = 7 };
+constexpr uint32_t kRecFcd = 6;
+constexpr uint32_t kRecLine = 16;
 
 constexpr int kMaxClauses = 3;
 constexpr int kIdxPerClause = 5;  // sub-indexes (axis, band) per driver clause (more -> always list)
@@ -112,10 +128,26 @@ GPC_HD uint32_t ent_off(uint32_t x) { return (x >> 8) << 4; }
 
 struct SubIdx {  // one (axis, band) bucket index of a driver clause
   uint8_t axis, band, bits, reserved;
-  uint32_t off;  // word offset of 2^bits + 1 bucket offsets (in entries, relative to `ent`)
-  uint32_t ent;  // word offset (multiple of 4) of the Ent entries, ascending record offset per bucket
+  uint32_t off;   // word offset of 2^bits + 1 bucket offsets (in entries, relative to `ent`)
+  uint32_t ent;   // word offset (multiple of 4) of the Ent entries, ascending record offset per bucket
+  uint32_t pres;  // composite sub-indexes: word offset of a 2^bits-bit map of the non-empty buckets
+                  // (0: none). It is small enough to stay in L2 (C3: 256 KB per sub-index) and most
+                  // buckets are empty (C3: 72-81 %), so the offset pair -- a random line of a
+                  // 25 MB array -- is fetched only for the ~1/4 of the probes that can list a rule.
 };
 
+// An inline hard pseudo-rule (TableHdr.hf): its record's fast descriptors, plus the two (value,
+// mask) terms of an FK_MK2 clause (two single-term boxes, e.g. the ct_state bypass flows
+// ct_state=-new+est / -new+rel).
+constexpr uint32_t kHardFast = 2;
+constexpr uint32_t FK_MK2 = 8;  // HardFast only: (v & mk[1]) == mk[0] || (v & mk[3]) == mk[2]
+struct HardFast {
+  uint32_t pv;    // priority | verdict << 16 | n_clauses << 24
+  uint32_t roff;  // record offset (rank bound of the soft scan; point-hash key)
+  uint32_t rid;   // rule id (tombstones of delta epochs)
+  uint32_t d[3 * kMaxClauses];
+  uint32_t mk[4];
+};
 struct TableHdr {
   uint32_t n_rules, n_hard;
   uint32_t hard_off;  // record offsets of the hard pseudo-rules (ascending)
@@ -134,6 +166,11 @@ struct TableHdr {
   uint32_t xmap_off;  // 2^16-bit map of the cx values any soft rule holds (cx_bit): a packet whose
                       // value is absent has no soft candidate at all (one load, L2-resident)
   SubIdx cidx[kIdxPerClause];
+  // Hard pseudo-rules inline (round 4): when the table has at most kHardFast of them and every
+  // clause has a one-word fast kind, their descriptors live here and the hard match is decided
+  // from the header (scalar loads) without reading any record; n_hfast = 0: the record loop.
+  uint32_t n_hfast;
+  HardFast hf[kHardFast];
 };
 
 struct ImageHdr {
@@ -144,6 +181,7 @@ struct ImageHdr {
   uint32_t v6_lpm;      // IPv6 image: word offset of its V6Lpm block (0 in IPv4 images)
   uint32_t isc;         // IngressSecurityClassifier bypasses installed (kIsc* bits)
   uint32_t bloom_axes;  // bit a: some driver entry tests the Bloom bits of axis a (Pkt::fm[a] is needed)
+  uint32_t live;        // bit t - 1: table t has rules (hard or soft); an empty table is a miss
 };
 // IngressSecurityClassifier (pipeline.go:2144-2182), from the installed flows: bit d (gpc_dest d =
 // gateway 1, tunnel 2, uplink 3) -- packets to that destination skip to IngressMetric; kIscHairpin
@@ -291,6 +329,35 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 #else
 #define GPC_STAT(i, v) ((void)0)
 #define GPC_TOUCH(p, n) ((void)0)
+#endif
+
+// Region stamps (diagnostic builds only, -DGPC_STAMPS; tools/stamps.py): from GPC_MARK(r) on, the
+// wave's s_memtime cycles are charged to region r; the kernel adds each wave's totals to
+// gpc_stamp_acc. Never defined in the product build.
+enum StampRegion : uint32_t { ST_PRE = 0, ST_HARD, ST_DRV, ST_SCAN, ST_VER, ST_TAIL, ST_FIN, ST_WALK, ST_POST, ST_N };
+#if defined(GPC_STAMPS) && defined(__HIPCC__)
+extern __device__ unsigned long long gpc_stamp_acc[32];
+__device__ __forceinline__ uint32_t* gpc_stamp_lds() {
+  __shared__ uint32_t st[ST_N + 3];  // per region cycles, current region, last time (lo, hi)
+  return st;
+}
+__device__ __forceinline__ void gpc_mark(uint32_t r) {
+  const uint64_t now = __builtin_amdgcn_s_memtime();
+  const unsigned long long act = __ballot(1);
+  if (__lane_id() == uint32_t(__ffsll((long long)act) - 1)) {
+    uint32_t* st = gpc_stamp_lds();
+    const uint64_t last = uint64_t(st[ST_N + 1]) | (uint64_t(st[ST_N + 2]) << 32);
+    st[st[ST_N]] += uint32_t(now - last);
+    st[ST_N] = r;
+    st[ST_N + 1] = uint32_t(now);
+    st[ST_N + 2] = uint32_t(now >> 32);
+  }
+}
+#endif
+#if defined(GPC_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define GPC_MARK(r) gpc_mark(r)
+#else
+#define GPC_MARK(r) ((void)0)
 #endif
 
 // ------------------------------------------------------------------------------ IPv6 interning
@@ -701,6 +768,25 @@ GPC_HD RecHdr load_rec_hdr(const uint32_t* rec) {
 #endif
   return h;
 }
+// A record's first line: header and fast descriptors (words 0-14) in one round of 16-B loads, so
+// the verification needs no further dependent load for its one-word clause kinds.
+struct RecLine {
+  uint32_t w[kRecLine];
+};
+GPC_HD RecLine load_rec_line(const uint32_t* rec) {
+  RecLine h;
+#if defined(__HIPCC__)
+  const uint4* q = reinterpret_cast<const uint4*>(rec);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint4 a = q[j];
+    h.w[4 * j] = a.x, h.w[4 * j + 1] = a.y, h.w[4 * j + 2] = a.z, h.w[4 * j + 3] = a.w;
+  }
+#else
+  for (uint32_t i = 0; i < kRecLine; i++) h.w[i] = rec[i];
+#endif
+  return h;
+}
 
 // Both buckets are loaded before either is compared (two independent 16-B loads).
 GPC_HD bool hash_contains(const Img& im, uint64_t key) {
@@ -795,23 +881,125 @@ GPC_HD bool clause_match(const Img& im, uint32_t roff, const W* c, const Pkt& p)
   return false;
 }
 
-// All clauses of a record; clause `last` (the driver, already a likely hit) is checked last
-// (last >= n_clauses: natural order). One clause_match call site keeps the code small.
-// `skip`: clauses already decided (the entry's exact interval test). (Loading every clause's first
-// four words in one round and deciding one-segment clauses from them measured slower on MI355X:
-// C2 10.22 -> 10.80 ms, C3 10.12 -> 10.24, profiles/r03k_clause_fast.txt.)
+// Four consecutive words at a dword-aligned address as one 16-B load (gfx950 allows dword-aligned
+// multi-dword global loads).
+template <typename W>
+GPC_HD void load_quad(const W* p, uint32_t* w) {
+#if defined(__HIPCC__)
+  struct Q {
+    uint32_t a, b, c, d;
+  } q;
+  __builtin_memcpy(&q, (const void*)p, 16);
+  w[0] = q.a, w[1] = q.b, w[2] = q.c, w[3] = q.d;
+#else
+  for (int i = 0; i < 4; i++) w[i] = p[i];
+#endif
+}
+
+// All clauses of a record (AND), from the fast descriptors of its first line: the one-word kinds
+// are decided with compares, the array kinds by one lock-step search over the (at most three)
+// clauses -- binary steps while a clause's window is longer than one 16-B chunk, then one chunk
+// compare -- so a verification is one round of descriptor loads plus a few rounds of 16-B loads,
+// with loop trip counts uniform over the wavefront and branch-free bodies (the round-3 segment
+// interpreter spent most of C1's time on exec-mask bookkeeping). FK_GENERIC clauses (rare) fall
+// back to clause_match. `dsc`: the record's nine descriptor words (already loaded with its first
+// line); `skip`: clauses already decided by the driver entry. W: uint32_t, or cword for records
+// read at a wave-uniform address (hard pseudo-rules).
 template <typename W = uint32_t>
-GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, uint32_t last, uint32_t skip, const Pkt& p) {
-  const uint32_t roff = uint32_t(rec - (const W*)im.blob);
+GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, const uint32_t* dsc, uint32_t skip, const Pkt& p) {
+  const W* blob = (const W*)im.blob;
   const uint32_t ncl = rec_nclauses(w2);
-  const uint32_t first = last < ncl ? last + 1 : 0;
-  for (uint32_t j = 0; j < ncl; j++) {
-    uint32_t k = first + j;
-    if (k >= ncl) k -= ncl;
-    if ((skip >> k) & 1u) continue;
-    if (!clause_match(im, roff, rec + rec_off(w2, k), p)) return false;
+  bool ok = true;
+  uint32_t gen = 0, hsh = 0;
+  uint32_t x[kMaxClauses], l[kMaxClauses], h[kMaxClauses], base[kMaxClauses], kd[kMaxClauses];
+#pragma unroll
+  for (int k = 0; k < kMaxClauses; k++) {
+    const uint32_t A = dsc[3 * k], B = dsc[3 * k + 1], C = dsc[3 * k + 2];
+    const bool need = uint32_t(k) < ncl && !((skip >> k) & 1u);
+    const uint32_t kind = need ? (A & 15u) : uint32_t(FK_ALWAYS);
+    const uint32_t v = p.ax[(A >> 4) & 15u];
+    x[k] = v;
+    kd[k] = kind;
+    base[k] = B;
+    l[k] = 0;
+    h[k] = kind >= FK_IVN ? (A >> 8) : 0u;
+    const bool r = kind == FK_IV1 ? (B <= v) & (v <= C) : kind == FK_MK1 ? (v & C) == B : true;
+    ok = ok & r;
+    gen |= kind == FK_GENERIC ? 1u << k : 0u;
+    hsh |= kind == FK_HASH ? 1u << k : 0u;
   }
-  return true;
+  // point-hash clauses (large exact-value sets): both buckets loaded before either compare
+  if (GPC_WAVE_ANY(ok & (hsh != 0u))) {
+    const uint32_t roff = uint32_t(rec - blob);
+#pragma unroll
+    for (int k = 0; k < kMaxClauses; k++)
+      if (ok & ((hsh >> k) & 1u)) ok = hash_contains(im, point_key(roff, (dsc[3 * k] >> 4) & 15u, x[k]));
+  }
+  // array clauses: window [l, h) of elements still to look at, per clause, in lock step
+  while (GPC_WAVE_ANY(ok & ((h[0] > l[0]) | (h[1] > l[1]) | (h[2] > l[2])))) {
+#pragma unroll
+    for (int k = 0; k < kMaxClauses; k++) {
+      const bool live = ok & (h[k] > l[k]);
+      const uint32_t kind = kd[k];
+      const uint32_t stride = kind == FK_IVN ? 2u : kind == FK_PTN ? 1u : kBoxWords;
+      const uint32_t cap = kind == FK_IVN ? 2u : kind == FK_PTN ? 4u : 1u;  // elements per 16-B chunk
+      const bool bin = live & (kind != FK_MKN) & (h[k] - l[k] > cap);
+      const uint32_t mid = (l[k] + h[k]) >> 1;
+      const uint32_t pos = bin ? mid : l[k];
+      const W* q = blob + (live ? base[k] + stride * pos : 0u);  // idle lanes read word 0 (a valid line)
+      GPC_TOUCH(q, 16);
+      uint32_t w[4];
+      load_quad(q, w);
+      const uint32_t v = x[k], n = h[k] - l[k];
+      // binary step: the last element whose low end is <= v stays in the window
+      const bool le = w[0] <= v;
+      // chunk compare over the window (at most cap elements)
+      const bool hit = kind == FK_IVN   ? ((w[0] <= v) & (v <= w[1])) | ((n > 1u) & (w[2] <= v) & (v <= w[3]))
+                       : kind == FK_PTN ? (w[0] == v) | ((n > 1u) & (w[1] == v)) | ((n > 2u) & (w[2] == v)) | ((n > 3u) & (w[3] == v))
+                                        : (v & w[3]) == w[0];
+      const bool fin = live & !bin & (hit | (kind != FK_MKN) | (n <= 1u));  // this clause is settled
+      if (bin) {
+        l[k] = le ? mid : l[k];
+        h[k] = le ? h[k] : mid;
+      }
+      if (live & !bin) {
+        ok = ok & (hit | !fin);
+        l[k] = fin ? h[k] : l[k] + 1u;  // MKN without a hit: next box
+      }
+    }
+  }
+  // clauses the descriptors cannot express: the segment interpreter
+  if (GPC_WAVE_ANY(ok & (gen != 0u))) {
+    if (ok & (gen != 0u)) {
+      const uint32_t roff = uint32_t(rec - blob);
+      for (uint32_t k = 0; k < ncl; k++)
+        if ((gen >> k) & 1u) ok = ok && clause_match(im, roff, rec + rec_off(w2, k), p);
+    }
+  }
+  return ok;
+}
+
+// An inline hard pseudo-rule (TableHdr.hf) against the packet: descriptor kinds are uniform, so
+// the only per-lane work is the compares (and the point-hash probe of an FK_HASH clause).
+GPC_HD bool hard_fast_match(const Img& im, const HardFast& hf, const Pkt& p) {
+  const uint32_t ncl = hf.pv >> 24;
+  bool ok = true;
+#pragma unroll
+  for (uint32_t k = 0; k < uint32_t(kMaxClauses); k++) {
+    if (k >= ncl) break;
+    const uint32_t A = hf.d[3 * k], B = hf.d[3 * k + 1], C = hf.d[3 * k + 2], kind = A & 15u;
+    const uint32_t v = p.ax[(A >> 4) & 15u];
+    if (kind == FK_HASH) {
+      ok = ok & hash_contains(im, point_key(hf.roff, (A >> 4) & 15u, v));
+    } else {
+      const bool r = kind == FK_IV1 ? (B <= v) & (v <= C)
+                     : kind == FK_MK1 ? (v & C) == B
+                     : kind == FK_MK2 ? ((v & hf.mk[1]) == hf.mk[0]) | ((v & hf.mk[3]) == hf.mk[2])
+                                      : true;
+      ok = ok & r;
+    }
+  }
+  return ok;
 }
 
 GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
@@ -928,6 +1116,7 @@ GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const ui
 // One rule table (table = 1..6). All per-list merge state is indexed with compile-time indices
 // only (unrolled), so it stays in VGPRs.
 GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
+  GPC_MARK(ST_HARD);
   const TableHdr& th = im.hdr->t[table - 1];
   TablePart res;
   res.h = res.s = res.win = 0;
@@ -936,26 +1125,49 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   // (wave-uniform: the list, the records and their clause data are read with scalar loads)
   uint32_t rH = th.end_off;
   uint32_t hprio = 0, hverdict = RV_MISS;
-  const cword* cblob = (const cword*)im.blob;
-  const cword* hard = cblob + th.hard_off;
-  for (uint32_t h = 0; h < th.n_hard; h++) {
-    GPC_TOUCH(&hard[h], 4);
-    const uint32_t off = hard[h];
-    const cword* rec = cblob + off;
-    GPC_TOUCH(rec, 4 * kRecHdrWords);
-    const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
-    if (rule_dead(im, rid)) continue;
-    if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
-      if ((w1 & 0xffffu) != hprio) break;
-      if (rec_verdict(w2) != hverdict && rule_match(im, rec, w2, 3, 0, p)) htie = kHTie;
-      continue;
+  if (th.n_hfast) {
+    // inline hard rules, rank order; branch-free per lane (a tie among hard flows of equal priority
+    // and different verdicts; lower-priority ones after the first match do not count)
+    bool stop = false;
+    for (uint32_t h = 0; h < th.n_hfast; h++) {
+      const HardFast& hf = th.hf[h];
+      if (rule_dead(im, hf.rid)) continue;
+      const uint32_t prio = hf.pv & 0xffffu, verdict = (hf.pv >> 16) & 0xffu;
+      const bool m = hard_fast_match(im, hf, p);
+      const bool found = rH != th.end_off;
+      stop = stop | (found & (prio != hprio));
+      htie = (!stop & found & (verdict != hverdict) & m) ? kHTie : htie;
+      const bool take = !found & m;
+      rH = take ? hf.roff : rH;
+      hprio = take ? prio : hprio;
+      hverdict = take ? verdict : hverdict;
     }
-    if (rule_match(im, rec, w2, 3, 0, p)) {
-      rH = off;
-      hprio = w1 & 0xffffu;
-      hverdict = rec_verdict(w2);
+  } else {
+    const cword* cblob = (const cword*)im.blob;
+    const cword* hard = cblob + th.hard_off;
+    for (uint32_t h = 0; h < th.n_hard; h++) {
+      GPC_TOUCH(&hard[h], 4);
+      const uint32_t off = hard[h];
+      const cword* rec = cblob + off;
+      GPC_TOUCH(rec, 4 * kRecLine);
+      const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
+      if (rule_dead(im, rid)) continue;
+      uint32_t dsc[3 * kMaxClauses];
+#pragma unroll
+      for (int j = 0; j < 3 * kMaxClauses; j++) dsc[j] = rec[kRecFcd + j];
+      if (rH != th.end_off) {  // tie among hard flows of equal priority and different verdicts
+        if ((w1 & 0xffffu) != hprio) break;
+        if (rec_verdict(w2) != hverdict && rule_match(im, rec, w2, dsc, 0u, p)) htie = kHTie;
+        continue;
+      }
+      if (rule_match(im, rec, w2, dsc, 0u, p)) {
+        rH = off;
+        hprio = w1 & 0xffffu;
+        hverdict = rec_verdict(w2);
+      }
     }
   }
+  GPC_MARK(ST_DRV);
   const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
   if (th.n_cidx == 0 && n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
     if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
@@ -976,16 +1188,32 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     const bool xin = (im.blob[th.xmap_off + (xb >> 5)] >> (xb & 31u)) & 1u;  // else no soft rule can match
     always_n = xin ? th.always_n[d] : 0u;
     uint32_t cnt = always_n;
+    // presence words (L2-resident) are read in the value-map word's round; an offset pair only
+    // for a present bucket of a packet whose value is in the map
+    uint32_t bk[kIdxPerClause], pw[kIdxPerClause];
+#pragma unroll
+    for (int i = 0; i < kIdxPerClause; i++) {
+      bk[i] = pw[i] = 0;
+      if (uint32_t(i) < nc) {
+        const SubIdx& si = th.cidx[i];
+        bk[i] = cbucket_of(si.band, si.bits, p.ax[si.axis], xv);
+        if (si.pres) {
+          GPC_TOUCH(im.blob + si.pres + (bk[i] >> 5), 4);
+          pw[i] = im.blob[si.pres + (bk[i] >> 5)];
+        } else {
+          pw[i] = ~0u;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < kIdxPerClause; i++) {
       lo0[i] = hi0[i] = lo1[i] = hi1[i] = 0;
-      if (uint32_t(i) < nc && xin) {
+      if ((uint32_t(i) < nc) & xin & ((pw[i] >> (bk[i] & 31u)) & 1u)) {
         const SubIdx& si = th.cidx[i];
-        const uint32_t b = cbucket_of(si.band, si.bits, p.ax[si.axis], xv);
         const uint32_t* o = im.blob + si.off;
-        GPC_TOUCH(o + b, 8);
+        GPC_TOUCH(o + bk[i], 8);
         uint32_t ob, oe;
-        load_pair(o + b, &ob, &oe);
+        load_pair(o + bk[i], &ob, &oe);
         lo0[i] = si.ent / 4 + ob;
         hi0[i] = si.ent / 4 + oe;
         cnt += hi0[i] - lo0[i];
@@ -1052,16 +1280,18 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   while (!done) {
     uint32_t c0, c1;
     bool more;
+    GPC_MARK(ST_SCAN);
     if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, c0, c1, more);
     else scan_lists<kLists>(im, p, dl, upto, total, after, rH, c0, c1, more);
+    GPC_MARK(ST_VER);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
       const uint32_t off = q ? c1 : c0;
       if (off == 0xffffffffu || done) break;
       after = off;
       const uint32_t* rec = im.blob + off;
-      GPC_TOUCH(rec, 4 * kRecHdrWords);
-      const RecHdr hd = load_rec_hdr(rec);
+      GPC_TOUCH(rec, 4 * kRecLine);
+      const RecLine hd = load_rec_line(rec);
       const uint32_t w1 = hd.w[1], w2 = hd.w[2];
       const uint32_t prio = w1 & 0xffffu;
       if (prio != level) {
@@ -1074,7 +1304,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       }
       GPC_STAT(3, 1);
       const uint32_t rid = hd.w[4] >> 8;
-      if (rule_dead(im, rid) || !rule_match(im, rec, w2, d, (hd.w[5] >> (3 * d)) & 7u, p)) {
+      if (rule_dead(im, rid) || !rule_match(im, rec, w2, &hd.w[kRecFcd], (hd.w[5] >> (3 * d)) & 7u, p)) {
         GPC_STAT(5, 1);
         continue;
       }
@@ -1093,6 +1323,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     }
     if (!more) done = true;
   }
+  GPC_MARK(ST_TAIL);
   if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
   if (have) {
     res.s = level | kSHave | noact | (level_done > 1 ? kSTie : 0u);
@@ -1142,6 +1373,7 @@ GPC_HD TablePart combine_parts(const View& v, const TablePart& a, TablePart b) {
 }
 
 GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_blob, const TablePart& q) {
+  GPC_MARK(ST_FIN);
   TableResult res;
   res.verdict = RV_MISS;
   res.tie = (q.h & kHTie) ? 1 : 0;
@@ -1192,14 +1424,15 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
   for (uint32_t h = 0; h < jt.n_hard; h++) {
     const uint32_t off = pool[jt.hard_off + h];
     const uint32_t* rec = pool + off;
-    const uint32_t w1 = rec[1], w2 = rec[2], rid = rec[4] >> 8;
+    const RecLine hd = load_rec_line(rec);
+    const uint32_t w1 = hd.w[1], w2 = hd.w[2], rid = hd.w[4] >> 8;
     if (rule_dead(im, rid)) continue;
     if (hfound) {
       if ((w1 & 0xffffu) != hprio) break;
-      if (rec_verdict(w2) != hverdict && rule_match(im, rec, w2, 3, 0, p)) htie = kHTie;
+      if (rec_verdict(w2) != hverdict && rule_match(im, rec, w2, &hd.w[kRecFcd], 0u, p)) htie = kHTie;
       continue;
     }
-    if (rule_match(im, rec, w2, 3, 0, p)) {
+    if (rule_match(im, rec, w2, &hd.w[kRecFcd], 0u, p)) {
       hfound = true;
       hprio = w1 & 0xffffu;
       hverdict = rec_verdict(w2);
@@ -1263,12 +1496,12 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
       if (!entry_pass(p, f)) continue;
       const uint32_t off = ew[3];
       const uint32_t* rec = pool + off;
-      GPC_TOUCH(rec, 4 * kRecHdrWords);
-      const RecHdr hd = load_rec_hdr(rec);
+      GPC_TOUCH(rec, 4 * kRecLine);
+      const RecLine hd = load_rec_line(rec);
       const uint32_t w1 = hd.w[1], w2 = hd.w[2];
       const uint32_t prio = w1 & 0xffffu, conj = hd.w[0];
       if (best && prio < best_prio) continue;  // cannot change the decision
-      if (!rule_match(im, rec, w2, d, 0, p)) continue;
+      if (!rule_match(im, rec, w2, &hd.w[kRecFcd], 0u, p)) continue;
       if (!best || prio > best_prio) {
         best = off;
         best_prio = prio;
@@ -1439,7 +1672,18 @@ GPC_HD StageOut walk_stage(const View& im, const Pkt& p, uint32_t t0, TraceStep*
   uint32_t conj = 0, ft = 0;  // ft = flags | tier << 8 (reg5/reg6 after a Pass keep its conj id and tier)
   for (uint32_t i = 0;; i++) {
     const uint32_t t = t0 + i;
+    // a table without rules (base-only epochs): a miss, without reading its header
+    if (!kJournal && !kTrace && !((im.base.hdr->live >> (t - 1)) & 1u)) {
+      if (i < 2) continue;
+      StageOut o;
+      o.slot = 0;
+      o.counted = 0;
+      o.v.conj = conj;
+      o.v.packed = pack_verdict(1 /*NO_MATCH*/, 0, ft >> 8, ft & 0xffu);
+      return o;
+    }
     const TableResult r = eval_table<kJournal>(im, t, p);
+    GPC_MARK(ST_WALK);
     if (kTrace && *n_trace < kMaxTraceSteps) {
       TraceStep& st = trace[(*n_trace)++];
       st.table = t;

@@ -536,6 +536,62 @@ std::vector<uint32_t> encode_clause(const std::vector<PendingSeg>& segs, std::ve
   return w;
 }
 
+// Fast descriptor (core.hpp FastKind) of a clause encoded by encode_clause. `data` tells where word
+// B must point: -1 nowhere (B holds a value), 0 the first data word of the clause's single inline
+// segment (clause-relative word 2), 1 its external data (B is patched like the clause's pointer).
+struct Fcd {
+  uint32_t a = FK_GENERIC, b = 0, c = 0;
+  int data = -1;
+};
+Fcd fast_clause(const std::vector<PendingSeg>& segs) {
+  Fcd f;
+  if (segs.size() != 1) return f;  // several segments: the interpreter
+  const PendingSeg& s = segs[0];
+  const uint32_t ax = uint32_t(s.axis) << 4;
+  const bool external = (s.kind == SK_IVAL && s.n > kInlineIvals) || (s.kind == SK_PTS && s.n > kInlinePoints) ||
+                        (s.kind == SK_BOX && s.n > kInlineBoxes);
+  switch (s.kind) {
+    case SK_ALWAYS:
+      f.a = FK_ALWAYS;
+      return f;
+    case SK_HASH:
+      f.a = FK_HASH | ax;
+      return f;
+    case SK_IVAL:
+    case SK_PTS:
+      if (s.n == 1) {
+        f.a = FK_IV1 | ax;
+        f.b = s.data[0];
+        f.c = s.kind == SK_IVAL ? s.data[1] : s.data[0];
+        return f;
+      }
+      f.a = (s.kind == SK_IVAL ? FK_IVN : FK_PTN) | ax | (s.n << 8);
+      f.data = external ? 1 : 0;
+      return f;
+    case SK_BOX: {
+      // single-term boxes on one axis only (the ct_state bypass flows, masked tun_id / ports)
+      uint32_t axis0 = 0xffu;
+      for (uint32_t i = 0; i < s.n; i++) {
+        const uint32_t meta = s.data[kBoxWords * i + 6];
+        if ((meta >> 24) != 1u) return f;
+        if (axis0 != 0xffu && (meta & 0xffu) != axis0) return f;
+        axis0 = meta & 0xffu;
+      }
+      if (s.n == 1) {
+        f.a = FK_MK1 | (axis0 << 4);
+        f.b = s.data[0];
+        f.c = s.data[3];
+        return f;
+      }
+      f.a = FK_MKN | (axis0 << 4) | (s.n << 8);
+      f.data = external ? 1 : 0;
+      return f;
+    }
+    default:
+      return f;
+  }
+}
+
 // Image blob (uint32 words) ------------------------------------------------------------------------
 struct Blob {
   std::vector<uint32_t> w;
@@ -963,6 +1019,14 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       si.bits = uint8_t(bits);
       si.off = B.put(offs.data(), offs.size(), 16);
       si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
+      si.pres = 0;
+      if (!std::getenv("GPC_NO_PRESENCE")) {  // core.hpp SubIdx.pres (GPC_NO_PRESENCE: experiments)
+        std::vector<uint32_t> pres(nb / 32, 0u);
+        for (uint32_t b = 0; b < nb; b++)
+          if (offs[b + 1] > offs[b]) pres[b >> 5] |= 1u << (b & 31u);
+        si.pres = B.put(pres.data(), pres.size(), 16);
+        out->bytes_bucket_offsets += 4ull * pres.size();
+      }
       out->bytes_bucket_offsets += 4ull * offs.size();
       out->bytes_entries += 4ull * ents.size();
       if (std::getenv("GPC_IMAGE_DEBUG"))
@@ -1715,8 +1779,9 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       }
       const uint32_t orid = n_versions++;
       // record: header, clauses, then this record's out-of-line segment data
-      std::vector<uint32_t> rec(kRecHdrWords, 0u), ext;
+      std::vector<uint32_t> rec(kRecLine, 0u), ext;
       std::vector<std::pair<uint32_t, uint32_t>> patches;  // (record word, ext offset)
+      std::vector<std::pair<uint32_t, uint32_t>> inl;      // (record word, record word of the data)
       uint32_t offs[3] = {0, 0, 0};
       for (int k = 0; k < r.n; k++) {
         std::vector<PendingSeg> ps;
@@ -1731,14 +1796,28 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
         }
         offs[k] = uint32_t(rec.size());
         for (auto& pt : cp) patches.push_back({uint32_t(rec.size()) + pt.first, pt.second});
+        const Fcd f = fast_clause(ps);  // fast descriptor (core.hpp FastKind)
+        rec[kRecFcd + 3 * k] = f.a;
+        rec[kRecFcd + 3 * k + 1] = f.b;
+        rec[kRecFcd + 3 * k + 2] = f.c;
+        if (f.data == 0) inl.push_back({kRecFcd + 3 * uint32_t(k) + 1, offs[k] + 2});
+        if (f.data == 1) {
+          if (cp.size() != 1) {
+            *err = "fast clause descriptor: external segment without its patch";
+            return -GPC_EINVAL;
+          }
+          patches.push_back({kRecFcd + 3 * uint32_t(k) + 1, cp[0].second});
+        }
         rec.insert(rec.end(), cw.begin(), cw.end());
       }
       while (rec.size() % 16) rec.push_back(0u);
       const uint32_t ext_at = uint32_t(rec.size());
       rec.insert(rec.end(), ext.begin(), ext.end());
+      for (int i = 0; i < 4; i++) rec.push_back(0u);  // 16-B chunk reads past the last array (core.hpp rule_match)
       while (pool.size() % 16) pool.push_back(0u);
       const uint32_t base_off = uint32_t(pool.size());
       for (auto& pt : patches) rec[pt.first] = base_off + ext_at + pt.second;
+      for (auto& pt : inl) rec[pt.first] = base_off + pt.second;
       rec[0] = r.hard ? 0u : r.conj_id;
       rec[1] = uint32_t(r.prio) | (uint32_t(r.act_prio) << 16);
       uint32_t slot = 0;
@@ -1840,6 +1919,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
   auto& counted_allow = G.counted_allow;
   auto& counted_deny = G.counted_deny;
   out->n_flows = G.n_flows;
+  out->hdr.live = 0;
   // ---- 2. per table: rank, emit records, driver indexes
   Blob B;
   B.w.reserve(1 << 20);
@@ -1870,6 +1950,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
     });
     TableHdr& th = out->hdr.t[t - 1];
     th.n_rules = uint32_t(rs.size());
+    if (!rs.empty()) out->hdr.live |= 1u << (t - 1);
     // value span of the exact axes over this table's soft rules (interval prefilter selectivity)
     uint64_t span[AX_N] = {0};
     {
@@ -1893,6 +1974,8 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
     std::vector<uint32_t> ext;
     std::vector<std::pair<uint32_t, uint32_t>> abs_patches;  // (absolute record word, ext offset)
     std::vector<uint32_t> hard_offs;
+    std::vector<HardFast> hard_fast;
+    bool hard_fits = true;
     for (size_t rank = 0; rank < rs.size(); rank++) {
       RuleB& r = *rs[rank];
       uint32_t rid = next_rid++;
@@ -1904,19 +1987,26 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
       std::vector<std::vector<uint32_t>> cw(r.n);
       std::vector<std::vector<std::pair<uint32_t, uint32_t>>> cp(r.n);
       std::vector<PendingSeg> hsegs;  // point-hash segments: keys need the record offset
+      Fcd fcd[3];
+      uint32_t mk2[3][4] = {};  // FK_MKN with two boxes: their (value, mask) terms (inline hard rules)
       for (int k = 0; k < r.n; k++) {
         std::vector<PendingSeg> ps;
         clause_segments(r.clause[k], &ps);
         for (auto& sg : ps)
           if (sg.kind == SK_HASH) hsegs.push_back(sg);
         cw[k] = encode_clause(ps, &ext, &cp[k]);
+        fcd[k] = fast_clause(ps);
+        if ((fcd[k].a & 15u) == FK_MKN && (fcd[k].a >> 8) == 2u) {
+          const std::vector<uint32_t>& bx = ps[0].data;
+          mk2[k][0] = bx[0], mk2[k][1] = bx[3], mk2[k][2] = bx[kBoxWords], mk2[k][3] = bx[kBoxWords + 3];
+        }
       }
       std::vector<int> order(r.n);
       for (int k = 0; k < r.n; k++) order[k] = k;
       std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cw[a].size() < cw[b].size(); });
       B.align(16);
       uint32_t base = uint32_t(B.w.size());
-      std::vector<uint32_t> rec(kRecHdrWords, 0);
+      std::vector<uint32_t> rec(kRecLine, 0);
       uint32_t offs[3] = {0, 0, 0};
       for (int k : order) {
         if (rec.size() > 255) {
@@ -1926,6 +2016,18 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         offs[k] = uint32_t(rec.size());
         for (auto& pt : cp[k]) abs_patches.push_back({base + uint32_t(rec.size()) + pt.first, pt.second});
         rec.insert(rec.end(), cw[k].begin(), cw[k].end());
+      }
+      for (int k = 0; k < r.n; k++) {  // fast descriptors (core.hpp FastKind)
+        rec[kRecFcd + 3 * k] = fcd[k].a;
+        rec[kRecFcd + 3 * k + 1] = fcd[k].data == 0 ? base + offs[k] + 2 : fcd[k].b;
+        rec[kRecFcd + 3 * k + 2] = fcd[k].c;
+        if (fcd[k].data == 1) {
+          if (cp[k].size() != 1) {
+            out->error = "fast clause descriptor: external segment without its patch";
+            return -GPC_EINVAL;
+          }
+          abs_patches.push_back({base + kRecFcd + 3 * uint32_t(k) + 1, cp[k][0].second});
+        }
       }
       rec[0] = r.hard ? 0 : r.conj_id;
       rec[1] = uint32_t(r.prio) | (uint32_t(r.act_prio) << 16);
@@ -1946,6 +2048,25 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         for (uint32_t v : sg.data) hash_keys.push_back(point_key(base, sg.axis, v));
       B.w.insert(B.w.end(), rec.begin(), rec.end());
       if (r.hard) {
+        // inline copy for TableHdr.hf (core.hpp HardFast), if every clause has a one-word kind
+        HardFast hf{};
+        bool fits = true;
+        int n_mk2 = 0;
+        hf.pv = uint32_t(r.prio) | ((uint32_t(r.verdict) & 0xffu) << 16) | (uint32_t(r.n) << 24);
+        hf.roff = base;
+        hf.rid = rid;
+        for (int k = 0; k < r.n; k++) {
+          const uint32_t kind = fcd[k].a & 15u;
+          hf.d[3 * k] = fcd[k].a, hf.d[3 * k + 1] = fcd[k].b, hf.d[3 * k + 2] = fcd[k].c;
+          if (kind == FK_MKN && (fcd[k].a >> 8) == 2u && n_mk2++ == 0) {
+            hf.d[3 * k] = (fcd[k].a & 0xf0u) | FK_MK2;
+            for (int j = 0; j < 4; j++) hf.mk[j] = mk2[k][j];
+          } else if (kind != FK_ALWAYS && kind != FK_IV1 && kind != FK_MK1 && kind != FK_HASH) {
+            fits = false;
+          }
+        }
+        hard_fast.push_back(hf);
+        hard_fits = hard_fits && fits;
         hard_offs.push_back(base);
         out->hard_rids[t - 1].push_back(rid);
       } else {
@@ -1962,6 +2083,11 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
     for (auto& pt : abs_patches) B.w[pt.first] = ext_base + pt.second;
     th.n_hard = uint32_t(hard_offs.size());
     th.hard_off = hard_offs.empty() ? 0 : B.put(hard_offs.data(), hard_offs.size(), 1);
+    th.n_hfast = 0;
+    if (hard_fits && !hard_fast.empty() && hard_fast.size() <= kHardFast && !std::getenv("GPC_NO_HARD_INLINE")) {
+      th.n_hfast = uint32_t(hard_fast.size());
+      for (size_t h = 0; h < hard_fast.size(); h++) th.hf[h] = hard_fast[h];
+    }
     T_.lap(1);
     // composite driver first: a table that has one never scans the plain sub-indexes, so they are
     // not emitted (only the always lists, which the composite driver scans too)
@@ -2045,6 +2171,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         si.bits = uint8_t(bits);
         si.off = B.put(offs.data(), offs.size(), 16);
         si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
+        si.pres = 0;
         out->bytes_bucket_offsets += 4ull * offs.size();
         if (std::getenv("GPC_IMAGE_DEBUG"))
           std::fprintf(stderr, "table %d clause %d axis %u band %u bits %u atoms %zu entries %zu\n", t, k, axis, band, bits,
