@@ -55,7 +55,9 @@ struct StreamScratch {  // device scratch of the packet grouping pre-pass on one
   uint8_t* p = nullptr;
   size_t bytes = 0;
   hipEvent_t done = nullptr;  // recorded after the last launch that used it
+  uint32_t small = 0;         // consecutive calls that needed < 1/8 of it (shrink hysteresis)
 };
+constexpr uint32_t kScratchShrinkAfter = 64;  // that many small calls in a row release the buffer
 constexpr size_t kScratchStreams = 8;  // idle buffers of other streams are released past this many
 
 // Key of the per-stream state (grouping scratch, epoch lifetime events, gpc_stream_epoch). The
@@ -98,6 +100,7 @@ struct DevEpoch {
   std::shared_ptr<DevImage> v6_pool;    // journal pool of that base (append-only)
   uint32_t v6_jhdr = 0;                 // this epoch's IPv6 JournalHdr (0: base only)
   uint32_t v6_lpm = 0;                  // its ImageHdr.v6_lpm
+  uint64_t base_gen = 0, v6_gen = 0;    // host base generation (gpc_ctx gen4 / gen6) base / v6 mirror
   uint64_t epoch = 0;
   std::map<StreamKey, hipEvent_t> last_use;  // last launch on each stream that used this epoch
 };
@@ -178,6 +181,11 @@ struct gpc_ctx {
   Journal journal;   // delta epochs over `last` (host mirror of the device pools)
   Journal journal6;  // IPv6 delta epochs over `last6`
   uint64_t n_full6 = 0, n_delta6 = 0;
+  // Generation of the host base images (`last`, `last6`), bumped whenever one is replaced. A device
+  // slot extends its published base with journal tails only while the base it holds is of the
+  // current generation; otherwise (an earlier commit rebuilt the host base and then failed to
+  // upload it) the slot re-uploads the base and the whole journal.
+  uint64_t gen4 = 1, gen6 = 1;
   std::vector<DevState> dev;             // device slots (gpc_create: one, cfg.device)
   uint64_t cur_epoch = 0;                // epoch every slot currently publishes (0: nothing committed)
   uint32_t group_key = GPC_GROUP_KEY_AUTO;                            // gpc_group_key (gpc_create)
@@ -332,7 +340,10 @@ static uint32_t group_axes(const HostImage& h) {
   return m;
 }
 
+static std::atomic<int> g_fail_uploads{0};  // gpc_debug_fail_uploads (fault injection in tests)
+
 static int upload_image(const HostImage& h, int device, hipStream_t s, std::shared_ptr<DevImage>* out) {
+  if (g_fail_uploads.load() > 0 && g_fail_uploads.fetch_sub(1) > 0) return -GPC_EDEV;
   auto d = std::make_shared<DevImage>();
   d->s = s;
   d->device = device;
@@ -881,6 +892,11 @@ int gpc_commit(gpc_ctx* ctx) { return commit_impl(ctx, false); }
 // buffer is rebuilt from the host shadow state -- base image, journal pool, IPv6 and Service
 // images -- without compiler work; the realized flows, conj ids and counter slots are unchanged.
 // Device counters restart from zero, as OVS flow counters do after the flows are replayed.
+int gpc_debug_fail_uploads(int n) {
+  g_fail_uploads.store(n > 0 ? n : 0);
+  return GPC_OK;
+}
+
 int gpc_replay(gpc_ctx* ctx) {
   if (!ctx) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
@@ -908,13 +924,15 @@ int gpc_replay(gpc_ctx* ctx) {
     }
     ctx->cur_epoch = 0;
   }
+  int drop_rc = GPC_OK;  // every old slot is dropped even when one of them fails
   for (DevState& O : old) {
-    if (hip_ok(hipSetDevice(O.device))) return -GPC_EDEV;
+    if (hip_ok(hipSetDevice(O.device))) drop_rc = -GPC_EDEV;
     (void)hipDeviceSynchronize();  // may fail after a reset: the old buffers are dropped regardless
     (void)hipGetLastError();
     drop_slot(O);
     (void)hipGetLastError();
   }
+  if (drop_rc) return drop_rc;
   if (ctx->last.blob.empty()) return GPC_OK;  // nothing committed yet
   const size_t cap = std::max<size_t>(1, ctx->slots.size());
   const uint32_t copies = counter_copies_for(cap);
@@ -924,9 +942,14 @@ int gpc_replay(gpc_ctx* ctx) {
   int rc = GPC_OK;
   for (size_t k = 0; k < ctx->dev.size() && !rc; k++) {
     DevState& D = ctx->dev[k];
-    if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
-    if (!D.ustream && hip_ok(hipStreamCreateWithFlags(&D.ustream, hipStreamNonBlocking))) return -GPC_EDEV;
+    // (a failure leaves rc set: the cleanup below releases what earlier slots uploaded)
+    if (hip_ok(hipSetDevice(D.device)) || (!D.ustream && hip_ok(hipStreamCreateWithFlags(&D.ustream, hipStreamNonBlocking)))) {
+      rc = -GPC_EDEV;
+      break;
+    }
     hipStream_t us = D.ustream;
+    ne[k].base_gen = ctx->gen4;
+    ne[k].v6_gen = ctx->gen6;
     rc = upload_image(ctx->last, D.device, us, &ne[k].base);
     if (!rc && jn.active()) {
       rc = alloc_pool(D.device, us, &ne[k].pool);
@@ -1000,7 +1023,11 @@ static int group_scratch(DevState& D, hipStream_t s, size_t need, uint8_t** out)
     (void)hipGetLastError();
   }
   StreamScratch& sc = D.scratch[st];
-  if (sc.bytes < need || sc.bytes / 8 > need) {
+  // Grow at once; shrink only after kScratchShrinkAfter consecutive small calls, so alternating
+  // large and small batches on one stream never allocate on the data path.
+  sc.small = sc.bytes / 8 > need ? sc.small + 1 : 0;
+  if (sc.bytes < need || sc.small > kScratchShrinkAfter) {
+    sc.small = 0;
     dev_free(sc.p, s);  // after the launches already queued on s
     sc.p = nullptr;
     sc.bytes = 0;
@@ -1557,6 +1584,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       ctx->comp.discard = false;
       if (ctx->comp.rc == GPC_OK && !force_full && !ctx->np.foreign() && !discard) {
         ctx->last = std::move(*ctx->comp.base);
+        ctx->gen4++;
         ctx->journal = std::move(*ctx->comp.journal);
         ctx->journal.set_base(&ctx->last);
         bg_base = std::move(ctx->comp.dbase);
@@ -1597,6 +1625,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       rc = build_image(ctx->np, ctx->slots, &img);
       if (rc) return rc;
       ctx->last = std::move(img);
+      ctx->gen4++;
       ctx->journal.reset(&ctx->last);
       installed = false;
     }
@@ -1625,7 +1654,9 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     Journal& j6 = ctx->journal6;
     v6_full = force_full || classifier_changed || ctx->np.foreign() || ctx->last6.blob.empty() || !ctx->last6.codes6 ||
               j6.any_noact || j6.n_live > std::max(kDeltaMinRules, ctx->last6.conj_rid.size() / kDeltaFraction) ||
-              j6.pool.size() > kPoolWords * 7 / 8;
+              j6.pool.size() > kPoolWords * 7 / 8 ||
+              // every epoch that interns a prefix re-emits the whole overflow table
+              ctx->last6.v6_ovf.size() > std::max<size_t>(4096, size_t(ctx->last6.v6_prefixes) / 8);
     if (!v6_full) {
       std::string err;
       try {
@@ -1652,6 +1683,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
         img6.error = e;
       }
       ctx->last6 = std::move(img6);
+      ctx->gen6++;
       j6.reset(&ctx->last6);
       ctx->n_full6++;
     } else {
@@ -1689,6 +1721,8 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   const bool bg_ok = installed && bg_base.size() == nd && bg_pool.size() == nd;
   Journal& jn = ctx->journal;
   bool new_pool = false;
+  bool resync4 = false;  // some slot holds a base of an older host generation: every slot re-uploads
+  for (size_t k = 0; k < nd; k++) resync4 |= ctx->dev[k].cur.base && ctx->dev[k].cur.base_gen != ctx->gen4;
   for (size_t k = 0; k < nd; k++) {
     DevState& D = ctx->dev[k];
     if (hip_ok(hipSetDevice(D.device))) return fail(-GPC_EDEV);
@@ -1700,19 +1734,20 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       bg_pool[k]->s = us;
       ne[k].base = std::move(bg_base[k]);
       ne[k].pool = std::move(bg_pool[k]);
-    } else if (full || installed || !D.cur.base) {
+    } else if (full || installed || resync4 || !D.cur.base) {
       if ((rc = upload_image(ctx->last, D.device, us, &ne[k].base))) return fail(rc);
     } else {
       ne[k].base = D.cur.base;
       ne[k].pool = D.cur.pool;
     }
+    ne[k].base_gen = ctx->gen4;
     if (jn.active() && !ne[k].pool) {  // the journal pool of a new base is allocated on first use
       if ((rc = alloc_pool(D.device, us, &ne[k].pool))) return fail(rc);
       new_pool = true;
     }
   }
   if (bg_ok) jn.uploaded = bg_uploaded;
-  else if (full || installed || !ctx->dev[0].cur.base) jn.uploaded = 0;
+  else if (full || installed || resync4 || !ctx->dev[0].cur.base) jn.uploaded = 0;
   if (new_pool) jn.uploaded = 0;
   // Append-only: only the new journal tail travels, staged once in a pinned buffer and padded to at
   // least kMinUploadBytes (the padding lands in not-yet-used pool space) so the runtime takes the
@@ -1736,8 +1771,14 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   // the IPv6 journal tail (delta epochs), staged the same way; a new pool on every slot when the
   // IPv6 base is new or its journal starts (lockstep: every slot has the same IPv6 base)
   Journal& j6 = ctx->journal6;
+  // a slot whose IPv6 base is missing or of an older host generation gets the base and the whole
+  // IPv6 journal again (a full IPv6 rebuild whose upload failed must not be extended)
+  bool resync6 = false;
+  if (ctx->cfg.ipv6_enabled && !v6_full && !ctx->last6.blob.empty())
+    for (size_t k = 0; k < nd; k++) resync6 |= !ctx->dev[k].cur.v6 || ctx->dev[k].cur.v6_gen != ctx->gen6;
+  if (resync6) v6_changed = true;
   const bool j6_active = v6_changed && !v6_full && j6.active();
-  if (j6_active && !ctx->dev[0].cur.v6_pool) j6.uploaded = 0;
+  if (j6_active && (resync6 || !ctx->dev[0].cur.v6_pool)) j6.uploaded = 0;
   const size_t j6_from = j6.uploaded;
   const bool tail6 = j6_active && j6.pool.size() > j6.uploaded;
   size_t copy6_bytes = 0;
@@ -1763,11 +1804,22 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (tail && hip_ok(hipMemcpyAsync(ne[k].pool->d_blob + jn.uploaded, ctx->stage, copy_bytes, hipMemcpyHostToDevice, us)))
       return fail(-GPC_EDEV);
     ne[k].jhdr = jhdr;
-    if (!v6_full) {  // the IPv6 base stays; a delta extends its journal (new prefixes' LPM entries included)
+    if (resync6) {  // the current host IPv6 base, then the whole journal into a fresh pool
+      if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
+      ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
+      if (j6_active) {
+        if ((rc = alloc_pool(D.device, us, &ne[k].v6_pool))) return fail(rc);
+        if (tail6 && hip_ok(hipMemcpyAsync(ne[k].v6_pool->d_blob, ctx->stage6, copy6_bytes, hipMemcpyHostToDevice, us)))
+          return fail(-GPC_EDEV);
+        ne[k].v6_jhdr = ctx->journal6.hdr_off;
+      }
+      ne[k].v6_gen = ctx->gen6;
+    } else if (!v6_full) {  // the IPv6 base stays; a delta extends its journal (new prefixes' LPM entries included)
       ne[k].v6 = D.cur.v6;
       ne[k].v6_lpm = D.cur.v6_lpm;
       ne[k].v6_pool = D.cur.v6_pool;
       ne[k].v6_jhdr = D.cur.v6_jhdr;
+      ne[k].v6_gen = D.cur.v6_gen;
       if (v6_changed && ne[k].v6) {
         if (j6_active && !ne[k].v6_pool) {
           if ((rc = alloc_pool(D.device, us, &ne[k].v6_pool))) return fail(rc);
@@ -1780,6 +1832,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     } else if (!ctx->last6.blob.empty()) {
       if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
+      ne[k].v6_gen = ctx->gen6;
     }
     if (!svc_changed) ne[k].svc = D.cur.svc;
     else if (!ctx->svc_blob.empty() && (rc = upload_words(ctx->svc_blob, D.device, us, &ne[k].svc))) return fail(rc);

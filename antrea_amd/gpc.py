@@ -127,7 +127,7 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
            "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay",
            "gpc_set_launch_timing", "gpc_launch_times", "gpc_create_multi", "gpc_n_devices", "gpc_classify_on",
-           "gpc_classify6_on", "gpc_classify_host_on", "gpc_counters_on", "gpc_debug_epoch6"]
+           "gpc_classify6_on", "gpc_classify_host_on", "gpc_counters_on", "gpc_debug_epoch6", "gpc_debug_fail_uploads"]
 
 _lib = None
 
@@ -149,6 +149,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_counters_on.argtypes = [vp, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
                                     C.POINTER(sz)]
     lib.gpc_destroy.argtypes = [vp]
+    lib.gpc_debug_fail_uploads.argtypes = [C.c_int]
     lib.gpc_destroy.restype = None
     lib.gpc_initialize.argtypes = [vp]
     lib.gpc_install_rule.argtypes = [vp, C.POINTER(gpc_rule)]
@@ -557,6 +558,10 @@ class Classifier:
     def compact(self):
         """Publish with a full image rebuild (empties the overlay)."""
         _check(self.lib.gpc_compact(self.h), "gpc_compact")
+
+    def debug_fail_uploads(self, n):
+        """Fault injection (tests): the next n device image uploads fail with GPC_EDEV."""
+        _check(self.lib.gpc_debug_fail_uploads(int(n)), "gpc_debug_fail_uploads")
 
     def classify_host(self, cols: Dict[str, np.ndarray], count=False, lb=False, slot=0):
         """Verdicts (n, 2); with lb=True also the Service stage results (n,) of LB_DTYPE."""

@@ -440,9 +440,13 @@ int gpc_trace(gpc_ctx* ctx, const gpc_pkt_soa* pkt, gpc_verdict* out, gpc_lb_res
               size_t cap, size_t* n_steps);
 /* IPv6 packets (pkts->src6 / dst6 columns) against the IPv6 half of the rule set (the ipv6_* /
  * tcp6 / udp6 / icmp6 flows and the family-less ones), as OVS classifies an IPv6 packet in the
- * same tables. Needs gpc_config.ipv6_enabled; every commit that changes rules rebuilds the IPv6
- * image in full (no delta epochs, no AntreaProxy stage for IPv6). Same verdict / counter layout.
- * -GPC_EINVAL if the IPv6 prefixes of the rule set need more than 32 code bits (core.hpp). */
+ * same tables. Needs gpc_config.ipv6_enabled. A commit that changes rules publishes an IPv6 delta
+ * epoch (the IPv6 base plus a journal of the changed rules; new prefixes are interned into the
+ * prefix tree in place and their LPM entries go to the journal's overflow table) and falls back
+ * to a full IPv6 rebuild for a new prefix length, a prefix that is not a leaf of the tree, or a
+ * journal past its size thresholds (rules, pool words, overflow entries). No AntreaProxy stage for
+ * IPv6. Same verdict / counter layout. -GPC_EINVAL if the IPv6 prefixes of the rule set need more
+ * than 32 code bits (core.hpp). */
 int gpc_classify6(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
 /* The data path on device slot `slot` of a gpc_create_multi context: pkts / out / lb_out live on
  * that slot's device and `stream` belongs to it (NULL: its null stream). gpc_classify* == slot 0. */
@@ -486,6 +490,10 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
 /* The same for the IPv6 image's journal (IPv6 delta epochs). */
 int gpc_debug_epoch6(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
+/* Test hook (fault injection): the next `n` device image uploads of gpc_commit / gpc_compact fail
+ * with GPC_EDEV, as a device error would; the host shadow state keeps the new build, and the next
+ * successful commit re-uploads every base the device slots do not hold (tests/test_gpu_ipv6_delta.py). */
+int gpc_debug_fail_uploads(int n);
 /* The epoch (gpc_image_stats.epoch) the last gpc_classify* launch on `stream` was bound to: with
  * classification concurrent to commits, every launch sees exactly this one committed epoch. */
 int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch);

@@ -60,3 +60,31 @@ def test_gpu_ipv6_delta_epochs_dual_stack(size):
     c.compact()
     assert c.image_stats()["v6_overlay_rules"] == 0
     _cmp(c.classify6_host(cols6), got, cols)
+
+
+def test_gpu_upload_failure_then_delta_resyncs():
+    """a commit that rebuilds the host bases in full and then fails to upload
+    them must not leave the device extending a stale (or missing) base. After an injected upload
+    failure on a full rebuild, the next delta commit re-uploads both bases and the whole journals;
+    the device's IPv4 and IPv6 verdicts then equal the host emulation of the epoch."""
+    wl = workload.config3(seed=11, n_policies_per_dir=6, rules_per_policy=8)
+    log4 = mcf.ops(wl, seed=0x6E)[:300]
+    log6 = _map_log(log4 + [{"op": "commit"}], dual=True)[:-1]
+    cols = _packets(wl, log4, 20000, seed=17)
+    cols6 = workload.packets_to_v6(cols)
+    c = gpc.Classifier(ipv4=True, ipv6=True, compact_after=-1)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(workload.to_ipv6(wl, dual=True).rules))
+    c.commit()
+    mcf.apply(c, [o for o in log6[:100] if o["op"] != "commit"])
+    c.commit()  # a delta epoch on both families
+    mcf.apply(c, [o for o in log6[100:150] if o["op"] != "commit"])
+    c.debug_fail_uploads(1)
+    with pytest.raises(gpc.GpcError):
+        c.compact()  # full rebuild of both host bases; the device keeps the previous epoch
+    c.debug_fail_uploads(0)
+    mcf.apply(c, [o for o in log6[150:] if o["op"] != "commit"])
+    c.commit()  # delta over the new host bases: every slot must re-upload them first
+    assert c.image_stats()["v6_overlay_rules"] > 0
+    _cmp(c.classify6_host(cols6), emu.classify6(c, cols6), cols)
+    _cmp(c.classify_host(cols), emu.classify(c, cols), cols)
