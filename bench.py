@@ -339,8 +339,6 @@ def main():
     if args.family == 6 and args.config in ("C4", "C5"):
         ap.error("--family 6: C1-C3 only (no IPv6 AntreaProxy stage / delta epochs)")
     churn = args.config == "C5"
-    if args.config == "C4":  # the C oracle has no AntreaProxy stage: no comparable CPU timing
-        args.no_cpu_baseline = True
     if churn:  # the timed batch sees many epochs; see DESIGN.md for C5's correctness check
         args.no_traffic = True
         args.no_cpu_baseline = True

@@ -11,13 +11,15 @@ import numpy as np
 from . import cbuild
 from .flowtext import parse_flow
 
-NF = 19
+NF = 20
 F = {"dl_type": 0, "nw_proto": 1, "nw_src": 2, "nw_dst": 3, "ct_nw_src": 4, "ct_nw_dst": 5, "in_port": 6, "reg0": 7,
      "reg1": 8, "reg3": 9, "reg7": 10, "tun_id": 11, "tp_src": 12, "tp_dst": 13, "icmp_type": 12, "icmp_code": 13,
-     "ct_state": 14, "conj_id": 15, "ct_mark": 18}
+     "ct_state": 14, "conj_id": 15, "ct_mark": 18, "reg4": 19}
 TABLE_IDS = {"AntreaPolicyEgressRule": 1, "EgressRule": 2, "EgressDefaultRule": 3, "AntreaPolicyIngressRule": 4,
              "IngressRule": 5, "IngressDefaultRule": 6, "EgressMetric": 7, "IngressMetric": 8, "L3Forwarding": 9,
-             "ConntrackCommit": 10, "Output": 11, "IngressSecurityClassifier": 12}
+             "ConntrackCommit": 10, "Output": 11, "IngressSecurityClassifier": 12, "ServiceLB": 13,
+             "EndpointDNAT": 14}
+KEEP_TABLES = {1, 2, 3, 4, 5, 6, 7, 8, 12, 13, 14}
 A_CONJ, A_SET_REG, A_CT_COMMIT, A_GOTO, A_GROUP, A_CONTROLLER = 1, 2, 3, 4, 5, 6
 
 # numpy twins of the C records (same layout as ocls_flow / ocls_action)
@@ -46,6 +48,9 @@ def load():
         _lib.ocls_create.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         _lib.ocls_destroy.argtypes = [C.c_void_p]
         _lib.ocls_classify.argtypes = [C.c_void_p, C.POINTER(OPkts), C.c_size_t, C.c_void_p, C.c_int, C.c_int]
+        _lib.ocls_classify_lb.argtypes = [C.c_void_p, C.POINTER(OPkts), C.c_size_t, C.c_void_p, C.c_void_p, C.c_int,
+                                          C.c_int]
+        _lib.ocls_set_services.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
         _lib.ocls_counters.restype = C.POINTER(C.c_uint64)
         _lib.ocls_counters.argtypes = [C.c_void_p]
         _lib.ocls_stats.argtypes = [C.c_void_p, C.c_void_p]
@@ -70,7 +75,7 @@ def _convert_lines(flow_lines: List[str]):
     for li, line in enumerate(flow_lines):
         f = parse_flow(line)
         t = TABLE_IDS.get(f["table"], 0)
-        if not (1 <= t <= 8 or t == 12):
+        if t not in KEEP_TABLES:
             continue
         m = f["match"]
         if any(x.startswith("ipv6") or x.startswith("ct_ipv6") for x in m) or m.get("dl_type", (0x800, 0))[0] != 0x800:
@@ -111,7 +116,9 @@ def _convert_lines(flow_lines: List[str]):
                 acts.append((A_SET_REG, a[1], a[2] & 0xFFFFFFFF, 0xFFFFFFFF if a[3] is None else a[3], 0, 0, 0))
             elif a[0] == "ct_commit":
                 lv, lm = a[2][0] if a[2] else (0, 0)
-                acts.append((A_CT_COMMIT, 0, TABLE_IDS.get(a[1], 0), 0, 0, lv, lm))
+                nat = a[3] if len(a) > 3 else None  # EndpointDNAT: nat(dst=ip:port)
+                acts.append((A_CT_COMMIT, 0, TABLE_IDS.get(a[1], 0), nat[0] if nat else 0,
+                             (nat[1] | 0x10000) if nat else 0, lv, lm))
             elif a[0] == "goto_table":
                 acts.append((A_GOTO, 0, TABLE_IDS.get(a[1], 0), 0, 0, 0, 0))
             elif a[0] == "group":
@@ -164,7 +171,7 @@ class CPipeline:
         flows, acts, kept = _convert(flow_lines, procs)
         self._flows = np.ascontiguousarray(flows, dtype=FLOW_DT)
         self._acts = np.ascontiguousarray(acts, dtype=ACT_DT)
-        assert self._flows.dtype.itemsize == 176 and self._acts.dtype.itemsize == 32
+        assert self._flows.dtype.itemsize == 184 and self._acts.dtype.itemsize == 32
         tiers = tiers or {}
         keys = np.array(sorted(tiers), dtype=np.uint32)
         vals = np.array([max(0, min(255, tiers[int(k)])) for k in keys], dtype=np.uint8)
@@ -180,7 +187,28 @@ class CPipeline:
         except Exception:
             pass
 
-    def classify(self, cols: Dict[str, np.ndarray], threads=1, count=False) -> np.ndarray:
+    def set_services(self, group_lines: List[str], pods: Dict[int, int]):
+        """The AntreaProxy stage's select groups (ovs-ofctl dump-groups text) and the Pod map
+        (IP -> ofport) of L3Forwarding; ServiceLB / EndpointDNAT flows come with the flow text."""
+        from .flowtext import parse_group
+        words = []
+        for line in group_lines:
+            g = parse_group(line)
+            words += [g["id"], len(g["buckets"])]
+            for b in g["buckets"]:
+                sets = [a for a in b["actions"] if a[0] == "set_reg"]
+                words.append(len(sets))
+                for a in sets:
+                    words += [a[1], a[2] & 0xFFFFFFFF, 0xFFFFFFFF if a[3] is None else a[3]]
+        self._gw = np.array(words, dtype=np.uint32)
+        self._pip = np.array(sorted(pods), dtype=np.uint32)
+        self._pport = np.array([pods[int(k)] for k in self._pip], dtype=np.uint32)
+        rc = load().ocls_set_services(self.h, self._gw.ctypes.data, len(self._gw), self._pip.ctypes.data,
+                                      self._pport.ctypes.data, len(self._pip))
+        assert rc == 0, "malformed group encoding"
+
+    def classify(self, cols: Dict[str, np.ndarray], threads=1, count=False, lb=False):
+        """Verdicts (n, 2); with lb=True also the Service stage's gpc_lb_result words (n, 4)."""
         p = OPkts()
         keep = []
         n = None
@@ -195,9 +223,12 @@ class CPipeline:
                 setattr(p, k, a.ctypes.data)
                 n = len(a)
         out = np.zeros(4 * n, dtype=np.uint32)
-        load().ocls_classify(self.h, C.byref(p), n, out.ctypes.data, threads, int(count))
-        return out.view(np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"),
-                                  ("flags", "u1")])).reshape(n, 2)
+        lbo = np.zeros(4 * n, dtype=np.uint32) if lb else None
+        load().ocls_classify_lb(self.h, C.byref(p), n, out.ctypes.data, lbo.ctypes.data if lb else None, threads,
+                                int(count))
+        v = out.view(np.dtype([("conj_id", "<u4"), ("action", "u1"), ("table", "u1"), ("tier", "u1"),
+                               ("flags", "u1")])).reshape(n, 2)
+        return (v, lbo.reshape(n, 4)) if lb else v
 
     def stats(self) -> Dict[str, int]:
         out = np.zeros(8, np.uint64)

@@ -42,12 +42,15 @@
 
 enum {
   F_DL_TYPE, F_NW_PROTO, F_NW_SRC, F_NW_DST, F_CT_NW_SRC, F_CT_NW_DST, F_IN_PORT, F_REG0, F_REG1, F_REG3, F_REG7,
-  F_TUN_ID, F_TP_SRC, F_TP_DST, F_CT_STATE, F_CONJ_ID, F_LABEL_LO, F_LABEL_HI, F_CT_MARK, NF
+  F_TUN_ID, F_TP_SRC, F_TP_DST, F_CT_STATE, F_CONJ_ID, F_LABEL_LO, F_LABEL_HI, F_CT_MARK, F_REG4, NF
 };
-/* tables: 1..6 rule tables, 7 EgressMetric, 8 IngressMetric, 12 IngressSecurityClassifier */
+/* tables: 1..6 rule tables, 7 EgressMetric, 8 IngressMetric, 12 IngressSecurityClassifier,
+ * 13 ServiceLB, 14 EndpointDNAT (the AntreaProxy stage in front of the policy tables) */
 #define T_ISC 12
-#define N_TABLES 13
-static const int kTables[] = {1, 2, 3, 4, 5, 6, 7, 8, T_ISC};
+#define T_SVCLB 13
+#define T_EPDNAT 14
+#define N_TABLES 15
+static const int kTables[] = {1, 2, 3, 4, 5, 6, 7, 8, T_ISC, T_SVCLB, T_EPDNAT};
 #define N_USED_TABLES (int)(sizeof kTables / sizeof kTables[0])
 
 /* flow action kinds (decoded by oracle/cls_c.py from the flow text) */
@@ -55,7 +58,8 @@ enum { A_CONJ = 1, A_SET_REG = 2, A_CT_COMMIT = 3, A_GOTO = 4, A_GROUP = 5, A_CO
 
 typedef struct {
   uint8_t kind, reg;
-  uint32_t a, b, c;          /* CONJ id,clause,n | SET_REG value,mask | CT table | GOTO table | GROUP id */
+  uint32_t a, b, c;          /* CONJ id,clause,n | SET_REG value,mask | CT table, nat ip, nat port | 1 << 16
+                                (c == 0: no nat) | GOTO table | GROUP id */
   uint64_t lv, lm;           /* CT label */
 } ocls_action;
 
@@ -143,6 +147,14 @@ typedef struct ocls {
   int n_tier;
   uint64_t* cnt;             /* per flow: packets, bytes (metric flows) */
   uint64_t stats[8];         /* summed over classify calls: see ocls_stats */
+  /* AntreaProxy stage (ocls_set_services): select groups and the Pod map of L3Forwarding */
+  uint32_t* gw;              /* group words: gid, n_buckets, per bucket n_sets, (reg, value, mask) x n_sets */
+  uint32_t* g_id;            /* sorted group ids and the word offset of each group in gw */
+  size_t* g_off;
+  int n_groups;
+  uint32_t* pod_ip;          /* sorted Pod IPs and their ofports */
+  uint32_t* pod_port;
+  int n_pods;
 } ocls;
 
 /* per-thread lookup workspace */
@@ -397,6 +409,11 @@ void ocls_destroy(ocls* c) {
   free(c->tier_conj);
   free(c->tier_val);
   free(c->cnt);
+  free(c->gw);
+  free(c->g_id);
+  free(c->g_off);
+  free(c->pod_ip);
+  free(c->pod_port);
   free(c);
 }
 
@@ -688,6 +705,181 @@ static void stage(const ocls* c, ws_t* w, int base, uint32_t* pv, uint32_t len, 
   *out_packed = action | (tindex << 8) | ((conj ? tier_of(c, conj) : 0u) << 16) | (flags << 24);
 }
 
+/* ------------------------------------------------------------------ AntreaProxy stage (C4)
+ * ServiceLB -> select group bucket -> EndpointDNAT -> L3Forwarding, restated as oracle/ovs_cls.py
+ * Pipeline.service_stage does over the realized flows (pipeline.go:2374-2431 ServiceLB, 2502-2528
+ * EndpointDNAT, 2553-2592 select groups). The bucket choice of an OVS select group is OVS-internal
+ * (dp_hash; not in the reference): restated with the symmetric hash of core.hpp lb_hash over a
+ * 2^k >= 64 slot table, slot s -> bucket s mod n (parity of the bucket choice is unpinned). */
+enum { LB_HIT = 1, LB_NO_ENDPOINT = 2, LB_DNAT = 4, LB_REMOTE = 8 };
+#define EP_TO_SELECT 0x10000u     /* fields.go EpToSelectRegMark (reg4[16..18] = 1) */
+#define SVC_NO_EP (1u << 14)      /* reg0 SvcNoEpRegMark */
+#define REMOTE_EP (1u << 26)      /* reg4 RemoteEndpointRegMark */
+
+/* Pod map and select groups (words: gid, n_buckets, then per bucket n_sets and n_sets x (reg,
+ * value, mask) of its set_field actions); copied. */
+int ocls_set_services(ocls* c, const uint32_t* gw, size_t n_gw, const uint32_t* pod_ip, const uint32_t* pod_port, int n_pods) {
+  free(c->gw);
+  free(c->g_id);
+  free(c->g_off);
+  free(c->pod_ip);
+  free(c->pod_port);
+  c->gw = (uint32_t*)xmalloc(4 * (n_gw + 1));
+  memcpy(c->gw, gw, 4 * n_gw);
+  int ng = 0;
+  for (size_t o = 0; o + 1 < n_gw; ng++) {  /* count, validating the encoding */
+    uint32_t nb = gw[o + 1];
+    o += 2;
+    for (uint32_t b = 0; b < nb; b++) {
+      if (o >= n_gw) return -1;
+      o += 1 + 3 * (size_t)gw[o];
+    }
+    if (o > n_gw) return -1;
+  }
+  c->g_id = (uint32_t*)xmalloc(4 * (size_t)(ng + 1));
+  c->g_off = (size_t*)xmalloc(sizeof(size_t) * (size_t)(ng + 1));
+  size_t o = 0;
+  for (int g = 0; g < ng; g++) {
+    c->g_id[g] = gw[o];
+    c->g_off[g] = o;
+    uint32_t nb = gw[o + 1];
+    o += 2;
+    for (uint32_t b = 0; b < nb; b++) o += 1 + 3 * (size_t)gw[o];
+  }
+  for (int i = 1; i < ng; i++)  /* sort by id (insertion: groups arrive nearly sorted) */
+    for (int j = i; j > 0 && c->g_id[j - 1] > c->g_id[j]; j--) {
+      uint32_t t = c->g_id[j];
+      c->g_id[j] = c->g_id[j - 1];
+      c->g_id[j - 1] = t;
+      size_t u = c->g_off[j];
+      c->g_off[j] = c->g_off[j - 1];
+      c->g_off[j - 1] = u;
+    }
+  c->n_groups = ng;
+  c->pod_ip = (uint32_t*)xmalloc(4 * (size_t)(n_pods + 1));
+  c->pod_port = (uint32_t*)xmalloc(4 * (size_t)(n_pods + 1));
+  memcpy(c->pod_ip, pod_ip, 4 * (size_t)n_pods);
+  memcpy(c->pod_port, pod_port, 4 * (size_t)n_pods);
+  for (int i = 1; i < n_pods; i++)
+    for (int j = i; j > 0 && c->pod_ip[j - 1] > c->pod_ip[j]; j--) {
+      uint32_t t = c->pod_ip[j];
+      c->pod_ip[j] = c->pod_ip[j - 1];
+      c->pod_ip[j - 1] = t;
+      t = c->pod_port[j];
+      c->pod_port[j] = c->pod_port[j - 1];
+      c->pod_port[j - 1] = t;
+    }
+  c->n_pods = n_pods;
+  return 0;
+}
+
+static uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+static uint32_t lb_hash(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport, uint32_t proto) {
+  return mix32((src ^ dst) ^ (mix32(((sport ^ dport) << 8) | (proto & 0xffu)) * 0x9e3779b1u));
+}
+
+static void apply_set_reg(uint32_t reg, uint32_t v, uint32_t m, uint32_t* r0, uint32_t* r3, uint32_t* r4, uint32_t* r7,
+                          int* set7) {
+  uint32_t* r = reg == 0 ? r0 : reg == 3 ? r3 : reg == 4 ? r4 : reg == 7 ? r7 : NULL;
+  if (!r) return;
+  *r = (*r & ~m) | (v & m);
+  if (reg == 7) *set7 = 1;
+}
+
+/* The Service stage of one packet: rewrites pv (nw_dst / tp_dst after DNAT, reg1 = the Endpoint's
+ * ofport, reg7 when the ServiceLB flow loads it) and *dest; lb = gpc_lb_result words {endpoint
+ * ip, port | flags << 16, group id, out_port}. Returns the LB flags (0: not a Service packet).
+ * pv[F_CT_NW_DST] keeps the pre-NAT destination. */
+static uint32_t service_stage(const ocls* c, ws_t* w, uint32_t* pv, uint32_t* dest, uint32_t* lb) {
+  lb[0] = lb[1] = lb[2] = lb[3] = 0;
+  const uint32_t proto = pv[F_NW_PROTO];
+  if ((proto != 6 && proto != 17 && proto != 132) || !c->tables[T_SVCLB].n_st) return 0;
+  uint32_t sv[NF];
+  memcpy(sv, pv, sizeof sv);
+  uint32_t r0 = 0, r3 = 0, r4 = EP_TO_SELECT, r7 = 0;
+  int set7 = 0, tie = 0;
+  sv[F_REG0] = r0;
+  sv[F_REG3] = r3;
+  sv[F_REG4] = r4;
+  const int fi = lookup(c, w, T_SVCLB, sv, 0, &tie);
+  if (fi < 0) return 0;
+  uint32_t flags = LB_HIT, gid = 0;
+  int has_group = 0;
+  const ocls_flow* f = &c->flows[fi];
+  for (int a = 0; a < f->n_act; a++) {
+    const ocls_action* ac = &c->acts[f->act_off + a];
+    if (ac->kind == A_SET_REG) apply_set_reg(ac->reg, ac->a, ac->b, &r0, &r3, &r4, &r7, &set7);
+    else if (ac->kind == A_GROUP) gid = ac->a, has_group = 1;
+  }
+  if (set7) pv[F_REG7] = r7;
+  lb[2] = gid;
+  int lo = 0, hi = c->n_groups;
+  while (lo < hi) {
+    int mid = (lo + hi) / 2;
+    if (c->g_id[mid] < gid) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint32_t* g = (has_group && lo < c->n_groups && c->g_id[lo] == gid) ? c->gw + c->g_off[lo] : NULL;
+  if (!g || g[1] == 0) {
+    flags |= LB_NO_ENDPOINT;
+    lb[1] = flags << 16;
+    return flags;
+  }
+  const uint32_t nb = g[1];
+  uint32_t lg = 6;
+  while ((1u << lg) < nb) lg++;
+  const uint32_t slot = lb_hash(pv[F_NW_SRC], pv[F_NW_DST], pv[F_TP_SRC], pv[F_TP_DST], proto) & ((1u << lg) - 1u);
+  const uint32_t* b = g + 2;
+  for (uint32_t k = 0; k < slot % nb; k++) b += 1 + 3 * b[0];
+  for (uint32_t k = 0; k < b[0]; k++) apply_set_reg(b[1 + 3 * k], b[2 + 3 * k], b[3 + 3 * k], &r0, &r3, &r4, &r7, &set7);
+  if (r0 & SVC_NO_EP) {  /* serviceNoEndpointFlow: packet-in, rejected */
+    flags |= LB_NO_ENDPOINT;
+    lb[1] = flags << 16;
+    return flags;
+  }
+  if (r4 & REMOTE_EP) flags |= LB_REMOTE;
+  const uint32_t ep_ip = r3, ep_port = r4 & 0xffffu;
+  sv[F_REG0] = r0;
+  sv[F_REG3] = r3;
+  sv[F_REG4] = r4;
+  const int di = lookup(c, w, T_EPDNAT, sv, 0, &tie);
+  if (di >= 0) {
+    const ocls_flow* d = &c->flows[di];
+    for (int a = 0; a < d->n_act; a++) {
+      const ocls_action* ac = &c->acts[d->act_off + a];
+      if (ac->kind == A_CT_COMMIT && (ac->c >> 16)) {
+        pv[F_NW_DST] = ac->b;
+        pv[F_TP_DST] = ac->c & 0xffffu;
+        flags |= LB_DNAT;
+      }
+    }
+  }
+  lo = 0, hi = c->n_pods;
+  while (lo < hi) {
+    int mid = (lo + hi) / 2;
+    if (c->pod_ip[mid] < ep_ip) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < c->n_pods && c->pod_ip[lo] == ep_ip) {
+    pv[F_REG1] = c->pod_port[lo];
+    *dest = 0; /* Pod */
+  } else {
+    pv[F_REG1] = 0;
+    *dest = (flags & LB_REMOTE) ? 2u /* tunnel */ : 1u /* gateway */;
+  }
+  lb[0] = ep_ip;
+  lb[1] = ep_port | (flags << 16);
+  lb[3] = pv[F_REG1];
+  return flags;
+}
+
 /* IngressSecurityClassifier as installed (pipeline.go:2144-2182): the destination class as its
  * PktDestinationField mark in reg0[4..7] (fields.go:54-57: tunnel 1, gateway 2, uplink 4) and the
  * packet's ct_mark; a flow out of the policy tables (IngressMetric / ConntrackCommit) makes the
@@ -711,7 +903,8 @@ static uint32_t ingress_classifier(const ocls* c, ws_t* w, uint32_t* pv, uint32_
   return 0;
 }
 
-static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo, size_t hi, uint32_t* out, uint64_t* cnt) {
+static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo, size_t hi, uint32_t* out, uint32_t* lb_out,
+                           uint64_t* cnt) {
   for (size_t i = lo; i < hi; i++) {
     uint32_t pv[NF];
     memset(pv, 0, sizeof pv);
@@ -731,13 +924,23 @@ static void classify_range(const ocls* c, ws_t* w, const ocls_pkts* p, size_t lo
     pv[F_TP_DST] = ported ? p->dport[i] : 0;
     pv[F_CT_STATE] = p->ct_state ? p->ct_state[i] : 0x21;
     uint32_t len = p->len ? p->len[i] : 0;
+    uint32_t dest = p->dest ? p->dest[i] : 0, lb[4];
+    const uint32_t lbf = service_stage(c, w, pv, &dest, lb);
+    if (lb_out) memcpy(lb_out + 4 * i, lb, sizeof lb);
+    if (lbf & LB_NO_ENDPOINT) { /* EndpointDNAT serviceNoEndpointFlow: rejected before the policy stages */
+      out[4 * i + 0] = 0;
+      out[4 * i + 1] = ACT_REJECT | (4u << 8); /* table code GPC_VTABLE_ENDPOINT_DNAT */
+      out[4 * i + 2] = 0;
+      out[4 * i + 3] = ACT_NONE;
+      continue;
+    }
     uint32_t ec, ep, gc, gp, isc;
     stage(c, w, 0, pv, len, cnt, &ec, &ep);
     uint32_t ea = ep & 0xff;
     if (ea == ACT_DROP || ea == ACT_REJECT || ea == ACT_ISO_DROP) {
       gc = 0;
       gp = ACT_NONE;
-    } else if ((isc = ingress_classifier(c, w, pv, p->dest ? p->dest[i] : 0, p->ct_mark ? p->ct_mark[i] : 0)) != 0) {
+    } else if ((isc = ingress_classifier(c, w, pv, dest, p->ct_mark ? p->ct_mark[i] : 0)) != 0) {
       gc = 0;
       gp = isc;
     } else {
@@ -758,18 +961,20 @@ typedef struct {
   const ocls_pkts* p;
   size_t lo, hi;
   uint32_t* out;
+  uint32_t* lb;
   uint64_t* cnt;
   ws_t ws;
 } job;
 
 static void* worker(void* arg) {
   job* j = (job*)arg;
-  classify_range(j->c, &j->ws, j->p, j->lo, j->hi, j->out, j->cnt);
+  classify_range(j->c, &j->ws, j->p, j->lo, j->hi, j->out, j->lb, j->cnt);
   return NULL;
 }
 
-/* out: 4 uint32 per packet (egress conj, egress packed, ingress conj, ingress packed). */
-int ocls_classify(ocls* c, const ocls_pkts* p, size_t n, uint32_t* out, int threads, int count) {
+/* out: 4 uint32 per packet (egress conj, egress packed, ingress conj, ingress packed); lb_out (or
+ * NULL): 4 uint32 per packet, the Service stage's gpc_lb_result words. */
+int ocls_classify_lb(ocls* c, const ocls_pkts* p, size_t n, uint32_t* out, uint32_t* lb_out, int threads, int count) {
   if (threads < 1) threads = 1;
   if ((size_t)threads > n && n) threads = (int)n;
   pthread_t* th = (pthread_t*)xmalloc(sizeof(pthread_t) * (size_t)threads);
@@ -781,6 +986,7 @@ int ocls_classify(ocls* c, const ocls_pkts* p, size_t n, uint32_t* out, int thre
     jobs[t].lo = n * (size_t)t / (size_t)threads;
     jobs[t].hi = n * (size_t)(t + 1) / (size_t)threads;
     jobs[t].out = out;
+    jobs[t].lb = lb_out;
     if (threads == 1) {
       worker(&jobs[t]);
     } else if (pthread_create(&th[t], NULL, worker, &jobs[t]) != 0) {
@@ -804,6 +1010,10 @@ int ocls_classify(ocls* c, const ocls_pkts* p, size_t n, uint32_t* out, int thre
   free(th);
   free(jobs);
   return 0;
+}
+
+int ocls_classify(ocls* c, const ocls_pkts* p, size_t n, uint32_t* out, int threads, int count) {
+  return ocls_classify_lb(c, p, n, out, NULL, threads, count);
 }
 
 const uint64_t* ocls_counters(const ocls* c) { return c->cnt; }

@@ -6,9 +6,12 @@
                              hide on both sides of a comparison.
 * `oracle_metrics(pipe)`  -- NetworkPolicyMetrics of the counters the C oracle accumulated
                              (parsed exactly as network_policy.go:1917-1980, 2034 parse the dump).
-* `non_service_mask`      -- packets of a workload with Services that do not hit a ServiceLB flow
-                             (the C oracle has no AntreaProxy stage; those packets' policy verdicts
-                             are comparable directly).
+* `service_flows(wl)`     -- for a workload with Services (C4): the ServiceLB / EndpointDNAT flow
+                             text, the select groups and the Pod map the C oracle's AntreaProxy stage
+                             runs on, as the product's host compiler realizes them (that text is
+                             pinned by the reference's client_test.go goldens, tests/test_service.py;
+                             the policy flows always come from the oracle compiler).
+* `non_service_mask`      -- packets of a workload with Services that do not hit a ServiceLB flow.
 * `OracleWorker`          -- the same in a separate CPU process (spawned, never touches a GPU):
                              bench.py starts it before its GPU work, then asks it to check a sample
                              of the timed batch (parity stamp) and to time the CPU baseline.
@@ -67,9 +70,29 @@ def oracle_flows(wl):
     return fnp.dump_flows()
 
 
+def service_flows(wl):
+    """(ServiceLB / EndpointDNAT flow lines, group lines, Pod map) of wl's Services, or None. Host
+    compiler only: nothing here touches a GPU."""
+    if getattr(wl, "services", None) is None:
+        return None
+    from antrea_amd import gpc, workload
+    c = gpc.Classifier(compact_after=-1)
+    try:
+        c.initialize()
+        workload.install_services(c, wl)
+        lines = [f for f in c.dump_flows() if "table=ServiceLB" in f or "table=EndpointDNAT" in f]
+        return lines, c.dump_groups(), dict(wl.pods)
+    finally:
+        del c
+
+
 def oracle_pipeline(wl, procs: Optional[int] = None):
     from .cls_c import CPipeline
-    return CPipeline(oracle_flows(wl), tiers_of(wl), procs=procs)
+    svc = service_flows(wl)
+    pipe = CPipeline(oracle_flows(wl) + (svc[0] if svc else []), tiers_of(wl), procs=procs)
+    if svc:
+        pipe.set_services(svc[1], svc[2])
+    return pipe
 
 
 def oracle_metrics(pipe) -> Dict[int, tuple]:
@@ -119,7 +142,7 @@ def _serve(conn, config: str, procs: int):
             _, cols, verdicts = msg
             t = time.time()
             want = pipe.classify(cols, threads=procs)
-            res = compare(verdicts, want, non_service_mask(wl, cols))
+            res = compare(verdicts, want)
             res["oracle_s"] = round(time.time() - t, 2)
             conn.send(res)
         elif msg[0] == "baseline":

@@ -9,8 +9,10 @@ compiler (oracle/compiler.py), loaded into the C restatement of the OVS classifi
 on. Stored: the verdicts (n x 2 records of 8 B, gpc_verdict layout), the metrics
 {conj: (packets, bytes, sessions)} as NetworkPolicyMetrics parses the Metric-table dump, a SHA-256
 of the packet columns and of the rule list (so a generator change is detected instead of silently
-comparing different inputs), and for C4 the mask of packets that hit no Service (the oracle has no
-AntreaProxy stage; only those are comparable).
+comparing different inputs), and for C4 the Service stage's LB result words of every packet (the C
+oracle runs the AntreaProxy stage, ovs_cls.c service_stage, over the ServiceLB / EndpointDNAT flows
+and groups the product realizes -- text pinned by the reference's client_test.go goldens). `mask`
+(kept for the loaders) selects every packet.
 """
 from __future__ import annotations
 
@@ -86,23 +88,19 @@ def make(config: str):
     wl, cols = packets(config)
     pipe = parity.oracle_pipeline(wl)
     t1 = time.time()
-    want = pipe.classify(cols, threads=parity.cpu_threads(), count=True)
+    want, lb = pipe.classify(cols, threads=parity.cpu_threads(), count=True, lb=True)
     t2 = time.time()
-    mask = parity.non_service_mask(wl, cols)
-    if getattr(wl, "svc_meta", None) is not None:
-        # counters of packets that hit a Service are not comparable: classify the non-Service ones
-        # again with counters on a fresh pipeline
-        pipe = parity.oracle_pipeline(wl)
-        sub = {k: v[mask] for k, v in cols.items()}
-        pipe.classify(sub, threads=parity.cpu_threads(), count=True)
+    mask = np.ones(len(cols["src"]), bool)
     m = parity.oracle_metrics(pipe)
     conj = np.array(sorted(m), np.uint32)
     met = np.array([m[int(c)] for c in conj], np.uint64).reshape(-1, 3)
+    extra = {"lb": lb} if getattr(wl, "services", None) else {}
     np.savez_compressed(path(config), verdicts=np.ascontiguousarray(want).view(np.uint32).reshape(-1, 4),
                         metric_conj=conj, metric_val=met, mask=mask, cols_sha256=cols_digest(cols),
-                        rules_sha256=rules_digest(wl), n_flows=pipe.n_flows)
-    print("%s: %d packets, %d flows, oracle setup %.0f s, classify %.1f s, %d comparable, %d metric rules"
-          % (config, len(cols["src"]), pipe.n_flows, t1 - t0, t2 - t1, int(mask.sum()), len(conj)))
+                        rules_sha256=rules_digest(wl), n_flows=pipe.n_flows, **extra)
+    print("%s: %d packets, %d flows, oracle setup %.0f s, classify %.1f s, %d metric rules%s"
+          % (config, len(cols["src"]), pipe.n_flows, t1 - t0, t2 - t1, len(conj),
+             ", %d Service hits" % int((lb[:, 1] >> 16 != 0).sum()) if extra else ""))
 
 
 def load(config: str) -> dict:

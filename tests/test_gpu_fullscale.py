@@ -54,16 +54,19 @@ def _nonzero(m):
 @pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4", "C3x"])
 def test_device_vs_oracle_fullscale(config, group):
     """Verdicts (conj id, action, table, tier, flags) and NetworkPolicyMetrics of 100k packets at
-    full scale equal the C oracle's exactly (C4: the packets that hit no Service, with the Service
-    stage live in the kernel; C3x: C3 with every optional column set -- conntrack states, pre-NAT
+    full scale equal the C oracle's exactly (C4: every packet, the Service stage's LB results too,
+    against the C oracle's AntreaProxy stage; C3x: C3 with every optional column set -- conntrack states, pre-NAT
     addresses, IngressSecurityClassifier destinations and hairpin mark, in_port, tun_id, reg7),
     with the packet grouping pre-pass off and on (the bench's 64M-packet batches are grouped)."""
     f, wl, cols = _inputs(config)
-    mask = f["mask"].astype(bool)
-    sub = cols if mask.all() else {k: v[mask] for k, v in cols.items()}
     c = _classifier(wl, group=group)
-    got = c.classify_host(sub, count=True)
-    res = parity.compare(got, f["verdicts"][mask])
+    if "lb" in f:  # C4: the LB result words of every packet against the oracle's AntreaProxy stage
+        got, lb = c.classify_host(cols, count=True, lb=True)
+        bad = np.nonzero((lb.view(np.uint32).reshape(-1, 4) != f["lb"]).any(axis=1))[0]
+        assert len(bad) == 0, (len(bad), bad[:5])
+    else:
+        got = c.classify_host(cols, count=True)
+    res = parity.compare(got, f["verdicts"])
     assert res["mismatches"] == 0, res
     assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
     acts = set(int(a) for a in np.unique(got["action"]))

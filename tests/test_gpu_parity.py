@@ -188,29 +188,35 @@ def test_gpu_delta_epochs(name, group):
 @pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
 @pytest.mark.parametrize("name", ["C1", "C4"])
 def test_gpu_service_stage(name, group):
-    """AntreaProxy stage on the device: verdicts and per-packet LB results equal the host emulation of
-    the same epoch (small: C1 + 60 Services; full: C4 = C3 + 10k Services x 10 Endpoints); the small
-    case also against the oracle; with and without the packet grouping pre-pass (LB results are
-    scattered back to caller order)."""
+    """AntreaProxy stage on the device: verdicts and per-packet LB results equal the oracle (small:
+    C1 + 60 Services against the Python oracle; full: C4 = C3 + 10k Services x 10 Endpoints against
+    the C oracle's fixture, 100k packets), with and without the packet grouping pre-pass (LB results
+    are scattered back to caller order)."""
     from tests.test_service import _oracle, _svc_workload
-    wl = _svc_workload("C1", 61) if name == "C1" else workload.config4()
-    n = 3000 if name == "C1" else 200_000
-    cols = workload.gen_packets(wl, n, seed=61)
+    from tests.golden import make_parity_fixtures as fx
+    if name == "C1":
+        wl = _svc_workload("C1", 61)
+        n = 3000
+        cols = workload.gen_packets(wl, n, seed=61)
+    else:  # the full-scale C4 fixture: the C oracle's AntreaProxy stage over every packet
+        f = fx.load("C4")
+        wl, cols = fx.packets("C4")
+        assert fx.cols_digest(cols) == str(f["cols_sha256"]) and fx.rules_digest(wl) == str(f["rules_sha256"])
+        n = len(cols["src"])
     c = gpc.Classifier(group_packets=group)
     c.initialize()
     c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
     workload.install_services(c, wl)
     c.commit()
     got, lb = c.classify_host(cols, lb=True)
-    want_lb = np.zeros(n, dtype=gpc.LB_DTYPE)
-    want = emu.classify(c, cols, lb=want_lb)
-    _cmp(got, want, cols)
-    assert (lb == want_lb).all()
     assert ((lb["flags"] & gpc.LB_HIT) != 0).mean() > 0.3
     if name == "C1":
         o, olb = _oracle(wl, c, cols, n)
         _cmp(got, o, cols)
         assert (lb == olb).all()
+    else:
+        _cmp(got, f["verdicts"], cols)
+        assert (lb.view(np.uint32).reshape(-1, 4) == f["lb"]).all()
 
 
 @pytest.mark.parametrize("name", ["C1dual"])

@@ -51,3 +51,37 @@ def test_c_vs_python_oracle(name, seed):
 
 # Full-size C2 / C3 parity of the product (host emulation and device) against the C oracle fed by
 # the ORACLE compiler's flows: tests/test_parity_fixtures.py and tests/test_gpu_fullscale.py.
+
+
+@pytest.mark.parametrize("name,seed", [("C1", 51), ("C3s", 52), ("C3s", 53)])
+def test_c_oracle_service_stage_vs_python(name, seed):
+    """The C oracle's AntreaProxy stage (ServiceLB -> select group -> EndpointDNAT -> L3Forwarding,
+    ovs_cls.c service_stage) == the Python oracle's (ovs_cls.py service_stage): verdicts and the
+    LB result words, over packets of which a large share address a Service (no-Endpoint Services,
+    remote / local Endpoints, Local traffic policy)."""
+    from oracle import parity
+    from tests.test_service import _svc_workload
+    wl = _svc_workload(name, seed)
+    n = 1500
+    cols = workload.gen_packets(wl, n, seed=seed)
+    cols["len"] = np.full(n, 100, np.uint16)
+    svc_lines, groups, pods = parity.service_flows(wl)
+    flows = parity.oracle_flows(wl) + svc_lines
+    tiers = parity.tiers_of(wl)
+    py = ovs_cls.Pipeline(flows, tiers, groups, pods)
+    c = parity.oracle_pipeline(wl)
+    got, lb = c.classify(cols, threads=2, count=True, lb=True)
+    hits = nd = 0
+    for i in range(n):
+        rec = []
+        e, g = py.classify({k: int(v[i]) for k, v in cols.items()}, lb=rec)
+        for j, v in enumerate((e, g)):
+            assert tuple(got[i, j][["action", "conj_id", "table", "tier", "flags"]].item()) == v, (i, j)
+        flags, r = rec[0]
+        want = [0, 0, 0, 0]
+        if flags:
+            want = [r["endpoint_ip"], r["endpoint_port"] | (flags << 16), r["group_id"], r["out_port"]]
+            hits += 1
+            nd += bool(flags & ovs_cls.LB_NO_ENDPOINT)
+        assert list(lb[i]) == want, (i, list(lb[i]), want)
+    assert hits > n // 4 and nd > 0

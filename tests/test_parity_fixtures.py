@@ -27,22 +27,31 @@ def test_fixture_inputs_stable(config):
     assert f["verdicts"].shape == (len(cols["src"]), 2)
 
 
-@pytest.mark.parametrize("config,composite", [("C2", "0"), ("C3", "0"), ("C3x", "0"), ("C2", "1"), ("C3", "1")])
+@pytest.mark.parametrize("config,composite", [("C2", "0"), ("C3", "0"), ("C3x", "0"), ("C2", "1"), ("C3", "1"),
+                                              ("C4", "1")])
 def test_emu_vs_oracle_fixture(config, composite, monkeypatch):
     """composite "1" (the default): the image carries composite driver indexes (core.hpp TableHdr
-    cidx; C2 and C3 qualify in both directions), "0": the plain per-clause driver indexes only."""
+    cidx; C2 and C3 qualify in both directions), "0": the plain per-clause driver indexes only.
+    C4: every packet, the Service stage's LB result words too (the C oracle's AntreaProxy stage)."""
     monkeypatch.setenv("GPC_COMPOSITE", composite)
     f = fx.load(config)
     wl, cols = fx.packets(config)
     c = gpc.Classifier()
     c.initialize()
     c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    svc = getattr(wl, "services", None) is not None
+    if svc:
+        workload.install_services(c, wl)
     emu.commit_host(c)
     _, slots = c.counters()
     arr = np.zeros((max(1, len(slots)), 3), dtype=np.uint64)
-    got = emu.classify(c, cols, counters=arr)
+    lb = np.zeros(len(cols["src"]), dtype=gpc.LB_DTYPE) if svc else None
+    got = emu.classify(c, cols, counters=arr, lb=lb)
     res = parity.compare(got, f["verdicts"])
     assert res["mismatches"] == 0, res
+    if svc:
+        bad = np.nonzero((lb.view(np.uint32).reshape(-1, 4) != f["lb"]).any(axis=1))[0]
+        assert len(bad) == 0, (len(bad), bad[:5])
     m = {int(s): tuple(int(x) for x in arr[i]) for i, s in enumerate(slots) if s and arr[i].any()}
     assert m == {k: v for k, v in f["metrics"].items() if any(v)}
 
