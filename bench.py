@@ -40,7 +40,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 PARITY_SAMPLE = 1 << 16
 # rocprofv3 passes (one run each: FETCH_SIZE takes 3 of the 4 TCC counter slots)
-PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"))
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"),
+              # what bounds a gather kernel below the bandwidth roof: wave-parked (s_waitcnt) share
+              # of wave cycles, vector-memory / scalar / vector instructions per wave
+              ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU",
+               "SQ_INSTS_VALU"))
 
 
 def _log(msg):
@@ -254,6 +258,24 @@ def _traffic(cs):
     return (2.0 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0, (cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0
 
 
+def _sq(cs):
+    """SQ counters of one launch kind per wave (quad-cycle counters x 4 = cycles)."""
+    if not cs or not cs.get("SQ_WAVES"):
+        return None
+    w = cs["SQ_WAVES"]
+    out = {}
+    for c, name in (("SQ_INSTS_VMEM_RD", "vmem_rd_per_wave"), ("SQ_INSTS_SALU", "salu_per_wave"),
+                    ("SQ_INSTS_VALU", "valu_per_wave")):
+        if cs.get(c) is not None:
+            out[name] = round(cs[c] / w, 1)
+    if cs.get("SQ_WAVE_CYCLES"):
+        out["cycles_per_wave"] = round(4.0 * cs["SQ_WAVE_CYCLES"] / w)
+        for c, name in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_ACTIVE_INST_ANY", "active_inst_frac")):
+            if cs.get(c) is not None:
+                out[name] = round(cs[c] / cs["SQ_WAVE_CYCLES"], 3)
+    return out
+
+
 def _roofline(pmc, kern_ms, n, b_in, b_out, lbar, launches):
     """Roofline of the dominant kernel (the launch kind with the largest HIP-event time per step,
     measured on the launch stream inside the timed region: gpc_launch_times), with the whole
@@ -280,6 +302,9 @@ def _roofline(pmc, kern_ms, n, b_in, b_out, lbar, launches):
                 raise RuntimeError("roofline sanity: %s measured %.0f GB/s exceeds the HBM peak" % (kind, gbs))
             d.update(gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_packet=round(tr / n, 1),
                      frac_without_fetch_x2=round(tr1 / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4))
+        sq = _sq(cs)
+        if sq:
+            d["sq"] = sq
         kernels[kind] = d
     dom = max(kernels, key=lambda k: kernels[k]["ms"] * kernels[k]["launches_per_step"]) if kernels else None
     rl = {"bound": "hbm", "kernel": dom, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
@@ -290,6 +315,8 @@ def _roofline(pmc, kern_ms, n, b_in, b_out, lbar, launches):
         tr, _ = _traffic(_pmc_kernel(by_kernel, dom))
         rl.update(achieved=kernels[dom]["gbs"], frac=kernels[dom]["frac"], traffic=int(tr),
                   kernel_ms=kernels[dom]["ms"], frac_without_fetch_x2=kernels[dom]["frac_without_fetch_x2"])
+    if dom and "sq" in kernels[dom]:
+        rl["sq"] = kernels[dom]["sq"]
     rl["kernels"] = kernels
     step = {"ms": round(kern_ms, 3)}
     f, w = pmc.get("FETCH_SIZE"), pmc.get("WRITE_SIZE")
@@ -335,7 +362,14 @@ def main():
                     help="gpc_config.group_packets: 0 = auto (batches >= 2^18 against images >= 4 MB), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),
                     help="6: the workload's addresses embedded in fd00:10::/96, IPv6 packets (gpc_classify6)")
+    ap.add_argument("--multidev", type=int, default=0,
+                    help="one process over N devices (gpc_create_multi: the agent's shape, one control plane per "
+                         "node) instead of one process per GPU; N slots, one stream and host thread per slot")
+    ap.add_argument("--multidev-devices", default="",
+                    help="HIP ordinals of the --multidev slots (default 0..N-1; e.g. 0,0 = two slots on one GPU)")
     args = ap.parse_args()
+    if args.multidev:
+        return main_multidev(args)
     if args.family == 6 and args.config in ("C4", "C5"):
         ap.error("--family 6: C1-C3 only (no IPv6 AntreaProxy stage / delta epochs)")
     churn = args.config == "C5"
@@ -553,6 +587,129 @@ def main():
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_multidev(args):
+    """bench.py --multidev N: one process, one gpc context over N device slots (gpc_create_multi),
+    as the agent runs it (one control plane per node, cmd/antrea-agent/agent.go:177). Every slot
+    holds the same epoch; each classifies its own packet shard (weak scaling: --packets per slot)
+    on its own stream, driven by its own host thread; the per-rule counters of all slots are summed
+    in-process by gpc_metrics (the in-process counterpart of the RCCL all-reduce). Same JSON line
+    schema; value = packets of all slots / the wall time of the timed region."""
+    import threading
+    import numpy as np
+    import torch
+    from antrea_amd import gpc, workload
+    from antrea_amd.build import build
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--multidev runs as one process (not under torchrun)")
+    if args.config in ("C5",) or args.family != 4:
+        raise SystemExit("--multidev: C1-C4, IPv4")
+    n_slots = args.multidev
+    devs = [int(x) for x in args.multidev_devices.split(",")] if args.multidev_devices else list(range(n_slots))
+    if len(devs) != n_slots:
+        raise SystemExit("--multidev-devices lists %d ordinals for %d slots" % (len(devs), n_slots))
+    worker = None
+    if not (args.no_parity and args.no_cpu_baseline):
+        from oracle.parity import OracleWorker
+        worker = OracleWorker(args.config)
+    build()
+    _log("building the %s rule set (one context, %d slots on devices %s)" % (args.config, n_slots, devs))
+    t0 = time.time()
+    wl = workload.CONFIGS[args.config]()
+    clf = gpc.Classifier(devices=devs, group_packets=args.group)
+    clf.initialize()
+    clf.batch_install_policy_rule_flows(wl.rules)
+    if getattr(wl, "services", None):
+        workload.install_services(clf, wl)
+    clf.commit()  # published on every slot
+    t_build = time.time() - t0
+    n = args.packets
+    count = not args.no_count
+    slots = []
+    for k, d in enumerate(devs):
+        dev = torch.device("cuda", d)
+        with torch.cuda.device(dev):
+            cols = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + k, device=dev)
+            slots.append({"dev": dev, "cols": cols, "soa": gpc.pkt_soa_device(cols),
+                          "out": torch.empty(2 * n * 8, dtype=torch.uint8, device=dev),
+                          "stream": torch.cuda.Stream(dev)})
+
+    def run(k, steps, evs=None):
+        sl = slots[k]
+        with torch.cuda.device(sl["dev"]):
+            for i in range(steps):
+                if evs is not None:
+                    evs[k][0][i].record(sl["stream"])
+                clf.classify_device(sl["soa"], n, sl["out"].data_ptr(), count=count, stream=sl["stream"].cuda_stream,
+                                    slot=k)
+                if evs is not None:
+                    evs[k][1][i].record(sl["stream"])
+
+    def all_slots(steps, evs=None):
+        th = [threading.Thread(target=run, args=(k, steps, evs)) for k in range(n_slots)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    def sync():
+        for sl in slots:
+            torch.cuda.synchronize(sl["dev"])
+
+    all_slots(args.warmup)
+    sync()
+    clf.reset_counters()
+    sync()
+    evs = [([torch.cuda.Event(enable_timing=True) for _ in range(args.steps)],
+            [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]) for sl in slots]
+    _log("timed region: %d steps x %d slots of %d packets" % (args.steps, n_slots, n))
+    t_start = time.perf_counter()
+    all_slots(args.steps, evs)
+    sync()
+    elapsed = time.perf_counter() - t_start
+    slot_ms = [sum(a.elapsed_time(b) for a, b in zip(*evs[k])) / args.steps for k in range(n_slots)]
+    total = n * args.steps * n_slots
+    metrics = clf.network_policy_metrics() if count else {}
+    parity = None
+    if worker is not None and not args.no_parity:
+        from antrea_amd.gpc import VERDICT_DTYPE
+        k_s = min(n, PARITY_SAMPLE // n_slots or 1)
+        res = []
+        for k, sl in enumerate(slots):
+            idx_h = (torch.arange(k_s, dtype=torch.int64) * n) // k_s
+            idx = idx_h.to(sl["dev"])
+            sample = _host_sample(sl["cols"], idx)
+            v8 = sl["out"].view(torch.uint8).reshape(n, 2, 8)
+            got = np.ascontiguousarray(v8[idx].cpu().numpy()).view(VERDICT_DTYPE).reshape(-1, 2)
+            res.append(worker.check(sample, got))
+        parity = {"checked": sum(r["checked"] for r in res), "mismatches": sum(r["mismatches"] for r in res),
+                  "sample": "%d packets per slot, stride %.0f over each slot's timed batch" % (k_s, n / k_s)}
+        if parity["mismatches"]:
+            print("PARITY FAILURE: %s" % json.dumps(res), file=sys.stderr)
+    cpu = None
+    if worker is not None and not args.no_cpu_baseline:
+        cpu = worker.baseline(args.cpu_seconds)
+    if worker is not None:
+        worker.close()
+    st = clf.image_stats()
+    res = {
+        "metric": "Mpps classified (5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW",
+        "value": round(total / elapsed / 1e6, 2), "unit": "Mpps", "n_gpus": len(set(devs)), "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": args.config, "rules": len(wl.rules), "packets_per_slot": n, "slots": n_slots,
+                   "devices": devs, "flows": st["n_flows"], "counters": count, "build_s": round(t_build, 1),
+                   "parallelism": "one process, gpc_create_multi over %d device slots (packet shards, one epoch "
+                                  "published on every slot)" % n_slots},
+        "slot_kernel_ms": [round(x, 3) for x in slot_ms],
+        "metrics_rules_nonzero": sum(1 for v in metrics.values() if any(v)),
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    if getattr(wl, "services", None):
+        res["metric"] = "Mpps classified (AntreaProxy ServiceLB/EndpointDNAT + policy) @100k rules, 10k Services"
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":

@@ -107,3 +107,23 @@ def test_slot_out_of_range_is_einval():
         c.classify_host(cols, slot=1)
     assert e.value.code == gpc.GPC_EINVAL
     c.close()
+
+
+def test_bench_multidev_two_slots():
+    """bench.py --multidev: one process, gpc_create_multi over two slots of the
+    box's one GPU ([0, 0]), one stream and host thread per slot, the standard JSON line, verdicts of
+    both slots checked against the C oracle on a sample, counters summed over the slots."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--multidev", "2", "--multidev-devices", "0,0", "--config",
+           "C1", "--steps", "3", "--warmup", "1", "--packets", str(1 << 20), "--no-traffic", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["config"]["slots"] == 2 and line["config"]["devices"] == [0, 0]
+    assert line["value"] > 0 and len(line["slot_kernel_ms"]) == 2
+    assert line["parity"]["checked"] > 0 and line["parity"]["mismatches"] == 0, line["parity"]
+    assert line["metrics_rules_nonzero"] > 0
