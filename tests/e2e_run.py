@@ -123,6 +123,8 @@ def run_case(case, backend="emu", compact_last=True):
     steps = []
     nsteps = len(case["steps"])
     for si, st in enumerate(case["steps"]):
+        for kind, name, ns in st.get("delete", []):  # resources the step deletes (kind, name, namespace)
+            ctrl.delete(kind, name, ns)
         for r in st["apply"]:
             ctrl.apply(copy.deepcopy(r))
         rules = ctrl.rules()

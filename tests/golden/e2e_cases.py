@@ -323,6 +323,21 @@ CASES.append(case("ANNP Group Service Reference create and update", "testANNPGro
                              grp("x", "grp-svc1", service=["x", "svc1"]), grp("x", "grp-svc2", service=["x", "svc3"])],
          [("new", "Connected"), ("expect", "x/c", "x/b", "Dropped")], ("reachability2", 1572, 1573))]))
 
+# ---------------------------------------------------------------------------------------- :1439, :1489 (Service refs)
+# testANNPGroupServiceRefPodAdd also probes two Pods it creates (CustomProbes: an app=b client to an
+# app=a server, Dropped); the fixed 9-Pod universe does not model created Pods, so its allPods
+# matrix is the step checked here.
+_svcref = [svc("x", "svc1", {"app": "a"}), svc("x", "svc2", {"app": "b"}),
+           grp("x", "grp-svc1", service=["x", "svc1"]), grp("x", "grp-svc2", service=["x", "svc2"]),
+           annp("x", "annp-grp-svc-ref", 1.0, [at(group="grp-svc1")], ingress=[rule("Drop", TCP80, [peer(group="grp-svc2")])])]
+CASES.append(case("ANNP Group Service Reference add pod", "testANNPGroupServiceRefPodAdd", steps=[
+    step("Port 80 updated", _svcref, [("new", "Connected"), ("expect", "x/b", "x/a", "Dropped")],
+         ("reachability", 1471, 1472))]))
+CASES.append(case("ANNP Group Service Reference delete", "testANNPGroupServiceRefDelete", steps=[
+    step("Port 80", _svcref, [("new", "Connected"), ("expect", "x/b", "x/a", "Dropped")], ("reachability", 1517, 1518)),
+    step("Services deleted", [], [("new", "Connected")], ("reachability2", 1529, 1529),
+         delete=[["Service", "svc1", "x"], ["Service", "svc2", "x"]])]))
+
 # ---------------------------------------------------------------------------------------- :1589 (Group ipBlocks)
 CASES.append(case("ANNP Drop Ingress From Group with ipBlocks to Pod: x/a", "testANNPGroupRefRuleIPBlocks", steps=[
     step("Port 80", [annp("x", "annp-deny-xb-xc-ips-ingress-for-xa", 1.0, [at(pod=POD("a"))],

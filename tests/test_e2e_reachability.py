@@ -58,6 +58,29 @@ def test_fixture_covers_reference_cases():
     n_eval = sum(len(s["eval"]) for c in CASES for s in c["steps"])
     n_pairs = sum(len(s["expected"]) for c in CASES for s in c["steps"])
     assert n_eval >= 30 and n_pairs >= 5000
+    # every antreapolicy_test.go test function that builds a Reachability (48; the fixture records the
+    # reference's SHA-256, so this list is the one of that snapshot)
+    assert len({c["go_func"] for c in CASES if c["go_file"].endswith("antreapolicy_test.go")}) >= 48
+    assert {"testANNPGroupServiceRefPodAdd", "testANNPGroupServiceRefDelete"} <= funcs
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/test/e2e"), reason="reference checkout absent (GPU box)")
+def test_fixture_covers_every_reachability_function():
+    """Scans the reference text: each test function of antreapolicy_test.go that calls
+    NewReachability (helpers excepted) has a case in the fixture."""
+    import re
+    helpers = {"applyDefaultDenyToAllNamespaces", "cleanupDefaultDenyNPs"}
+    has, cur = set(), None
+    with open("/root/reference/test/e2e/antreapolicy_test.go") as f:
+        for line in f:
+            m = re.match(r"func (\w+)\(", line)
+            if m:
+                cur = m.group(1)
+            if cur and "NewReachability(" in line:
+                has.add(cur)
+    funcs = {c["go_func"] for c in CASES}
+    assert has - helpers <= funcs, sorted(has - helpers - funcs)
+    assert len(has - helpers) == 48
 
 
 def test_churn_steps_use_incremental_calls():
