@@ -43,6 +43,11 @@ N_REASSIGN = 30
 COMMIT_EVERY = 100
 N_PKTS, PKT_SEED = 100_000, 0xF1C6
 PATH = os.path.join(HERE, "parity_C5.npz")
+# intermediate states checked by the concurrent-commit device test (tests/test_gpu_boundary.py):
+# the oracle's verdicts for the first N_AT packets after commit marker k of the log (1-based; the
+# final state is `verdicts`)
+AT_COMMITS = (1, 17)
+N_AT = 20_000
 
 
 def _ip(v):
@@ -170,7 +175,17 @@ def make():
     fnp.initialize()
     fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
     t1 = time.time()
-    apply(fnp, log)
+    at = {}
+    n_commit = [0]
+
+    def on_commit():
+        n_commit[0] += 1
+        if n_commit[0] in AT_COMMITS:
+            p = CPipeline(fnp.dump_flows(), parity.tiers_of(wl))
+            sub = {k: v[:N_AT] for k, v in cols.items()}
+            at[n_commit[0]] = np.ascontiguousarray(p.classify(sub, threads=parity.cpu_threads())).view(np.uint32).reshape(-1, 4)
+
+    apply(fnp, log, on_commit)
     t2 = time.time()
     pipe = CPipeline(fnp.dump_flows(), parity.tiers_of(wl))
     want = pipe.classify(cols, threads=parity.cpu_threads(), count=True)
@@ -181,7 +196,9 @@ def make():
     counts = {k: sum(1 for o in log if o["op"] == k) for k in ("add", "del", "uninstall", "install", "reassign", "commit")}
     np.savez_compressed(PATH, verdicts=np.ascontiguousarray(want).view(np.uint32).reshape(-1, 4), metric_conj=conj,
                         metric_val=met, cols_sha256=fx.cols_digest(cols), rules_sha256=fx.rules_digest(wl),
-                        log_sha256=log_digest(log), n_flows=pipe.n_flows, op_counts=json.dumps(counts))
+                        log_sha256=log_digest(log), n_flows=pipe.n_flows, op_counts=json.dumps(counts),
+                        at_commits=np.array(sorted(at), np.int32),
+                        **{"verdicts_at_%d" % k: v for k, v in at.items()})
     print("C5 fixture: %s, %d flows after the log; compile %.0f s, log %.0f s, classify %.1f s"
           % (counts, pipe.n_flows, t1 - t0, t2 - t1, t3 - t2))
 
@@ -190,6 +207,8 @@ def load() -> dict:
     with np.load(PATH, allow_pickle=False) as z:
         d = {k: z[k] for k in z.files}
     d["verdicts"] = np.ascontiguousarray(d["verdicts"]).view(parity.VERDICT_NP).reshape(-1, 2)
+    d["at"] = {int(k): np.ascontiguousarray(d["verdicts_at_%d" % k]).view(parity.VERDICT_NP).reshape(-1, 2)
+               for k in d.get("at_commits", [])}
     d["metrics"] = {int(c): tuple(int(x) for x in v) for c, v in zip(d["metric_conj"], d["metric_val"])}
     return d
 

@@ -194,6 +194,86 @@ def test_gpu_classification_concurrent_with_commits():
     assert {k: tuple(v) for k, v in c.network_policy_metrics().items() if any(v)} == want_m
 
 
+def test_gpu_concurrent_commits_c3_vs_oracle():
+    """C5 as it runs, at full scale: the C3 rule set (100k rules), a control thread
+    replaying the seeded churn log of parity_C5.npz (address adds / deletes incl. base peers,
+    uninstall / reinstall, priority reassignment) and publishing a delta epoch at every commit
+    marker, while the main thread keeps launching classification on its own stream. For the first,
+    a middle and the last commit, the control thread waits until a launch is bound to that epoch
+    (gpc_stream_epoch); that launch's verdicts equal the C oracle over the ORACLE compiler's replay
+    of the same op prefix (make_churn_fixture.py verdicts_at_k / verdicts)."""
+    import torch
+    from oracle import parity
+    from tests.golden import make_churn_fixture as mcf
+    from tests.golden import make_parity_fixtures as fx
+    f = mcf.load()
+    wl, log, cols = mcf.inputs()
+    assert mcf.log_digest(log) == str(f["log_sha256"]) and fx.cols_digest(cols) == str(f["cols_sha256"])
+    n_commits = sum(1 for o in log if o["op"] == "commit")
+    check = {k: f["at"][k] for k in f["at"]}
+    check[n_commits] = f["verdicts"]
+    assert len(check) == 3
+    n = len(cols["src"])
+    dev = torch.device("cuda", 0)
+    signed = {4: np.int32, 2: np.int16, 1: np.uint8}
+    dcols = {k: torch.as_tensor(np.ascontiguousarray(v).view(signed[v.dtype.itemsize])).to(dev) for k, v in cols.items()}
+    soa = gpc.pkt_soa_device(dcols)
+    c = gpc.Classifier(compact_after=-1)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    c.commit()
+    want_epoch = {}  # commit number -> epoch published for it (checked ones)
+    waiting = {"epoch": None}
+    seen = threading.Event()
+    stop, errors = threading.Event(), []
+
+    def control():
+        k = [0]
+
+        def on_commit():
+            c.commit()
+            k[0] += 1
+            if k[0] in check:
+                e = c.image_stats()["epoch"]
+                want_epoch[k[0]] = e
+                seen.clear()
+                waiting["epoch"] = e
+                if not seen.wait(120):
+                    raise RuntimeError("no launch bound to epoch %d" % e)
+            time.sleep(0.001)
+
+        try:
+            mcf.apply(c, log, on_commit)
+        except Exception as e:  # surfaced in the main thread
+            errors.append(e)
+        finally:
+            stop.set()
+
+    s = torch.cuda.Stream(dev)
+    th = threading.Thread(target=control, daemon=True)
+    th.start()
+    bound = {}  # epoch -> device verdicts of a launch bound to it
+    while not stop.is_set() or waiting["epoch"] is not None:
+        out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
+        c.classify_device(soa, n, out.data_ptr(), stream=s.cuda_stream)
+        e = c.stream_epoch(s.cuda_stream)
+        if e == waiting["epoch"]:
+            bound[e] = out
+            waiting["epoch"] = None
+            seen.set()
+        if stop.is_set() and waiting["epoch"] is None:
+            break
+    th.join()
+    torch.cuda.synchronize(dev)
+    assert not errors, errors
+    st = c.image_stats()
+    assert st["n_delta_builds"] >= n_commits - 2, st  # the log went through delta epochs
+    for k, want in sorted(check.items()):
+        got = bound[want_epoch[k]].cpu().numpy().view(gpc.VERDICT_DTYPE).reshape(n, 2)[:len(want)]
+        res = parity.compare(got, want)
+        assert res["mismatches"] == 0, (k, res)
+
+
 def _free_port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
