@@ -103,7 +103,8 @@ constexpr uint32_t kBoxWords = 7;
 //   FK_PTN      n >= 2 sorted points at word B
 //   FK_MKN      n single-term boxes (kBoxWords each: value at +0, mask at +3) at word B
 // Clause data (the segment lists) starts at word kRecLine. Arrays a descriptor points at are
-// followed by at least 4 readable words (chunks are read 16 B at a time).
+// followed by at least 16 readable words (a final chunk reads up to kChunkQuads x 16 B from its
+// window start).
 enum FastKind : uint32_t { FK_GENERIC = 0, FK_ALWAYS = 1, FK_IV1 = 2, FK_MK1 = 3, FK_HASH = 4, FK_IVN = 5, FK_PTN = 6, FK_MKN = 7 };
 constexpr uint32_t kRecFcd = 6;
 constexpr uint32_t kRecLine = 16;
@@ -322,7 +323,7 @@ GPC_HD uint32_t filt_pkt_axis(uint32_t axis, uint32_t v) {
 
 // ------------------------------------------------------------------------------ evaluation
 #ifdef GPC_EMU_STATS  // test-only instrumentation (tests/csrc/emu.cpp); never defined in the product build
-extern "C" unsigned long long gpc_emu_stats[8];
+extern "C" unsigned long long gpc_emu_stats[16];
 extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 #define GPC_STAT(i, v) (gpc_emu_stats[i] += (v))
 #define GPC_TOUCH(p, n) gpc_emu_touch((p), (n), __LINE__)
@@ -883,6 +884,11 @@ GPC_HD bool clause_match(const Img& im, uint32_t roff, const W* c, const Pkt& p)
 
 // Four consecutive words at a dword-aligned address as one 16-B load (gfx950 allows dword-aligned
 // multi-dword global loads).
+#ifndef GPC_CHUNK_QUADS
+#define GPC_CHUNK_QUADS 2
+#endif
+constexpr int kChunkQuads = GPC_CHUNK_QUADS;  // 16-B loads of a final chunk in rule_match's search
+
 template <typename W>
 GPC_HD void load_quad(const W* p, uint32_t* w) {
 #if defined(__HIPCC__)
@@ -937,26 +943,46 @@ GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, const uint32_t*
   }
   // array clauses: window [l, h) of elements still to look at, per clause, in lock step
   while (GPC_WAVE_ANY(ok & ((h[0] > l[0]) | (h[1] > l[1]) | (h[2] > l[2])))) {
+    GPC_STAT(9, 1);
 #pragma unroll
     for (int k = 0; k < kMaxClauses; k++) {
       const bool live = ok & (h[k] > l[k]);
       const uint32_t kind = kd[k];
       const uint32_t stride = kind == FK_IVN ? 2u : kind == FK_PTN ? 1u : kBoxWords;
-      const uint32_t cap = kind == FK_IVN ? 2u : kind == FK_PTN ? 4u : 1u;  // elements per 16-B chunk
-      const bool bin = live & (kind != FK_MKN) & (h[k] - l[k] > cap);
+      // elements one final chunk covers: kChunkQuads 16-B loads issued together (all but the first
+      // only by lanes whose window needs them), one box for FK_MKN
+      const uint32_t cap = kind == FK_IVN ? 2u * kChunkQuads : kind == FK_PTN ? 4u * kChunkQuads : 1u;
+      const uint32_t n = h[k] - l[k];
+      const bool bin = live & (kind != FK_MKN) & (n > cap);
       const uint32_t mid = (l[k] + h[k]) >> 1;
       const uint32_t pos = bin ? mid : l[k];
       const W* q = blob + (live ? base[k] + stride * pos : 0u);  // idle lanes read word 0 (a valid line)
+      const uint32_t words = bin ? 1u : n * stride;  // words of the window
+      uint32_t w[4 * kChunkQuads];
       GPC_TOUCH(q, 16);
-      uint32_t w[4];
       load_quad(q, w);
-      const uint32_t v = x[k], n = h[k] - l[k];
+#pragma unroll
+      for (int j = 1; j < kChunkQuads; j++) {
+        w[4 * j] = w[4 * j + 1] = w[4 * j + 2] = w[4 * j + 3] = 0u;
+        if (live & (words > 4u * j) & (kind != FK_MKN)) {
+          GPC_TOUCH(q + 4 * j, 16);
+          load_quad(q + 4 * j, &w[4 * j]);
+        }
+      }
+      const uint32_t v = x[k];
       // binary step: the last element whose low end is <= v stays in the window
       const bool le = w[0] <= v;
       // chunk compare over the window (at most cap elements)
-      const bool hit = kind == FK_IVN   ? ((w[0] <= v) & (v <= w[1])) | ((n > 1u) & (w[2] <= v) & (v <= w[3]))
-                       : kind == FK_PTN ? (w[0] == v) | ((n > 1u) & (w[1] == v)) | ((n > 2u) & (w[2] == v)) | ((n > 3u) & (w[3] == v))
-                                        : (v & w[3]) == w[0];
+      bool hit = false;
+      if (kind == FK_IVN) {
+#pragma unroll
+        for (uint32_t j = 0; j < 2u * kChunkQuads; j++) hit = hit | ((n > j) & (w[2 * j] <= v) & (v <= w[2 * j + 1]));
+      } else if (kind == FK_PTN) {
+#pragma unroll
+        for (uint32_t j = 0; j < 4u * kChunkQuads; j++) hit = hit | ((n > j) & (w[j] == v));
+      } else {
+        hit = (v & w[3]) == w[0];
+      }
       const bool fin = live & !bin & (hit | (kind != FK_MKN) | (n <= 1u));  // this clause is settled
       if (bin) {
         l[k] = le ? mid : l[k];
@@ -1066,6 +1092,7 @@ GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const ui
   // entry at index 0 (offset 0 is never a record), so the body has no divergent branches.
   // kScanUnroll entries are loaded before any is used: that many loads in flight per lane.
   for (uint32_t j0 = 0; GPC_WAVE_ANY(j0 < total); j0 += kScanUnroll) {
+    GPC_STAT(10, 1);
     Ent ev[kScanUnroll];
 #pragma unroll
     for (int u = 0; u < kScanUnroll; u++) {
@@ -1281,6 +1308,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     uint32_t c0, c1;
     bool more;
     GPC_MARK(ST_SCAN);
+    GPC_STAT(8, 1);
     if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, c0, c1, more);
     else scan_lists<kLists>(im, p, dl, upto, total, after, rH, c0, c1, more);
     GPC_MARK(ST_VER);

@@ -1819,7 +1819,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       while (rec.size() % 16) rec.push_back(0u);
       const uint32_t ext_at = uint32_t(rec.size());
       rec.insert(rec.end(), ext.begin(), ext.end());
-      for (int i = 0; i < 4; i++) rec.push_back(0u);  // 16-B chunk reads past the last array (core.hpp rule_match)
+      for (int i = 0; i < 16; i++) rec.push_back(0u);  // chunk reads past the last array (core.hpp rule_match)
       while (pool.size() % 16) pool.push_back(0u);
       const uint32_t base_off = uint32_t(pool.size());
       for (auto& pt : patches) rec[pt.first] = base_off + ext_at + pt.second;

@@ -7,7 +7,7 @@
 #include <algorithm>
 #include <vector>
 extern "C" {
-unsigned long long gpc_emu_stats[8];
+unsigned long long gpc_emu_stats[16];
 }
 #include <map>
 static std::vector<uintptr_t> g_lines;
@@ -16,6 +16,8 @@ extern "C" {
 unsigned long long gpc_emu_site_lines[2048];
 // per packet (first 1M): record verifications and entries scanned (SIMT divergence studies)
 unsigned gpc_emu_pkt_verif[1 << 20], gpc_emu_pkt_scan[1 << 20];
+// per packet: scan passes (while iterations of eval_part), rule_match search iterations, scan_lists iterations
+unsigned gpc_emu_pkt_pass[1 << 20], gpc_emu_pkt_search[1 << 20], gpc_emu_pkt_iter[1 << 20];
 }
 extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int site) {
   uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -64,7 +66,8 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
              view_bloom_axes(im));
     g_lines.clear();
     g_line_site.clear();
-    const unsigned long long v0 = ::gpc_emu_stats[3], s0 = ::gpc_emu_stats[4];
+    const unsigned long long v0 = ::gpc_emu_stats[3], s0 = ::gpc_emu_stats[4], p0 = ::gpc_emu_stats[8],
+                             q0 = ::gpc_emu_stats[9], r0 = ::gpc_emu_stats[10];
     PacketOut o = classify_packet(im, p, dest, pk->ct_mark ? pk->ct_mark[i] : 0u);
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
@@ -74,6 +77,9 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
     if (i < (1u << 20)) {
       gpc_emu_pkt_verif[i] = unsigned(::gpc_emu_stats[3] - v0);
       gpc_emu_pkt_scan[i] = unsigned(::gpc_emu_stats[4] - s0);
+      gpc_emu_pkt_pass[i] = unsigned(::gpc_emu_stats[8] - p0);
+      gpc_emu_pkt_search[i] = unsigned(::gpc_emu_stats[9] - q0);
+      gpc_emu_pkt_iter[i] = unsigned(::gpc_emu_stats[10] - r0);
     }
     for (auto& kv : g_line_site) gpc_emu_site_lines[kv.second & 2047]++;                                                              // packets
     uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);

@@ -25,7 +25,7 @@ def load():
         subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"),
                         "-I" + os.path.join(ROOT, "antrea_amd", "csrc"), src, "-o", LIB], check=True)
     _lib = C.CDLL(LIB)
-    _lib.gpc_emu_stats_arr = (C.c_ulonglong * 8).in_dll(_lib, "gpc_emu_stats")
+    _lib.gpc_emu_stats_arr = (C.c_ulonglong * 16).in_dll(_lib, "gpc_emu_stats")
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
     _lib.emu_classify.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                   C.POINTER(gpc.gpc_pkt_soa), C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -85,7 +85,7 @@ def stats(reset=False):
     arr = load().gpc_emu_stats_arr
     v = list(arr)
     if reset:
-        for i in range(8):
+        for i in range(16):
             arr[i] = 0
     return v
 
