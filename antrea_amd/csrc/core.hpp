@@ -125,7 +125,13 @@ constexpr int kIdxPerClause = 5;  // sub-indexes (axis, band) per driver clause 
 struct alignas(16) Ent {
   uint32_t x, y, lo, hi;
 };
-GPC_HD uint32_t ent_off(uint32_t x) { return (x >> 8) << 4; }
+// Exact-value entries (composite driver, round 4): bit 31 of x set -> y is the exact value of the
+// table's composite axis cx the entry was listed under (not Bloom bits), and the interval test is
+// the rule's service clause when that is one interval; together they decide both non-band
+// clauses exactly (record word 5 skips them), so a candidate is verified from its first line alone.
+// Record offsets are then < 2^27 words (23 bits of x).
+constexpr uint32_t kEntExactX = 1u << 31;
+GPC_HD uint32_t ent_off(uint32_t x) { return ((x & ~kEntExactX) >> 8) << 4; }
 
 struct SubIdx {  // one (axis, band) bucket index of a driver clause
   uint8_t axis, band, bits, reserved;
@@ -1028,14 +1034,15 @@ GPC_HD bool hard_fast_match(const Img& im, const HardFast& hf, const Pkt& p) {
   return ok;
 }
 
-GPC_HD bool entry_pass(const Pkt& p, const Ent& e) {  // branch-free
+// xv: the packet's value of the table's composite axis (exact-value entries; any value elsewhere).
+GPC_HD bool entry_pass(const Pkt& p, const Ent& e, uint32_t xv) {  // branch-free
   const uint32_t bax = e.x & 15u, iax = (e.x >> 4) & 15u;
   const bool l4 = (e.y & p.l4m) != 0u;
   // Bloom axis < 8: IP / exact-axis bits; 8..14 (probe entry): second service Bloom; 15: none
   const bool bl = (bax == kFiltNoAxis) | ((e.y & p.fm[bax & 7u]) != 0u);
   const uint32_t v = p.ax[iax < AX_N ? iax : 0];
   const bool iv = (iax == kFiltNoAxis) | ((e.lo <= v) & (v <= e.hi));
-  return l4 & bl & iv;
+  return ((e.x & kEntExactX) ? e.y == xv : l4 & bl) & iv;
 }
 
 // Scan length of one table for the packet (the driver clause's candidate count, as eval_part picks
@@ -1084,7 +1091,7 @@ constexpr int kScanUnroll = GPC_SCAN_UNROLL;  // entry loads in flight per lane 
 // entry with one compare instead of kLists - 1.
 template <int kL>
 GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const uint32_t* upto, uint32_t total,
-                       uint32_t after, uint32_t rH, uint32_t& c0, uint32_t& c1, bool& more) {
+                       uint32_t after, uint32_t rH, uint32_t xv, uint32_t& c0, uint32_t& c1, bool& more) {
   const Ent* E = reinterpret_cast<const Ent*>(im.blob);
   c0 = c1 = 0xffffffffu;
   more = false;
@@ -1110,7 +1117,7 @@ GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const ui
 #pragma unroll
     for (int u = 0; u < kScanUnroll; u++) {
       const uint32_t off = ent_off(ev[u].x);
-      ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u]);
+      ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u], xv);
       probe |= ps[u] & ((ev[u].x & 15u) - 8u < 7u);
     }
     // Probe entries that passed: exact membership of the packet in the non-driver point-set
@@ -1298,6 +1305,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   }
   const uint32_t total = upto[kLists - 1];
   const bool one_idx = nc ? nc <= 1 : n0 <= 1 && n1 <= 1;  // table-uniform: every driver list set has <= 1 sub-index
+  const uint32_t xv = nc ? p.ax[th.cx] : 0u;  // exact-value entries exist only in composite lists
   uint32_t after = 0;       // rescan bound (exclusive); record offsets are > 0
   int have = 0;             // result found
   uint32_t level = 0xffffffffu;
@@ -1309,8 +1317,8 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     bool more;
     GPC_MARK(ST_SCAN);
     GPC_STAT(8, 1);
-    if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, c0, c1, more);
-    else scan_lists<kLists>(im, p, dl, upto, total, after, rH, c0, c1, more);
+    if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, xv, c0, c1, more);
+    else scan_lists<kLists>(im, p, dl, upto, total, after, rH, xv, c0, c1, more);
     GPC_MARK(ST_VER);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
@@ -1521,7 +1529,7 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
       f.y = ew[5];
       f.lo = ew[6];
       f.hi = ew[7];
-      if (!entry_pass(p, f)) continue;
+      if (!entry_pass(p, f, 0u)) continue;  // (journal entries are never exact-value entries)
       const uint32_t off = ew[3];
       const uint32_t* rec = pool + off;
       GPC_TOUCH(rec, 4 * kRecLine);

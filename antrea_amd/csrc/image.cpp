@@ -951,6 +951,8 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     size_t nsoft = 0;
     std::vector<std::vector<uint32_t>> xsets;
     std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>> sub;
+    std::vector<std::pair<uint32_t, uint32_t>> xpatch;  // (record word 5 offset, skip bits) of exact-value rules
+    const bool exact_ok = !std::getenv("GPC_NO_EXACT_X");  // (experiments)
     for (size_t rank = 0; rank < rs.size() && ok; rank++) {
       const RuleB& r = *rs[rank];
       if (r.hard) continue;
@@ -971,7 +973,23 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       if (!ok) break;
       std::sort(xs.begin(), xs.end());
       xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
-      const std::array<uint32_t, 4> ent = entry_of(r, cb, rec_off[rank], span);
+      std::array<uint32_t, 4> ent = entry_of(r, cb, rec_off[rank], span);
+      // exact-value entry (core.hpp kEntExactX) when the rule's remaining clause, if any, is one
+      // interval: the entry then decides every clause but the band clause (record word 5 skips them)
+      int sc = -1;
+      uint32_t sax = kFiltNoAxis, slo = 0, shi = 0;
+      bool exact = exact_ok && r.n <= 3 && rec_off[rank] < (1u << 27);
+      if (exact && r.n == 3) {
+        sc = 3 - cb - ce;
+        const auto& cl = r.clause[sc];
+        exact = !cl.empty() && cl[0].t.size() == 1 && cl[0].t[0].axis < AX_N &&
+                clause_hull(cl, cl[0].t[0].axis, &slo, &shi) && clause_is_interval(cl, cl[0].t[0].axis, slo, shi);
+        if (exact) sax = cl[0].t[0].axis;
+      }
+      if (exact) {
+        ent = {((rec_off[rank] >> 4) << 8) | (sax << 4) | kFiltNoAxis | kEntExactX, 0u, slo, shi};
+        xpatch.push_back({rec_off[rank] + 5, ((1u << ce) | (sc >= 0 ? 1u << sc : 0u)) << (3 * cb)});
+      }
       for (auto& a : r.clause[cb]) {
         AtomKey key;
         if (!atom_key(a, &key) || key.axis > AX_CTDST) {
@@ -1004,7 +1022,11 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       be.clear();
       for (auto& e : kv.second)
         for (uint64_t k = e.key.lo >> sh; k <= (e.key.hi >> sh); k++)
-          for (uint32_t x : xsets[e.xi]) be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), e.ent});
+          for (uint32_t x : xsets[e.xi]) {
+            std::array<uint32_t, 4> en = e.ent;
+            if (en[0] & kEntExactX) en[1] = x;
+            be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), en});
+          }
       std::sort(be.begin(), be.end());
       be.erase(std::unique(be.begin(), be.end()), be.end());
       const uint32_t nb = 1u << bits;
@@ -1045,6 +1067,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     th.xmap_off = B.put(xmap.data(), xmap.size(), 16);
     th.cband = uint8_t(cb);
     th.cx = uint8_t(X);
+    for (auto& pt : xpatch) B.w[pt.first] |= pt.second;
     return;
   }
 }
