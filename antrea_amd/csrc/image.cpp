@@ -2117,6 +2117,8 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
       th.n_hfast = uint32_t(hard_fast.size());
       for (size_t h = 0; h < hard_fast.size(); h++) th.hf[h] = hard_fast[h];
     }
+    if (std::getenv("GPC_IMAGE_DEBUG"))
+      std::fprintf(stderr, "table %d: %zu rules, %u hard (%u inline)\n", t, rs.size(), th.n_hard, th.n_hfast);
     T_.lap(1);
     // composite driver first: a table that has one never scans the plain sub-indexes, so they are
     // not emitted (only the always lists, which the composite driver scans too)
