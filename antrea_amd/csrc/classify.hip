@@ -296,29 +296,14 @@ __device__ __forceinline__ uint64_t logical_block(uint32_t mode) {
 // orig != null: a grouped batch (group_tiles_kernel): pk holds the grouped columns, lane i of the
 // logical block order classifies grouped packet i, whose caller index is orig[i]. IPv6 batches come
 // here as code columns (v6_code_kernel) against the IPv6 image.
-template <bool kDelta, bool kSvc, int kStage, bool kSort = false>
-__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta ? GPC_DELTA_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
-    EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
-    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
-    uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
-  // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
-  __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
-#if defined(GPC_STAMPS)
-  {
-    uint32_t* st = gpc_stamp_lds();
-    if (threadIdx.x < ST_N + 1) st[threadIdx.x] = threadIdx.x == ST_N ? uint32_t(ST_PRE) : 0u;
-    const uint64_t now = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) st[ST_N + 1] = uint32_t(now), st[ST_N + 2] = uint32_t(now >> 32);
-    __syncthreads();
-  }
-  auto body = [&]() {
-#else
-  {
-#endif
-  const uint64_t block_base = logical_block<kGroupTile / block_threads<kSort>()>(xcd_order) * block_threads<kSort>();
-  uint64_t i = block_base + threadIdx.x;
-  if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
-  if (i >= n) return;
+// Packet i of the batch through the Service stage (kSvc) and the policy stage(s) of the launch;
+// pkt_lane / pkt_stride: this lane's column of the block's [word][lane] packet table in LDS.
+template <bool kDelta, bool kSvc, int kStage>
+__device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t i, uint4* __restrict__ out,
+                                             uint4* __restrict__ lb_out, unsigned long long* __restrict__ counters, int count,
+                                             const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
+                                             uint2* __restrict__ gout, uint4* __restrict__ park, uint32_t* pkt_lane,
+                                             uint32_t pkt_stride) {
   // Ingress launch: only the egress action of the egress half is read here; nothing of it is held
   // over the walk (the result is stored as a half).
   uint32_t ea = 0;
@@ -402,7 +387,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
     im.n_img = 2u;
   }
-  Pkt p(pkt_lds + threadIdx.x, block_threads<kSort>());
+  Pkt p(pkt_lane, pkt_stride);
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
            pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
            view_bloom_axes(im));
@@ -443,6 +428,33 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if (kStage == 2) store2(g.conj, g.packed);
   else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
   else out[i] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
+}
+
+template <bool kDelta, bool kSvc, int kStage, bool kSort = false>
+__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta ? GPC_DELTA_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
+    EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
+    unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
+    uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
+  // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
+  __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
+#if defined(GPC_STAMPS)
+  {
+    uint32_t* st = gpc_stamp_lds();
+    if (threadIdx.x < ST_N + 1) st[threadIdx.x] = threadIdx.x == ST_N ? uint32_t(ST_PRE) : 0u;
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) st[ST_N + 1] = uint32_t(now), st[ST_N + 2] = uint32_t(now >> 32);
+    __syncthreads();
+  }
+  auto body = [&]() {
+#else
+  {
+#endif
+  const uint64_t block_base = logical_block<kGroupTile / block_threads<kSort>()>(xcd_order) * block_threads<kSort>();
+  uint64_t i = block_base + threadIdx.x;
+  if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
+  if (i >= n) return;
+  classify_one<kDelta, kSvc, kStage>(ep, pk, i, out, lb_out, counters, count, orig, mid, gout, park,
+                                     pkt_lds + threadIdx.x, block_threads<kSort>());
 #if defined(GPC_STAMPS)
   };
   body();
