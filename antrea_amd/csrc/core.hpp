@@ -187,7 +187,8 @@ struct ImageHdr {
   uint32_t n_slots;
   uint32_t v6_lpm;      // IPv6 image: word offset of its V6Lpm block (0 in IPv4 images)
   uint32_t isc;         // IngressSecurityClassifier bypasses installed (kIsc* bits)
-  uint32_t bloom_axes;  // bit a: some driver entry tests the Bloom bits of axis a (Pkt::fm[a] is needed)
+  uint32_t bloom_axes;  // bit a: some driver entry tests the Bloom bits of axis a (Pkt::fm[a] is needed);
+                        // kBloomL4: some entry is not an exact-value entry (Pkt::l4m is needed)
   uint32_t live;        // bit t - 1: table t has rules (hard or soft); an empty table is a miss
 };
 // IngressSecurityClassifier (pipeline.go:2144-2182), from the installed flows: bit d (gpc_dest d =
@@ -310,6 +311,7 @@ GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0
 // top 8 / 16 / 24 / 32 address bits; exact axes (in_port, reg1, reg7, tun_id): band 4 keyed by the value.
 constexpr uint32_t kFiltIpBits = 20, kFiltL4Shift = 20, kFiltL4Bits = 12;
 constexpr uint32_t kFiltNoAxis = 15u;
+constexpr uint32_t kBloomL4 = 1u << 8;  // ImageHdr / JournalHdr bloom_axes: the service bits are tested
 constexpr uint32_t kFiltL4All = 0xfff00000u;
 GPC_HD uint32_t filt_ip_bit(uint32_t axis, uint32_t band, uint32_t key) {
   return 1u << uint32_t((uint64_t(mix32(key ^ (axis << 24) ^ (band << 28))) * kFiltIpBits) >> 32);
@@ -1856,8 +1858,9 @@ GPC_HD void make_pkt(Pkt& p, uint32_t src, uint32_t dst, uint32_t sport, uint32_
   make_axes(p, src, dst, sport, dport, proto, out_port, in_port, svc_group, tun_id, ct_src, ct_dst, ct_state);
 #pragma unroll
   for (uint32_t a = 0; a < 8; a++) p.fm[a] = (bloom_axes >> a) & 1u ? filt_pkt_axis(a, p.ax[a]) : 0u;
-  p.l4m = filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12) |
-          filt_l4x_bit(proto_class(proto), p.ax[AX_L4D] & 0xffffu);
+  p.l4m = (bloom_axes & kBloomL4) ? filt_l4_bit(proto_class(proto), (p.ax[AX_L4D] & 0xffffu) >> 12) |
+                                        filt_l4x_bit(proto_class(proto), p.ax[AX_L4D] & 0xffffu)
+                                  : 0u;
 }
 
 }  // namespace gpc

@@ -1025,6 +1025,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
           for (uint32_t x : xsets[e.xi]) {
             std::array<uint32_t, 4> en = e.ent;
             if (en[0] & kEntExactX) en[1] = x;
+            else out->hdr.bloom_axes |= bloom_axis_bit(en[0]) | kBloomL4;
             be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), en});
           }
       std::sort(be.begin(), be.end());
@@ -1868,7 +1869,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       JournalTable& jt = tables_[t - 1];
       for (int k = 0; k < 2 && k < r.n; k++) {
         const std::array<uint32_t, 4> pf = entry_of(r, k, 0u, span);
-        bloom_axes_ |= bloom_axis_bit(pf[0]);
+        bloom_axes_ |= bloom_axis_bit(pf[0]) | kBloomL4;
         for (auto& a : r.clause[k]) {
           AtomKey key;
           const bool keyed = atom_key(a, &key) && journal_keys(key, &keys);
@@ -2132,14 +2133,16 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         RuleB& r = *rs[rank];
         if (r.hard || k >= r.n) continue;
         std::array<uint32_t, 4> ent = entry_of(r, k, rec_off[rank], span);
-        out->hdr.bloom_axes |= bloom_axis_bit(ent[0]);
         for (auto& a : r.clause[k]) {
           AtomKey key;
           if (!atom_key(a, &key)) {
             always.push_back(ent);
+            out->hdr.bloom_axes |= bloom_axis_bit(ent[0]) | kBloomL4;
             continue;
           }
           sub[{key.axis, key.band}].push_back({key, ent});
+          // (a composite table emits no plain sub-index entry: only what it emits needs filter bits)
+          if (!composite) out->hdr.bloom_axes |= bloom_axis_bit(ent[0]) | kBloomL4;
         }
       }
       // Host addresses get the exact band only where they dominate the axis (Pod / AddressGroup
