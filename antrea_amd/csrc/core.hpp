@@ -291,12 +291,16 @@ GPC_HD uint32_t bucket_of(uint32_t axis, uint32_t band, uint32_t bits, uint32_t 
   if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
   return v & ((1u << bits) - 1u);
 }
+// Hash of a composite table's exact value x: the value-map bit and every sub-index bucket of the
+// packet derive from this one mix (the compiler computes it once per table: two multiplies, then
+// one mix per sub-index -- 32-bit multiplies issue at a quarter of the VALU rate).
+GPC_HD uint32_t cx_hash(uint32_t x) { return mix32(x ^ 0x2545f491u); }
 // Bit of exact value x in a composite table's value map (TableHdr xmap_off, 2^16 bits).
-GPC_HD uint32_t cx_bit(uint32_t x) { return mix32(x ^ 0x2545f491u) >> 16; }
+GPC_HD uint32_t cx_bit(uint32_t x) { return cx_hash(x) >> 16; }
 // Composite driver bucket (TableHdr cidx): IP band key of v on (axis, band) with the exact value x.
 GPC_HD uint32_t cbucket_of(uint32_t band, uint32_t bits, uint32_t v, uint32_t x) {
   const uint32_t key = v >> ip_band_shift(band);
-  return mix32((key * 0x9e3779b1u) ^ mix32(x ^ (band << 28) ^ 0x5bd1e995u)) >> (32 - bits);
+  return mix32((key * 0x9e3779b1u) ^ cx_hash(x) ^ (band * 0x68e31da4u)) >> (32 - bits);
 }
 // Point-hash key of value v on `axis` of the record at word offset `off` (16-word aligned, < 2^28):
 // (off / 16) << 4 | axis in the high word. ~0 (empty slot) is never a key.
@@ -304,8 +308,9 @@ GPC_HD uint64_t point_key(uint32_t off, uint32_t axis, uint32_t v) {
   return (uint64_t(((off >> 4) << 4) | axis) << 32) | v;
 }
 constexpr uint32_t kHashSlots = 2;  // 16-B buckets, two choices: one 16-B load per choice
+// The two cuckoo choices take the low and the high half of one mix (one 64-bit mix per probe).
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
-GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k ^ 0x9e3779b97f4a7c15ull) >> 32) & mask; }
+GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k) >> 32) & mask; }
 
 // Entry filter bits. IP axes: band 1/2/3/4 = prefix length 8-15 / 16-23 / 24-31 / 32 keyed by the
 // top 8 / 16 / 24 / 32 address bits; exact axes (in_port, reg1, reg7, tun_id): band 4 keyed by the value.
