@@ -745,6 +745,10 @@ GPC_HD uint32_t jkey(uint32_t axis, uint32_t band, uint32_t v) {  // bucket key 
   if (axis == AX_L4D || axis == AX_L4S) return (proto_class(v >> 16) << 13) | ((v & 0xffffu) >> 3);
   return v;
 }
+// Journal key of a table with a composite base index (TableHdr n_cidx): the band key of the band
+// clause combined with the packet's value x of the composite axis, so a chain lists only the changed
+// rules that hold both (as the base's composite buckets do); a collision costs a verification.
+GPC_HD uint32_t jxkey(uint32_t key, uint32_t x) { return mix32((key * 0x9e3779b1u) ^ cx_hash(x)); }
 GPC_HD uint32_t jmeta(uint32_t table, uint32_t clause, uint32_t axis, uint32_t band) {
   return table | (clause << 3) | (axis << 5) | (band << 9);
 }
@@ -1514,6 +1518,7 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
       const uint32_t axis = jt.kinds[d][i] & 15u, band = jt.kinds[d][i] >> 4;
       meta = jmeta(table, d, axis, band);
       key = jkey(axis, band, p.ax[axis]);
+      if (bt.n_cidx) key = jxkey(key, p.ax[bt.cx]);
       e = jhead(pool, jh, jbucket(meta, key, jh->lg));
     }
     const bool always = i == jt.n_kinds[d];

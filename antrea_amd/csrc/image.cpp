@@ -1693,8 +1693,20 @@ bool journal_keys(const AtomKey& k, std::vector<uint32_t>* out) {
 
 }  // namespace
 
+// Chain-head table size: chains are per head bucket, so a journal of many entries needs many heads
+// (a composite-keyed journal lists a rule once per key and value). 16 bits for small bases, up to 21
+// (1 M heads, 16 K head pages; the page table travels with every epoch: 64 KB) for C3-sized ones.
+constexpr uint32_t kJournalLgMin = 16, kJournalLgMax = 20;
+
 void Journal::reset(const HostImage* base, uint32_t lg) {
   base_ = base;
+  if (!lg) {
+    uint32_t mx = kJournalLgMax;
+    if (const char* e = std::getenv("GPC_JOURNAL_LG_MAX"))  // (experiments)
+      mx = uint32_t(std::min(24, std::max(int(kJournalLgMin), std::atoi(e))));
+    lg = kJournalLgMin;
+    while (lg < mx && base && (uint64_t(1) << lg) < uint64_t(base->n_rids) * 16) lg++;
+  }
   lg_ = lg;
   pool.assign(16, 0u);  // offset 0 is "none"
   uploaded = 0;
@@ -1865,14 +1877,28 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       }
       live_[r.conj_id] = orid;
       n_live++;
-      // driver entries for clauses 0 and 1
+      // driver entries for clauses 0 and 1. A table with a composite base index walks only its band
+      // clause, keyed by (band key, composite value) (core.hpp jxkey): one entry per key and value of
+      // the rule's other clause; a rule whose other clause is not such a value set goes to the always
+      // list of the band clause.
       JournalTable& jt = tables_[t - 1];
+      const TableHdr& bt = base_->hdr.t[t - 1];
+      std::vector<uint32_t> xs;
+      bool xok = false;
+      if (bt.n_cidx && r.n >= 2) {
+        xok = r.clause[1 - bt.cband].size() <= kCompositeMaxValues;
+        for (auto& a : r.clause[1 - bt.cband]) {
+          xok = xok && a.t.size() == 1 && a.t[0].mask == 0xffffffffu && a.t[0].axis == bt.cx;
+          if (xok) xs.push_back(a.t[0].val);
+        }
+      }
       for (int k = 0; k < 2 && k < r.n; k++) {
+        if (bt.n_cidx && k != bt.cband) continue;  // the kernel never walks the other clause's chains
         const std::array<uint32_t, 4> pf = entry_of(r, k, 0u, span);
         bloom_axes_ |= bloom_axis_bit(pf[0]) | kBloomL4;
         for (auto& a : r.clause[k]) {
           AtomKey key;
-          const bool keyed = atom_key(a, &key) && journal_keys(key, &keys);
+          const bool keyed = (!bt.n_cidx || xok) && atom_key(a, &key) && journal_keys(key, &keys);
           if (!keyed) {
             const uint32_t e[kJEntWords] = {jt.always[k], 0u, (orid << kJOridShift), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
             const uint32_t eo = append(e, kJEntWords, kJEntWords);
@@ -1890,6 +1916,13 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
             jt.kinds[k][jt.n_kinds[k]++] = uint8_t(kind);
           }
           const uint32_t meta = jmeta(uint32_t(t), uint32_t(k), key.axis, key.band);
+          if (bt.n_cidx) {  // (band key, value) keys
+            std::vector<uint32_t> kx;
+            kx.reserve(keys.size() * xs.size());
+            for (uint32_t kv : keys)
+              for (uint32_t x : xs) kx.push_back(jxkey(kv, x));
+            keys.swap(kx);
+          }
           for (uint32_t kv : keys) {
             const uint32_t bkt = jbucket(meta, kv, lg_);
             const uint32_t e[kJEntWords] = {heads_[bkt], kv, meta | (orid << kJOridShift), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};

@@ -81,7 +81,8 @@ int extend_image6(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t h
 // device only receives pool[uploaded, size). Cost per commit ~ the changed rules, not the journal.
 class Journal {
  public:
-  void reset(const HostImage* base, uint32_t lg = 16);
+  // lg: log2 of the chain-head table; 0 = sized to the base (kJournalLgMin..kJournalLgMax)
+  void reset(const HostImage* base, uint32_t lg = 0);
   // IPv6 journal: rules gathered as an IPv6 image over the base's codes (base->codes6)
   void set_family(int fam) { fam_ = fam; }
   // IPv6: the overflow LPM table the next epoch header points at (appended by the next apply)

@@ -432,6 +432,29 @@ class Classifier:
         _check(self._addr_call(self.lib.gpc_del_rule_addrs, rule_id, addr_type, addrs, priority),
                "DeletePolicyRuleAddress")
 
+    def rule_addr_ip4(self, add: bool, rule_id: int, addr_type: str, ip4: int, priority=None):
+        """AddPolicyRuleAddress (add) / DeletePolicyRuleAddress of one IPv4 host address given as an
+        int, through preallocated argument buffers: no string parsing or per-call marshalling, so a
+        control loop (bench.py C5) pays the library's cost per op, as a cgo caller would. Not
+        thread-safe (one buffer per classifier)."""
+        if not hasattr(self, "_fast_addr"):
+            self._fast_addr = gpc_addr()
+            self._fast_addr.kind = ADDR_KINDS["ip"]
+            self._fast_addr.family = 4
+            self._fast_prio = C.c_uint16(0)
+        a = self._fast_addr
+        a.ip[0], a.ip[1], a.ip[2], a.ip[3] = (ip4 >> 24) & 255, (ip4 >> 16) & 255, (ip4 >> 8) & 255, ip4 & 255
+        p = None
+        if priority is not None:
+            self._fast_prio.value = priority
+            p = C.pointer(self._fast_prio)
+        t = 0 if addr_type == "src" else 1
+        if add:
+            rc = self.lib.gpc_add_rule_addrs(self.h, rule_id, t, C.byref(a), 1, p, 0, 0)
+        else:
+            rc = self.lib.gpc_del_rule_addrs(self.h, rule_id, t, C.byref(a), 1, p)
+        _check(rc, "AddPolicyRuleAddress" if add else "DeletePolicyRuleAddress")
+
     def reassign_flow_priorities(self, updates: Dict[int, int], table: str):
         ks = list(updates)
         f = (C.c_uint16 * max(1, len(ks)))(*ks)

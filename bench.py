@@ -90,32 +90,47 @@ class _ChurnOps:
 
     def apply(self, k):
         rng, clf = self.rng, self.clf
+        fast = getattr(clf, "rule_addr_ip4", None)  # the library's per-op cost, not string marshalling
         for _ in range(k):
             if self.added and rng.random() < 0.5:
-                rid, a, prio = self.added.pop(int(rng.integers(len(self.added))))
-                clf.delete_policy_rule_address(rid, "src", [a], prio)
+                rid, v, prio = self.added.pop(int(rng.integers(len(self.added))))
+                if fast:
+                    fast(False, rid, "src", v, prio)
+                else:
+                    clf.delete_policy_rule_address(rid, "src", [_ip4(v)], prio)
             else:
                 r = self.rules[int(rng.integers(len(self.rules)))]
                 v = int(rng.integers(0, 1 << 32))
-                a = "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
-                clf.add_policy_rule_address(r["flow_id"], "src", [a], r.get("priority"))
-                self.added.append((r["flow_id"], a, r.get("priority")))
+                if fast:
+                    fast(True, r["flow_id"], "src", v, r.get("priority"))
+                else:
+                    clf.add_policy_rule_address(r["flow_id"], "src", [_ip4(v)], r.get("priority"))
+                self.added.append((r["flow_id"], v, r.get("priority")))
         self.issued += k
 
 
-def _churn_loop(ops, rate, max_batch, stop, rec):
+def _ip4(v):
+    return "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+def _churn_loop(ops, rate, max_batch, stop, rec, interval=0.0):
     """Control-plane thread of C5. Address ops (_ChurnOps) become due at `rate` per second; each
-    pass applies every op due so far (at most `max_batch`) and publishes them with one gpc_commit.
-    Per op, the update latency is the time from the op being due to the commit that made it
-    visible returning; rec gets (ops, commit_seconds, [latencies]) per commit."""
+    pass applies every op due so far (at most `max_batch`) and publishes them with one gpc_commit,
+    at most one commit per `interval` seconds (the agent's bundle batching: every commit is an
+    epoch the data path switches to). Per op, the update latency is the time from the op being due
+    to the commit that made it visible returning; rec gets (ops, commit_seconds, [latencies]) per
+    commit."""
     import numpy as np
     t0 = time.perf_counter()
     base = ops.issued
+    last = t0 - interval
     while not stop.is_set():
-        due = int((time.perf_counter() - t0) * rate) - (ops.issued - base)
-        if due <= 0:
+        now = time.perf_counter()
+        due = int((now - t0) * rate) - (ops.issued - base)
+        if due <= 0 or now - last < interval:
             time.sleep(0.0002)
             continue
+        last = now
         due = min(due, max_batch)
         first = ops.issued - base
         ops.apply(due)
@@ -358,6 +373,8 @@ def main():
     ap.add_argument("--keep-pmc", default="", help="directory that keeps the PMC passes' counter CSVs")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
+    ap.add_argument("--commit-interval-ms", type=float, default=10.0,
+                    help="C5: at most one gpc_commit per this many ms (ops due meanwhile share it)")
     ap.add_argument("--group", type=int, default=0,
                     help="gpc_config.group_packets: 0 = auto (batches >= 2^18 against images >= 4 MB), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),
@@ -452,8 +469,8 @@ def main():
         sys.setswitchinterval(2e-4)  # the control thread must not wait 5 ms for the GIL behind launches
         stop = threading.Event()
         churn_ops = _ChurnOps(clf, wl, seed=1234)  # the same op stream on every rank
-        th = threading.Thread(target=_churn_loop, args=(churn_ops, args.churn_rate, args.max_batch, stop, lat),
-                              daemon=True)
+        th = threading.Thread(target=_churn_loop, args=(churn_ops, args.churn_rate, args.max_batch, stop, lat,
+                                                        args.commit_interval_ms / 1e3), daemon=True)
         th.start()
         while len(lat) < 5:  # control loop running before the timed region
             time.sleep(0.01)
@@ -484,6 +501,7 @@ def main():
         pct = lambda a, q: round(float(np.percentile(a, q)), 3) if len(a) else None
         update = {"ops": int(ops), "commits": len(rec), "ops_per_s": round(ops / elapsed, 1),
                   "target_ops_per_s": args.churn_rate, "ops_per_commit_mean": round(ops / max(1, len(rec)), 1),
+                  "commit_interval_ms": args.commit_interval_ms, "timed_s": round(elapsed, 2),
                   "op_latency_ms": {"p50": pct(op_ms, 50), "p99": pct(op_ms, 99),
                                     "max": round(float(op_ms.max()), 3) if len(op_ms) else None},
                   "commit_ms": {"p50": pct(commit_ms, 50), "p99": pct(commit_ms, 99)},
