@@ -112,6 +112,7 @@ struct DevEpoch {
   std::shared_ptr<DevImage> base;       // shared by the delta epochs built on it
   std::shared_ptr<DevImage> pool;       // journal pool of that base (d_hdr unused; append-only)
   uint32_t jhdr = 0;                    // this epoch's JournalHdr in the pool (0: base only)
+  int jmode = kModeBase;                // what the kernel reads of it (Journal::mode: point extensions only, or the journal)
   std::shared_ptr<DevImage> svc;        // Service image (d_hdr unused), shared until Services change
   std::shared_ptr<DevImage> v6;         // IPv6 base image (ipv6_enabled), shared by its delta epochs
   std::shared_ptr<DevImage> v6_pool;    // journal pool of that base (append-only)
@@ -158,8 +159,10 @@ struct DevState {
 // max(kDeltaMinRules, base rules / kDeltaFraction) live rules or its pool would pass its capacity.
 constexpr size_t kDeltaMinRules = 16384;
 constexpr size_t kDeltaFraction = 4;
+constexpr size_t kPendingCapFactor = 2;  // journal allowance while a background compaction is pending
 constexpr size_t kPoolWords = size_t(256) << 20;  // 1 GiB journal pool per base (HBM is 288 GB)
 constexpr size_t kMinUploadBytes = size_t(1) << 20;
+constexpr size_t kExtCompactValues = size_t(1) << 16;  // live point-extension values that ask for a compaction
 
 // Background compaction: a shadow compiler replays the control-plane log on its own thread; asked
 // to compact, it builds a full image of its state at a commit boundary, catches up on the log by
@@ -192,6 +195,7 @@ struct gpc_ctx {
   // full holds `data` through every blocking launch and would otherwise re-take it ahead of a
   // waiting commit (std::mutex is not fair): measured 0.8-1.5 s per commit beside classification.
   std::atomic<uint32_t> publishers{0};
+  std::atomic<int> fail_uploads{0};  // gpc_debug_fail_uploads: this context's next commit / replay uploads fail
   // Launch pacing (pace_take): per (slot, stream), the events after the last kPaceDepth calls.
   std::mutex pace_mu;
   std::map<std::pair<uint32_t, StreamKey>, std::deque<hipEvent_t>> pace;
@@ -364,25 +368,44 @@ static uint32_t group_axes(const HostImage& h) {
   return m;
 }
 
-static std::atomic<int> g_fail_uploads{0};  // gpc_debug_fail_uploads (fault injection in tests)
 
 // Launch pacing. A caller that enqueues classify calls faster than the device runs them fills the
 // stream's hardware queue, and its next launch then blocks -- inside the data lock, which a commit
 // needs to publish its epoch (measured: commits waited 0.8-1.4 s beside a saturating caller). So a
-// call first waits, outside every lock, until the call kPaceDepth calls before it on the same stream
-// has finished; the device still has kPaceDepth calls queued, and no launch blocks.
-constexpr size_t kPaceDepth = 8;
+// call first waits, outside every lock, until the call `depth` (gpc_config.launch_pacing, default
+// kPaceDepth) calls before it on the same stream has finished; the device still has that many calls
+// queued, and no launch blocks. The per-stream queues are bounded like the grouping scratch: past
+// kPaceStreams streams, the queues whose events have all completed (idle streams, exited threads of
+// hipStreamPerThread) are dropped and their events destroyed.
+constexpr size_t kPaceDepth = 8, kPaceStreams = 64;
+static void pace_trim(gpc_ctx* ctx) {  // pace_mu held
+  if (ctx->pace.size() <= kPaceStreams) return;
+  for (auto it = ctx->pace.begin(); it != ctx->pace.end();) {
+    bool idle = true;
+    for (hipEvent_t e : it->second) idle = idle && hipEventQuery(e) == hipSuccess;
+    if (!idle) {
+      (void)hipGetLastError();
+      ++it;
+      continue;
+    }
+    for (hipEvent_t e : it->second) (void)hipEventDestroy(e);
+    it = ctx->pace.erase(it);
+  }
+}
 struct Pace {
   gpc_ctx* ctx;
   uint32_t slot;
   hipStream_t st;
   hipEvent_t ev = nullptr;
   Pace(gpc_ctx* c, uint32_t sl, hipStream_t s, bool on) : ctx(c), slot(sl), st(s) {  // the slot's device is current
-    if (!on) return;
+    const int32_t cfg = ctx->cfg.launch_pacing;
+    if (!on || cfg < 0) return;
+    const size_t depth = cfg > 0 ? size_t(cfg) : kPaceDepth;
     {
       std::lock_guard<std::mutex> p(ctx->pace_mu);
+      pace_trim(ctx);
       auto& q = ctx->pace[{slot, stream_key(st)}];
-      if (q.size() >= kPaceDepth) {
+      if (q.size() >= depth) {
         ev = q.front();
         q.pop_front();
       }
@@ -404,8 +427,11 @@ struct Pace {
   }
 };
 
-static int upload_image(const HostImage& h, int device, hipStream_t s, std::shared_ptr<DevImage>* out) {
-  if (g_fail_uploads.load() > 0 && g_fail_uploads.fetch_sub(1) > 0) return -GPC_EDEV;
+// fail: the context's gpc_debug_fail_uploads counter (commit / replay uploads only; the background
+// compactor's uploads pass none)
+static int upload_image(const HostImage& h, int device, hipStream_t s, std::shared_ptr<DevImage>* out,
+                        std::atomic<int>* fail = nullptr) {
+  if (fail && fail->load() > 0 && fail->fetch_sub(1) > 0) return -GPC_EDEV;
   auto d = std::make_shared<DevImage>();
   d->s = s;
   d->device = device;
@@ -969,8 +995,9 @@ int gpc_commit(gpc_ctx* ctx) { return commit_impl(ctx, false); }
 // buffer is rebuilt from the host shadow state -- base image, journal pool, IPv6 and Service
 // images -- without compiler work; the realized flows, conj ids and counter slots are unchanged.
 // Device counters restart from zero, as OVS flow counters do after the flows are replayed.
-int gpc_debug_fail_uploads(int n) {
-  g_fail_uploads.store(n > 0 ? n : 0);
+int gpc_debug_fail_uploads(gpc_ctx* ctx, int n) {
+  if (!ctx) return -GPC_EINVAL;
+  ctx->fail_uploads.store(n > 0 ? n : 0);
   return GPC_OK;
 }
 
@@ -1027,15 +1054,16 @@ int gpc_replay(gpc_ctx* ctx) {
     hipStream_t us = D.ustream;
     ne[k].base_gen = ctx->gen4;
     ne[k].v6_gen = ctx->gen6;
-    rc = upload_image(ctx->last, D.device, us, &ne[k].base);
+    rc = upload_image(ctx->last, D.device, us, &ne[k].base, &ctx->fail_uploads);
     if (!rc && jn.active()) {
       rc = alloc_pool(D.device, us, &ne[k].pool);
       if (!rc && hip_ok(hipMemcpyAsync(ne[k].pool->d_blob, jn.pool.data(), jn.pool.size() * 4, hipMemcpyHostToDevice, us)))
         rc = -GPC_EDEV;
       ne[k].jhdr = jn.hdr_off;
+      ne[k].jmode = jn.mode();
     }
     if (!rc && !ctx->last6.blob.empty()) {
-      rc = upload_image(ctx->last6, D.device, us, &ne[k].v6);
+      rc = upload_image(ctx->last6, D.device, us, &ne[k].v6, &ctx->fail_uploads);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
       const Journal& j6 = ctx->journal6;
       if (!rc && j6.active()) {
@@ -1181,9 +1209,10 @@ int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n
   const auto d = launch_lock(ctx->data, ctx->publishers);
   DevState& D = ctx->dev[slot];
   if (!D.cur.base) return -GPC_EINVAL;  // nothing committed yet
-  EpochArgs ep{D.cur.base->d_hdr, D.cur.base->d_blob, D.cur.jhdr ? D.cur.pool->d_blob : nullptr, D.cur.jhdr,
+  const bool jpool = D.cur.jhdr && D.cur.jmode != kModeBase;
+  EpochArgs ep{D.cur.base->d_hdr, D.cur.base->d_blob, jpool ? D.cur.pool->d_blob : nullptr, D.cur.jhdr,
                D.cur.svc ? D.cur.svc->d_blob : nullptr, 0u, {D.cur.base->sort_table[0], D.cur.base->sort_table[1]},
-               uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1};
+               uint32_t(D.counter_cap * kCounterWords), D.counter_copies - 1, uint32_t(D.cur.jmode)};
   hipStream_t st = (hipStream_t)stream;
   // packet grouping (classify.hip group_*): one scratch buffer per stream, reused stream-ordered by
   // the next batch on that stream (launches of one stream run in order), so callers on different
@@ -1194,7 +1223,7 @@ int gpc_classify_on(gpc_ctx* ctx, uint32_t slot, const gpc_pkt_soa* pk, size_t n
   // egress and the ingress launch (classify.hip launch); without it (no memory) one launch does both
   const size_t park_bytes = D.cur.svc && n && ctx->svc_split ? (16 * n + 255) & ~size_t(255) : 0;
   uint8_t* scratch = nullptr;
-  if (group_batch(ctx, n, *D.cur.base, D.cur.jhdr != 0)) {
+  if (group_batch(ctx, n, *D.cur.base, jpool && D.cur.jmode == kModeJournal)) {
     if (const int e = group_scratch_for(ctx, D, st, park_bytes + group_scratch_bytes(*pk, n, ga.lb), &scratch)) return e;
     if (scratch) ga.scratch = scratch + park_bytes;
   }
@@ -1486,6 +1515,8 @@ int gpc_get_image_stats(gpc_ctx* ctx, gpc_image_stats* out) {
   out->v6_delta_builds = ctx->n_delta6;
   out->v6_overlay_rules = ctx->journal6.n_live;
   out->v6_prefixes = ctx->last6.v6_prefixes;
+  out->n_ext_rules = ctx->journal.n_ext_rules();
+  out->n_ext_values = ctx->journal.n_ext_values();
   if (cur.base) {
     out->group_key = group_key(ctx);
     out->lane_sort = cur.base->sort_table[0] | uint32_t(cur.base->sort_table[1]) << 8;
@@ -1696,8 +1727,10 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   // in flight the journal takes up to every rule of the base instead: a synchronous rebuild here
   // would stall the control thread for a whole image build (C5 at 10 000 ops/s: commit p99 3.5 s,
   // 6 blocking rebuilds in 70 s) and discard the compaction it overtakes.
-  const size_t live_cap = ctx->comp_pending ? std::max(kDeltaMinRules, ctx->last.conj_rid.size())
-                                            : std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction);
+  // The allowance is a bounded multiple of the normal cap (a slow or failing compaction
+  // must not leave the data path walking a base-sized journal).
+  const size_t normal_cap = std::max(kDeltaMinRules, ctx->last.conj_rid.size() / kDeltaFraction);
+  const size_t live_cap = ctx->comp_pending ? kPendingCapFactor * normal_cap : normal_cap;
   bool full = force_full || !have_base || classifier_changed || ctx->last.any_noact || ctx->np.foreign() || ctx->journal.any_noact ||
               ctx->journal.n_live > live_cap || ctx->journal.pool.size() > kPoolWords * 7 / 8;
   int rc = GPC_OK;
@@ -1727,7 +1760,11 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   // ask the compactor for a new base once the journal is large; commits continue meanwhile
   const int32_t ca = ctx->cfg.compact_after;
   const size_t soft = ca > 0 ? size_t(ca) : std::max<size_t>(2048, ctx->last.conj_rid.size() / 32);
-  if (!full && ca >= 0 && !ctx->comp_pending && ctx->journal.n_live > soft) {
+  // (or once many point extensions are live, or the pool is a quarter full: epochs that only move
+  // extensions append an index each, and the compactor folds them into a new base)
+  if (!full && ca >= 0 && !ctx->comp_pending &&
+      (ctx->journal.n_live + ctx->journal.n_ext_rules() > soft || ctx->journal.n_ext_values() > kExtCompactValues ||
+       ctx->journal.pool.size() > kPoolWords / 4)) {
     {
       std::lock_guard<std::mutex> c(ctx->comp.mu);
       if (ctx->comp.enabled && !ctx->comp.busy && !ctx->comp.ready) {
@@ -1828,7 +1865,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       ne[k].base = std::move(bg_base[k]);
       ne[k].pool = std::move(bg_pool[k]);
     } else if (full || installed || resync4 || !D.cur.base) {
-      if ((rc = upload_image(ctx->last, D.device, us, &ne[k].base))) return fail(rc);
+      if ((rc = upload_image(ctx->last, D.device, us, &ne[k].base, &ctx->fail_uploads))) return fail(rc);
     } else {
       ne[k].base = D.cur.base;
       ne[k].pool = D.cur.pool;
@@ -1897,8 +1934,9 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (tail && hip_ok(hipMemcpyAsync(ne[k].pool->d_blob + jn.uploaded, ctx->stage, copy_bytes, hipMemcpyHostToDevice, us)))
       return fail(-GPC_EDEV);
     ne[k].jhdr = jhdr;
+    ne[k].jmode = jhdr ? jn.mode() : kModeBase;
     if (resync6) {  // the current host IPv6 base, then the whole journal into a fresh pool
-      if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
+      if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6, &ctx->fail_uploads))) return fail(rc);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
       if (j6_active) {
         if ((rc = alloc_pool(D.device, us, &ne[k].v6_pool))) return fail(rc);
@@ -1923,7 +1961,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
         ne[k].v6_jhdr = j6_active ? ctx->journal6.hdr_off : 0u;
       }
     } else if (!ctx->last6.blob.empty()) {
-      if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6))) return fail(rc);
+      if ((rc = upload_image(ctx->last6, D.device, us, &ne[k].v6, &ctx->fail_uploads))) return fail(rc);
       ne[k].v6_lpm = ctx->last6.hdr.v6_lpm;
       ne[k].v6_gen = ctx->gen6;
     }

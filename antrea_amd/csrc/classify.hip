@@ -298,7 +298,7 @@ __device__ __forceinline__ uint64_t logical_block(uint32_t mode) {
 // here as code columns (v6_code_kernel) against the IPv6 image.
 // Packet i of the batch through the Service stage (kSvc) and the policy stage(s) of the launch;
 // pkt_lane / pkt_stride: this lane's column of the block's [word][lane] packet table in LDS.
-template <bool kDelta, bool kSvc, int kStage>
+template <int kDelta, bool kSvc, int kStage>
 __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t i, uint4* __restrict__ out,
                                              uint4* __restrict__ lb_out, unsigned long long* __restrict__ counters, int count,
                                              const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
@@ -381,11 +381,14 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
       return;
     }
   }
-  View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
-  if (kDelta) {
+  View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr, 0u};
+  if (kDelta != kModeBase) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
-    if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
-    im.n_img = 2u;
+    im.ext = jh->ext_off;
+    if (kDelta == kModeJournal) {
+      if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
+      im.n_img = 2u;
+    }
   }
   Pkt p(pkt_lane, pkt_stride);
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
@@ -430,8 +433,9 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   else out[i] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
 }
 
-template <bool kDelta, bool kSvc, int kStage, bool kSort = false>
-__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta ? GPC_DELTA_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
+// kDelta: the epoch mode (core.hpp kModeBase / kModeExt / kModeJournal).
+template <int kDelta, bool kSvc, int kStage, bool kSort = false>
+__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta == kModeJournal ? GPC_DELTA_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
     uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
@@ -550,7 +554,7 @@ static void launch_unpermute(const void* mid, uint32_t mid_words, const uint2* g
                      reinterpret_cast<const uint32_t*>(mid), mid_words, gout, orig, n, out, lbg, lb_out);
 }
 
-template <bool kDelta, bool kSvc>
+template <int kDelta, bool kSvc>
 static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_verdict* out, uint4* lb_out,
                    unsigned long long* counters, int count, const uint32_t* orig, uint2* mid, uint32_t xo, uint2* gout,
                    uint4* park, hipStream_t stream, LaunchMarks* marks) {
@@ -611,17 +615,18 @@ __global__ void trace_kernel(EpochArgs ep, gpc_pkt_soa pk, uint4* __restrict__ o
     }
   }
   lb_out[0] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
-  View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr};
+  View im{{ep.blob, ep.hdr, nullptr, ep.pool}, {ep.pool, nullptr, nullptr, ep.pool}, 1u, ep.jhdr, 0u};
   if (ep.pool) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(ep.pool + ep.jhdr);
     if (jh->bdead_off) im.base.dead = ep.pool + jh->bdead_off;
     im.n_img = 2u;
+    im.ext = jh->ext_off;
   }
   Pkt p(pkt_lds, 1);
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[0] : 0u, svc_group,
            pk.tun_id ? pk.tun_id[0] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
            view_bloom_axes(im));
-  const PacketOut o = classify_packet<true, 0, true>(im, p, dest, ct_mark, steps, n_steps);
+  const PacketOut o = classify_packet<kModeJournal, 0, true>(im, p, dest, ct_mark, steps, n_steps);
   out[0] = make_uint4(o.e.conj, o.e.packed, o.g.conj, o.g.packed);
 }
 
@@ -770,15 +775,19 @@ int launch_classify(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_
   }
   EpochArgs e = ep;
   if (group && group->key == GPC_GROUP_KEY_SCAN) e.sort_table[0] = e.sort_table[1] = 0;  // lanes already grouped by scan length
-  const bool delta = ep.pool != nullptr, svc = ep.svc != nullptr;
+  // epoch mode: a journal (records / tombstones) or only point extensions over the base
+  const int mode = !ep.pool ? kModeBase : ep.mode == uint32_t(kModeExt) ? kModeExt : kModeJournal;
+  const bool svc = ep.svc != nullptr;
   // with Services one launch does both stages; grouped, it stores both verdict halves (and the LB
   // results) in grouped order for the un-permute, like the two launches without Services
   if (svc && lb_out && gout && !lbg) return -GPC_EINVAL;  // the caller sized the scratch without lb
   uint4* const lbk = lbg ? lbg : lb_out;
-  if (delta && svc) launch<true, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
-  else if (delta) launch<true, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
-  else if (svc) launch<false, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
-  else launch<false, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
+  if (mode == kModeJournal && svc) launch<kModeJournal, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
+  else if (mode == kModeJournal) launch<kModeJournal, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
+  else if (mode == kModeExt && svc) launch<kModeExt, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
+  else if (mode == kModeExt) launch<kModeExt, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
+  else if (svc) launch<kModeBase, true>(e, *p, n, out, lbk, counters, count, orig, mid, xo, gout, park, stream, marks);
+  else launch<kModeBase, false>(e, *p, n, out, lb_out, counters, count, orig, mid, xo, gout, nullptr, stream, marks);
   if (gout) launch_unpermute(mid, 2, gout, orig, n, reinterpret_cast<uint4*>(out), svc ? lbg : nullptr, lb_out, stream, marks);
   launch_mark(marks, kLaunchEnd, stream);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;

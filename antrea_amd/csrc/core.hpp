@@ -706,7 +706,12 @@ struct View {
   Img base, ovl;
   uint32_t n_img;  // 1 or 2
   uint32_t jhdr;
+  uint32_t ext;    // ExtHdr word offset in the pool (ovl.blob), 0: no point extensions
 };
+
+// Epoch modes (kernel instantiations): the base image alone; the base plus point extensions (no
+// journal walk, no tombstones); the base with tombstones, the journal and point extensions.
+constexpr int kModeBase = 0, kModeExt = 1, kModeJournal = 2;
 
 // ------------------------------------------------------------------------------ journal
 // Append-only delta store (journal.cpp). Every commit appends, never rewrites, so launches of
@@ -735,8 +740,11 @@ struct JournalHdr {
   // IPv6 journals: LPM entries of the prefixes interned since the base (image.cpp extend_image6),
   // a hash laid out like V6Lpm's (2^v6_ovf_log2 buckets) probed next to the base's; 0: none
   uint32_t v6_ovf_off, v6_ovf_log2;
+  uint32_t ext_off;        // ExtHdr of this epoch's point extensions (0: none)
+  uint32_t jflags;         // kJUsed: the journal holds records, tombstones or hard rules (else only extensions)
   JournalTable t[6];
 };
+constexpr uint32_t kJUsed = 1u;
 constexpr uint32_t kJEntWords = 8;
 constexpr uint32_t kJOridShift = 12, kJMetaMask = (1u << kJOridShift) - 1u;  // meta: 12 bits, orid: 20
 constexpr uint32_t kJPageHeads = 64;
@@ -1571,12 +1579,129 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
   return res;
 }
 
-// kJournal = false: the base image alone (the journal code is not instantiated).
-template <bool kJournal>
+// ------------------------------------------------------------------------------ point extensions
+// A rule whose current version differs from its base record only by exact values added to ONE
+// clause (AddPolicyRuleAddress of Pod IPs / ofports / single ports, network_policy.go:1661) keeps
+// its base record live: no tombstone, no journal copy (image.cpp Journal::apply). Each added value
+// is an entry (table, axis, value) -> (base record, clause). Why that is exact: a packet the new
+// version matches either matches the base version -- the base driver lists and verifies it as
+// before, and a base match implies a match of the superset -- or fails some base clause and then
+// holds an added value on the extended clause's axis, where the probe finds the rule and verifies
+// its other clauses from the base record (the extended clause is decided by the probe). The index
+// is small (live added values) and emitted whole per epoch: a presence bitmap (one L2-resident
+// load settles almost every packet), bucket offsets, 16-B entries {value, table | axis << 3 |
+// clause << 7, record offset, priority}.
+struct ExtHdr {
+  uint32_t n;                   // entries
+  uint32_t pres_off, pres_log2;  // presence bitmap: 2^pres_log2 bits
+  uint32_t bkt_off, bkt_log2;    // 2^bkt_log2 + 1 bucket offsets (entry index)
+  uint32_t ent_off;              // entries, kExtEntWords words each, bucket-sorted
+  uint32_t axes[6];              // per table: bit a = some entry of the table is on axis a
+};
+constexpr uint32_t kExtEntWords = 4;
+GPC_HD uint32_t ext_meta(uint32_t table, uint32_t axis, uint32_t clause) { return table | (axis << 3) | (clause << 7); }
+GPC_HD uint32_t ext_hash(uint32_t table, uint32_t axis, uint32_t v) {
+  return mix32(v ^ mix32(((table << 4) | axis) * 0x9e3779b1u + 0x632be5abu));
+}
+
+// Best completion among the extended rules the packet's values reach in this table (hard rules are
+// never extended): priority desc, conj id asc, and whether two rules completed at that level.
+GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p) {
+  TablePart res;
+  res.h = res.s = res.win = 0;
+  const uint32_t* pool = v.ovl.blob;
+  const ExtHdr* eh = reinterpret_cast<const ExtHdr*>(pool + v.ext);
+  uint32_t axes = eh->axes[table - 1];
+  uint32_t best = 0, best_prio = 0, best_conj = 0, at_best = 0;
+  while (axes) {
+    const uint32_t a = uint32_t(__builtin_ctz(axes));
+    axes &= axes - 1u;
+    const uint32_t val = p.ax[a], h = ext_hash(table, a, val);
+    const uint32_t pb = h >> (32u - eh->pres_log2);
+    GPC_TOUCH(pool + eh->pres_off + (pb >> 5), 4);
+    if (!((pool[eh->pres_off + (pb >> 5)] >> (pb & 31u)) & 1u)) continue;
+    uint32_t e, end;
+    GPC_TOUCH(pool + eh->bkt_off + (h & ((1u << eh->bkt_log2) - 1u)), 8);
+    load_pair(pool + eh->bkt_off + (h & ((1u << eh->bkt_log2) - 1u)), &e, &end);
+    const uint32_t meta = table | (a << 3);
+    for (; e < end; e++) {
+      const uint32_t* en = pool + eh->ent_off + e * kExtEntWords;
+      GPC_TOUCH(en, 16);
+      uint32_t ew[kExtEntWords];
+#if defined(__HIPCC__)
+      const uint4 q = *reinterpret_cast<const uint4*>(en);
+      ew[0] = q.x, ew[1] = q.y, ew[2] = q.z, ew[3] = q.w;
+#else
+      for (uint32_t w = 0; w < kExtEntWords; w++) ew[w] = en[w];
+#endif
+      if (ew[0] != val || (ew[1] & 0x7fu) != meta) continue;
+      const uint32_t prio = ew[3];
+      if (best && prio < best_prio) continue;  // cannot change the decision
+      const uint32_t* rec = v.base.blob + ew[2];
+      GPC_TOUCH(rec, 4 * kRecLine);
+      const RecLine hd = load_rec_line(rec);
+      const uint32_t conj = hd.w[0];
+      if (!rule_match(v.base, rec, hd.w[2], &hd.w[kRecFcd], 1u << (ew[1] >> 7), p)) continue;
+      if (!best || prio > best_prio) {
+        best = ew[2];
+        best_prio = prio;
+        best_conj = conj;
+        at_best = 1;
+      } else if (conj != best_conj) {
+        at_best++;
+        if (conj < best_conj) {
+          best = ew[2];
+          best_conj = conj;
+        }
+      }
+    }
+  }
+  if (best) {
+    res.s = best_prio | kSHave | (at_best > 1 ? kSTie : 0u);
+    res.win = best;
+  }
+  return res;
+}
+
+// a (base, or base + journal) and e (extended rules; records in the base) for one table. The hard
+// match is a's; e counts only above it. One rule reached both ways is one completion, not a tie.
+GPC_HD TablePart merge_ext(const View& v, const TablePart& a, const TablePart& e) {
+  if (!(e.s & kSHave)) return a;
+  const bool hf = (a.h & kHFound) != 0;
+  const uint32_t hp = a.h & 0xffffu, al = a.s & 0xffffu, el = e.s & 0xffffu;
+  const bool va = (a.s & kSHave) != 0;
+  if (hf && el <= hp) return a;
+  TablePart r;
+  r.h = a.h;
+  if (va && al == el) {
+    if (!(a.s & (kSImg | kSNoAct)) && a.win == e.win) {
+      r.s = a.s | (e.s & kSTie);
+      r.win = a.win;
+      return r;
+    }
+    const uint32_t ca = (a.s & kSNoAct) ? 0xffffffffu : ((a.s & kSImg) ? v.ovl.blob : v.base.blob)[a.win];
+    const uint32_t ce = v.base.blob[e.win];
+    const bool pe = ce < ca;
+    r.s = (pe ? e.s : a.s) | kSTie;
+    r.win = pe ? e.win : a.win;
+    return r;
+  }
+  if (!va || el > al) {
+    r.s = e.s;
+    r.win = e.win;
+    return r;
+  }
+  return a;
+}
+
+// kMode (kModeBase / kModeExt / kModeJournal): what of the epoch the table walk reads; the base
+// instantiation compiles neither the journal nor the extension code.
+template <int kMode>
 GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
   TablePart acc = eval_part(v.base, table, p);
-  if (kJournal && v.n_img > 1) acc = combine_parts(v, acc, eval_journal(v, table, p));
-  return finish_part(v.base.blob, kJournal ? v.ovl.blob : nullptr, acc);
+  if (kMode >= kModeJournal && v.n_img > 1) acc = combine_parts(v, acc, eval_journal(v, table, p));
+  if (kMode >= kModeExt && v.ext) acc = merge_ext(v, acc, eval_ext(v, table, p));
+  return finish_part(v.base.blob, kMode >= kModeJournal ? v.ovl.blob : nullptr, acc);
 }
 
 // ------------------------------------------------------------------------------ Service image
@@ -1715,13 +1840,14 @@ struct StageOut {
   uint32_t slot;
   int counted;
 };
-template <bool kJournal, bool kTrace>
+template <int kMode, bool kTrace>
 GPC_HD StageOut walk_stage(const View& im, const Pkt& p, uint32_t t0, TraceStep* trace, uint32_t* n_trace) {
   uint32_t conj = 0, ft = 0;  // ft = flags | tier << 8 (reg5/reg6 after a Pass keep its conj id and tier)
   for (uint32_t i = 0;; i++) {
     const uint32_t t = t0 + i;
-    // a table without rules (base-only epochs): a miss, without reading its header
-    if (!kJournal && !kTrace && !((im.base.hdr->live >> (t - 1)) & 1u)) {
+    // a table without rules (epochs without a journal: extended rules are base rules): a miss,
+    // without reading its header
+    if (kMode < kModeJournal && !kTrace && !((im.base.hdr->live >> (t - 1)) & 1u)) {
       if (i < 2) continue;
       StageOut o;
       o.slot = 0;
@@ -1730,7 +1856,7 @@ GPC_HD StageOut walk_stage(const View& im, const Pkt& p, uint32_t t0, TraceStep*
       o.v.packed = pack_verdict(1 /*NO_MATCH*/, 0, ft >> 8, ft & 0xffu);
       return o;
     }
-    const TableResult r = eval_table<kJournal>(im, t, p);
+    const TableResult r = eval_table<kMode>(im, t, p);
     GPC_MARK(ST_WALK);
     if (kTrace && *n_trace < kMaxTraceSteps) {
       TraceStep& st = trace[(*n_trace)++];
@@ -1771,7 +1897,7 @@ GPC_HD StageOut walk_stage(const View& im, const Pkt& p, uint32_t t0, TraceStep*
 // kStage: 0 = both stages; 1 = egress only; 2 = ingress only (the caller has checked that the
 // egress verdict lets the packet reach the ingress tables). kStage 0 runs walk_stage in a loop over
 // the two stages so the table evaluation is instantiated once.
-template <bool kJournal = true, int kStage = 0, bool kTrace = false>
+template <int kMode = kModeJournal, int kStage = 0, bool kTrace = false>
 GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, uint32_t ct_mark,
                                  TraceStep* trace = nullptr, uint32_t* n_trace = nullptr) {
   PacketOut o;
@@ -1780,7 +1906,7 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, ui
   o.eslot = o.gslot = 0;
   o.ecounted = o.gcounted = 0;
   if (kStage == 1 || kStage == 2) {
-    const StageOut s = walk_stage<kJournal, kTrace>(im, p, kStage == 1 ? 1u : 4u, trace, n_trace);
+    const StageOut s = walk_stage<kMode, kTrace>(im, p, kStage == 1 ? 1u : 4u, trace, n_trace);
     if (kStage == 1) {
       o.e = s.v;
       o.eslot = s.slot;
@@ -1794,7 +1920,7 @@ GPC_HD PacketOut classify_packet(const View& im, const Pkt& p, uint32_t dest, ui
   }
 #pragma nounroll
   for (uint32_t stage = 0; stage < 2; stage++) {
-    const StageOut s = walk_stage<kJournal, kTrace>(im, p, stage ? 4u : 1u, trace, n_trace);
+    const StageOut s = walk_stage<kMode, kTrace>(im, p, stage ? 4u : 1u, trace, n_trace);
     if (stage) {
       o.g = s.v;
       o.gslot = s.slot;

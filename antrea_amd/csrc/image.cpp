@@ -85,6 +85,27 @@ struct RuleB {
   bool pin = false;  // the action flow sends the packet to the controller (DNS interception)
 };
 
+// Point extensions (core.hpp ExtHdr, Journal::apply): an atom's identity and a rule's record
+// fields other than its atoms, as 64-bit hashes.
+uint64_t atom_hash(const Atom& a) {
+  uint64_t h = 0x9ae16a3b2f90404full ^ a.t.size();
+  for (const Term& t : a.t) h = mix64(mix64(h ^ ((uint64_t(t.val) << 32) | t.mask)) ^ t.axis);
+  return h;
+}
+uint64_t rule_sig(const RuleB& r, bool counted, uint32_t slot) {
+  uint64_t h = mix64(uint64_t(r.prio) | uint64_t(r.act_prio) << 16 | uint64_t(r.verdict) << 32 | uint64_t(r.n) << 40 |
+                     uint64_t(r.tier) << 48);
+  return mix64(h ^ (uint64_t(r.has_act) | uint64_t(r.pin) << 1 | uint64_t(counted) << 2 | uint64_t(slot) << 8));
+}
+std::vector<uint64_t> clause_hashes(const std::vector<Atom>& atoms) {
+  std::vector<uint64_t> v;
+  v.reserve(atoms.size());
+  for (const Atom& a : atoms) v.push_back(atom_hash(a));
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  return v;
+}
+
 inline uint32_t prefix_mask(int plen) { return plen <= 0 ? 0u : plen >= 32 ? 0xffffffffu : ~((1u << (32 - plen)) - 1); }
 inline bool is_prefix(uint32_t m) { return ((~m) & ((~m) + 1u)) == 0; }
 inline int leading_ones(uint32_t m) {
@@ -1731,6 +1752,10 @@ void Journal::reset(const HostImage* base, uint32_t lg) {
   ovf_table_.clear();
   ovf_off_ = ovf_log2_ = 0;
   ovf_dirty_ = false;
+  ext_.clear();
+  ext_values_ = ext_off_ = 0;
+  journaled_ = false;
+  pt_off_ = bdead_pt_off_ = odead_pt_off_ = 0;
 }
 
 uint32_t Journal::n_tombstones() const {
@@ -1747,27 +1772,51 @@ uint32_t Journal::append(const uint32_t* w, size_t n, size_t align) {
   return off;
 }
 
+// Point extensions per rule (core.hpp ExtHdr): at most kExtMaxRuleValues added values per rule and
+// kExtMaxValues in all (past them a rule takes the journal; the compactor folds them into a base).
+constexpr size_t kExtMaxRuleValues = 256, kExtMaxValues = size_t(1) << 20;
+
+// The index of every live point extension, appended to the pool (published whole per epoch: it is
+// small, and nothing published is rewritten). Returns its ExtHdr offset (0: no extensions).
+uint32_t Journal::emit_ext() {
+  if (ext_.empty()) return 0;
+  struct E {
+    uint32_t bkt, w[kExtEntWords];
+  };
+  std::vector<E> es;
+  es.reserve(ext_values_);
+  ExtHdr h{};
+  h.n = ext_values_;
+  h.pres_log2 = 12;
+  while (h.pres_log2 < 24 && (uint64_t(1) << h.pres_log2) < uint64_t(ext_values_) * 32) h.pres_log2++;
+  h.bkt_log2 = 6;
+  while (h.bkt_log2 < 22 && (uint64_t(1) << h.bkt_log2) < uint64_t(ext_values_)) h.bkt_log2++;
+  std::vector<uint32_t> pres(size_t(1) << (h.pres_log2 - 5), 0u), offs((size_t(1) << h.bkt_log2) + 1, 0u);
+  for (auto& kv : ext_) {
+    const ExtRule& e = kv.second;
+    for (auto& av : e.values) {
+      const uint32_t hs = ext_hash(e.table, av.first, av.second);
+      const uint32_t pb = hs >> (32u - h.pres_log2);
+      pres[pb >> 5] |= 1u << (pb & 31u);
+      es.push_back({hs & ((1u << h.bkt_log2) - 1u), {av.second, ext_meta(e.table, av.first, e.clause), e.rec_off, e.prio}});
+      h.axes[e.table - 1] |= 1u << av.first;
+    }
+  }
+  std::stable_sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.bkt < b.bkt; });
+  for (const E& e : es) offs[e.bkt + 1]++;
+  for (size_t b = 0; b + 1 < offs.size(); b++) offs[b + 1] += offs[b];
+  std::vector<uint32_t> ents;
+  ents.reserve(es.size() * kExtEntWords);
+  for (const E& e : es) ents.insert(ents.end(), e.w, e.w + kExtEntWords);
+  h.pres_off = append(pres.data(), pres.size(), 16);
+  h.bkt_off = append(offs.data(), offs.size(), 16);
+  h.ent_off = ents.empty() ? h.bkt_off : append(ents.data(), ents.size(), 16);
+  return append(reinterpret_cast<const uint32_t*>(&h), sizeof h / 4, 16);
+}
+
 int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables,
                    std::string* err, bool alloc) {
-  // 1. tombstones: every earlier copy of a changed rule (base or journal)
-  for (uint32_t c : conj) {
-    auto it = live_.find(c);
-    if (it != live_.end()) {
-      set_bit(odead_, it->second, &odirty_);
-      live_.erase(it);
-      n_live--;
-    }
-    auto b = base_->conj_rid.find(c);
-    if (b != base_->conj_rid.end()) set_bit(bdead_, b->second, &bdirty_);
-  }
-  for (int t = 0; t < 6; t++) {
-    if (!((hard_tables >> t) & 1u)) continue;
-    for (uint32_t o : hard_orids_[t]) set_bit(odead_, o, &odirty_);
-    hard_orids_[t].clear();
-    hard_offs_[t].clear();
-    for (uint32_t rid : base_->hard_rids[t]) set_bit(bdead_, rid, &bdirty_);
-  }
-  // 2. current versions
+  // 0. current versions of the changed rules
   Gather G;
   G.fam = fam_;
   G.codes = fam_ == 6 ? base_->codes6.get() : nullptr;
@@ -1780,6 +1829,125 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     *err = G.error;
     return rc;
   }
+  // 1. point extensions: a rule whose new version is its base record plus exact values on one
+  // clause keeps the base record (core.hpp ExtHdr); a rule back at its base version drops its
+  // extension. Every other changed rule takes the journal (jconj).
+  const bool ext_off = std::getenv("GPC_NO_EXTENSIONS") != nullptr;  // (experiments, A/B tests)
+  bool ext_changed = false;
+  std::set<uint32_t> jconj;
+  auto extend = [&](uint32_t c) {
+    if (fam_ != 4 || ext_off || live_.count(c)) return false;
+    auto b = base_->base_rules.find(c);
+    if (b == base_->base_rules.end()) return false;
+    auto rid = base_->conj_rid.find(c);  // a tombstoned base record (an earlier uninstall) stays dead
+    if (rid == base_->conj_rid.end() ||
+        (rid->second / 32 < bdead_.size() && ((bdead_[rid->second / 32] >> (rid->second % 32)) & 1u)))
+      return false;
+    const BaseRule& br = b->second;
+    auto it = G.soft[br.table].find(c);
+    if (it == G.soft[br.table].end()) return false;
+    for (int t = 1; t <= 6; t++)
+      if (t != int(br.table) && G.soft[t].count(c)) return false;
+    RuleB& r = it->second;
+    if (!r.prio_set || !r.has_act) return false;
+    for (int k = 0; k < r.n; k++)
+      if (r.clause[k].empty()) return false;
+    auto pit = np.policies().find(c);
+    r.tier = pit != np.policies().end() ? uint8_t(std::max(0, std::min(255, pit->second->tier))) : 0;
+    const bool is_deny = r.verdict == RV_DROP || r.verdict == RV_REJECT;
+    r.counted = r.has_act && ((r.verdict == RV_ALLOW && G.counted_allow.count(c)) || (is_deny && G.counted_deny.count(c)));
+    uint32_t slot = 0;
+    const bool counted = r.counted && slots.lookup(c, alloc, &slot);
+    if (rule_sig(r, counted, slot) != br.sig) return false;
+    ExtRule e;
+    e.table = br.table;
+    e.rec_off = br.rec_off;
+    e.prio = r.prio;
+    int kx = -1;
+    for (int k = 0; k < r.n; k++) {
+      std::vector<std::pair<uint64_t, const Atom*>> now;
+      now.reserve(r.clause[k].size());
+      for (const Atom& a : r.clause[k]) now.push_back({atom_hash(a), &a});
+      std::sort(now.begin(), now.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      const std::vector<uint64_t>& was = br.atoms[k];
+      size_t j = 0;
+      for (size_t i = 0; i < now.size(); i++) {
+        if (i && now[i].first == now[i - 1].first) continue;
+        while (j < was.size() && was[j] < now[i].first) return false;  // a base atom is gone
+        if (j < was.size() && was[j] == now[i].first) {
+          j++;
+          continue;
+        }
+        const Atom& a = *now[i].second;  // added: must be one exact value on one axis
+        if (a.t.size() != 1 || a.t[0].mask != 0xffffffffu || a.t[0].axis >= AX_N || (kx >= 0 && kx != k)) return false;
+        kx = k;
+        e.values.push_back({a.t[0].axis, a.t[0].val});
+      }
+      if (j != was.size()) return false;
+    }
+    std::sort(e.values.begin(), e.values.end());
+    auto old = ext_.find(c);
+    const size_t had = old == ext_.end() ? 0 : old->second.values.size();
+    if (kx < 0) {  // the base version again
+      if (old != ext_.end()) {
+        ext_values_ -= uint32_t(had);
+        ext_.erase(old);
+        ext_changed = true;
+      }
+      return true;
+    }
+    e.clause = uint32_t(kx);
+    if (e.values.size() > kExtMaxRuleValues || ext_values_ - had + e.values.size() > kExtMaxValues) return false;
+    if (old != ext_.end() && old->second == e) return true;
+    ext_values_ = uint32_t(ext_values_ - had + e.values.size());
+    ext_[c] = std::move(e);
+    ext_changed = true;
+    return true;
+  };
+  for (uint32_t c : conj) {
+    if (extend(c)) continue;
+    jconj.insert(c);
+    auto old = ext_.find(c);
+    if (old != ext_.end()) {
+      ext_values_ -= uint32_t(old->second.values.size());
+      ext_.erase(old);
+      ext_changed = true;
+    }
+  }
+  if (hard_tables) journaled_ = true;  // (rules: once a tombstone or a record is written, below)
+  if (std::getenv("GPC_IMAGE_DEBUG") && (!jconj.empty() || hard_tables)) {
+    std::fprintf(stderr, "journal: %zu rules, hard tables 0x%x:", jconj.size(), unsigned(hard_tables));
+    for (uint32_t c : jconj) {
+      int in_t = 0;
+      for (int t = 1; t <= 6; t++)
+        if (G.soft[t].count(c)) in_t = t;
+      std::fprintf(stderr, " %u(table %d, base %d)", c, in_t, int(base_->base_rules.count(c)));
+    }
+    std::fprintf(stderr, "\n");
+  }
+  // 2. tombstones: every earlier copy of a rule that takes the journal (base or journal)
+  for (uint32_t c : jconj) {
+    auto it = live_.find(c);
+    if (it != live_.end()) {
+      set_bit(odead_, it->second, &odirty_);
+      live_.erase(it);
+      n_live--;
+      journaled_ = true;
+    }
+    auto b = base_->conj_rid.find(c);
+    if (b != base_->conj_rid.end()) {
+      set_bit(bdead_, b->second, &bdirty_);
+      journaled_ = true;
+    }
+  }
+  for (int t = 0; t < 6; t++) {
+    if (!((hard_tables >> t) & 1u)) continue;
+    for (uint32_t o : hard_orids_[t]) set_bit(odead_, o, &odirty_);
+    hard_orids_[t].clear();
+    hard_offs_[t].clear();
+    for (uint32_t rid : base_->hard_rids[t]) set_bit(bdead_, rid, &bdirty_);
+  }
+  // 3. current versions of the journal's rules
   uint64_t span[AX_N];  // interval prefilter choice: price hulls against the whole axis
   for (int a = 0; a < AX_N; a++) span[a] = 1ull << 32;
   std::set<uint32_t> dirty_pages;
@@ -1788,7 +1956,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     std::vector<RuleB*> rs;
     for (auto& kv : G.soft[t]) {
       RuleB& r = kv.second;
-      if (!r.prio_set) continue;
+      if (!r.prio_set || !jconj.count(r.conj_id)) continue;
       bool complete = true;
       for (int k = 0; k < r.n; k++) complete &= !r.clause[k].empty();
       if (!complete) continue;
@@ -1820,6 +1988,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
         return -GPC_ENOMEM;
       }
       const uint32_t orid = n_versions++;
+      journaled_ = true;
       // record: header, clauses, then this record's out-of-line segment data
       std::vector<uint32_t> rec(kRecLine, 0u), ext;
       std::vector<std::pair<uint32_t, uint32_t>> patches;  // (record word, ext offset)
@@ -1938,21 +2107,30 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       }
     }
   }
-  // 3. copy-on-write head pages, then this epoch's page table, bitmaps and header
+  // 4. copy-on-write head pages, then this epoch's page table (the previous one when no head page
+  // changed: an epoch that only moves point extensions appends no 64-KB page table), bitmaps, the
+  // extension index and the header
   for (uint32_t pg : dirty_pages) pt_[pg] = append(&heads_[size_t(pg) * kJPageHeads], kJPageHeads, kJPageHeads);
   JournalHdr h{};
   h.lg = lg_;
-  h.pt_off = append(pt_.data(), pt_.size(), 16);
+  if (!dirty_pages.empty() || !pt_off_) pt_off_ = append(pt_.data(), pt_.size(), 16);
+  h.pt_off = pt_off_;
   // tombstone bitmaps: changed 8192-bit pages copied on write, then this epoch's page tables
-  auto publish = [&](std::vector<uint32_t>& bm, std::vector<uint32_t>& pt, std::set<uint32_t>& dirty, uint32_t n_ids) {
+  auto publish = [&](std::vector<uint32_t>& bm, std::vector<uint32_t>& pt, std::set<uint32_t>& dirty, uint32_t n_ids,
+                     uint32_t* last) {
     if (bm.empty()) return 0u;
     const size_t n_pages = size_t(n_ids >> kDeadPageShift) + 1;
+    if (dirty.empty() && *last && pt.size() >= n_pages) return *last;
     if (pt.size() < n_pages) pt.resize(n_pages, 0u);
     bm.resize(std::max(bm.size(), n_pages * kDeadPageWords), 0u);
     for (uint32_t pg : dirty) pt[pg] = append(&bm[size_t(pg) * kDeadPageWords], kDeadPageWords, kDeadPageWords);
     dirty.clear();
-    return append(pt.data(), pt.size(), 16);
+    *last = append(pt.data(), pt.size(), 16);
+    return *last;
   };
+  if (ext_changed) ext_off_ = emit_ext();
+  h.ext_off = ext_off_;
+  h.jflags = journaled_ ? kJUsed : 0u;
   h.bloom_axes = bloom_axes_;
   if (ovf_dirty_) {
     ovf_off_ = append(ovf_table_.data(), ovf_table_.size(), 16);
@@ -1960,8 +2138,8 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
   }
   h.v6_ovf_off = ovf_off_;
   h.v6_ovf_log2 = ovf_log2_;
-  h.bdead_off = publish(bdead_, bpt_, bdirty_, base_->n_rids);
-  h.odead_off = publish(odead_, opt_, odirty_, n_versions);
+  h.bdead_off = publish(bdead_, bpt_, bdirty_, base_->n_rids, &bdead_pt_off_);
+  h.odead_off = publish(odead_, opt_, odirty_, n_versions, &odead_pt_off_);
   for (int t = 0; t < 6; t++) {
     h.t[t] = tables_[t];
     if (!hard_offs_[t].empty()) {
@@ -2135,6 +2313,13 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
       } else {
         out->conj_rid[r.conj_id] = rid;
         if (!r.has_act) out->any_noact = true;
+        if (G.fam == 4) {  // what a later point extension of this rule is checked against
+          BaseRule& br = out->base_rules[r.conj_id];
+          br.table = uint32_t(t);
+          br.rec_off = base;
+          br.sig = rule_sig(r, counted, slot);
+          for (int k = 0; k < r.n; k++) br.atoms[k] = clause_hashes(r.clause[k]);
+        }
       }
     }
     B.align(16);

@@ -17,6 +17,14 @@ namespace gpc {
 
 class V6Codes;  // IPv6 prefix tree and codes (image.cpp)
 
+// A soft rule of a base image as point extensions need it (Journal::apply): where its record is,
+// a signature of everything but its match atoms, and per clause the sorted hashes of its atoms.
+struct BaseRule {
+  uint32_t table = 0, rec_off = 0;
+  uint64_t sig = 0;
+  std::vector<uint64_t> atoms[kMaxClauses];
+};
+
 struct HostImage {
   ImageHdr hdr{};
   std::vector<uint32_t> blob;        // hdr offsets index this (uint32 words)
@@ -34,6 +42,7 @@ struct HostImage {
   // IPv6 image: LPM entries of the prefixes delta commits interned ({masked address, len} -> code),
   // published through the IPv6 journal's overflow table (extend_image6)
   std::map<std::array<uint32_t, 5>, uint32_t> v6_ovf;
+  std::unordered_map<uint32_t, BaseRule> base_rules;  // IPv4 image: soft rules by conj id (point extensions)
 };
 
 // Stable counter slots per conjunction id (freed on uninstall, reused later; identical on every
@@ -95,6 +104,10 @@ class Journal {
   int apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>& conj, uint8_t hard_tables, std::string* err,
             bool alloc = true);
   bool active() const { return hdr_off != 0; }
+  // What the current epoch needs of the kernel (core.hpp kModeBase / kModeExt / kModeJournal).
+  int mode() const { return journaled_ ? kModeJournal : ext_off_ ? kModeExt : kModeBase; }
+  uint32_t n_ext_rules() const { return uint32_t(ext_.size()); }
+  uint32_t n_ext_values() const { return ext_values_; }
   uint32_t n_tombstones() const;
   std::vector<uint32_t> pool;  // host mirror of the device pool
   size_t uploaded = 0;         // words already on the device
@@ -116,6 +129,19 @@ class Journal {
   std::vector<uint32_t> ovf_table_;
   uint32_t ovf_off_ = 0, ovf_log2_ = 0;
   bool ovf_dirty_ = false;
+  // point extensions (core.hpp ExtHdr): conj -> its base record and the values added to one clause
+  struct ExtRule {
+    uint32_t table = 0, rec_off = 0, clause = 0, prio = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> values;  // (axis, value), sorted
+    bool operator==(const ExtRule& o) const {
+      return table == o.table && rec_off == o.rec_off && clause == o.clause && prio == o.prio && values == o.values;
+    }
+  };
+  std::map<uint32_t, ExtRule> ext_;
+  uint32_t ext_values_ = 0, ext_off_ = 0;
+  bool journaled_ = false;  // records, tombstones or hard rules since reset (JournalHdr kJUsed)
+  uint32_t pt_off_ = 0, bdead_pt_off_ = 0, odead_pt_off_ = 0;  // last published page tables (reused if unchanged)
+  uint32_t emit_ext();
 };
 
 }  // namespace gpc

@@ -18,6 +18,7 @@ struct EpochArgs {
   uint8_t sort_table[2];  // per policy stage launch: table (1-6) whose scan length groups lanes, 0 = none
   uint32_t ctr_stride;    // per-rule counters: words per copy (counter_cap * kCounterWords)
   uint32_t ctr_mask;      // number of striped copies - 1 (a block updates copy blockIdx & mask)
+  uint32_t mode;          // with a pool: kModeExt = only point extensions over the base, else the journal
 };
 // One packet (index 0 of the device columns) through the table walk with a per-table trace.
 int launch_trace(const EpochArgs& ep, const gpc_pkt_soa& pk, uint4* out, uint4* lb_out, TraceStep* steps, uint32_t* n_steps,

@@ -43,7 +43,8 @@ class gpc_config(C.Structure):
     _fields_ = [("ipv4_enabled", C.c_int32), ("ipv6_enabled", C.c_int32), ("enable_antrea_policy", C.c_int32),
                 ("enable_deny_tracking", C.c_int32), ("cookie", C.c_uint64), ("device", C.c_int32),
                 ("compact_after", C.c_int32), ("ovs_meters", C.c_int32), ("external_node", C.c_int32),
-                ("group_packets", C.c_int32), ("group_key", C.c_int32), ("reserved", C.c_int32 * 2)]
+                ("group_packets", C.c_int32), ("group_key", C.c_int32), ("launch_pacing", C.c_int32),
+                ("reserved", C.c_int32 * 1)]
 
 
 class gpc_addr(C.Structure):
@@ -102,7 +103,8 @@ class gpc_image_stats(C.Structure):
                 ("n_overlay_rules", C.c_uint32), ("n_tombstones", C.c_uint32), ("n_full_builds", C.c_uint64),
                 ("n_delta_builds", C.c_uint64), ("n_background_builds", C.c_uint64), ("group_key", C.c_uint32),
                 ("lane_sort", C.c_uint32), ("v6_full_builds", C.c_uint64), ("v6_delta_builds", C.c_uint64),
-                ("v6_overlay_rules", C.c_uint32), ("v6_prefixes", C.c_uint32)]
+                ("v6_overlay_rules", C.c_uint32), ("v6_prefixes", C.c_uint32), ("n_ext_rules", C.c_uint32),
+                ("n_ext_values", C.c_uint32)]
 
 
 class gpc_endpoint(C.Structure):
@@ -149,7 +151,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_counters_on.argtypes = [vp, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
                                     C.POINTER(sz)]
     lib.gpc_destroy.argtypes = [vp]
-    lib.gpc_debug_fail_uploads.argtypes = [C.c_int]
+    lib.gpc_debug_fail_uploads.argtypes = [vp, C.c_int]
     lib.gpc_destroy.restype = None
     lib.gpc_initialize.argtypes = [vp]
     lib.gpc_install_rule.argtypes = [vp, C.POINTER(gpc_rule)]
@@ -368,14 +370,14 @@ class Classifier:
 
     def __init__(self, ipv4=True, ipv6=False, enable_antrea_policy=True, enable_deny_tracking=False,
                  cookie=0x1020000000000, device=0, compact_after=0, ovs_meters=False, k8s_node=True, group_packets=0,
-                 group_key=0, devices=None):
+                 group_key=0, devices=None, launch_pacing=0):
         self.lib = load()
         cfg = gpc_config(ipv4_enabled=int(ipv4), ipv6_enabled=int(ipv6),
                          enable_antrea_policy=int(enable_antrea_policy),
                          enable_deny_tracking=int(enable_deny_tracking), cookie=cookie, device=device,
                          compact_after=int(compact_after), ovs_meters=int(ovs_meters),
                          external_node=int(not k8s_node), group_packets=int(group_packets),
-                         group_key=int(group_key))
+                         group_key=int(group_key), launch_pacing=int(launch_pacing))
         h = C.c_void_p()
         if devices is None:
             _check(self.lib.gpc_create(C.byref(cfg), C.byref(h)), "gpc_create")
@@ -584,7 +586,7 @@ class Classifier:
 
     def debug_fail_uploads(self, n):
         """Fault injection (tests): the next n device image uploads fail with GPC_EDEV."""
-        _check(self.lib.gpc_debug_fail_uploads(int(n)), "gpc_debug_fail_uploads")
+        _check(self.lib.gpc_debug_fail_uploads(self.h, int(n)), "gpc_debug_fail_uploads")
 
     def classify_host(self, cols: Dict[str, np.ndarray], count=False, lb=False, slot=0):
         """Verdicts (n, 2); with lb=True also the Service stage results (n,) of LB_DTYPE."""
@@ -709,4 +711,5 @@ class Classifier:
                 "n_delta_builds": st.n_delta_builds, "n_background_builds": st.n_background_builds,
                 "group_key": st.group_key, "lane_sort": [st.lane_sort & 0xff, st.lane_sort >> 8],
                 "v6_full_builds": st.v6_full_builds, "v6_delta_builds": st.v6_delta_builds,
-                "v6_overlay_rules": st.v6_overlay_rules, "v6_prefixes": st.v6_prefixes}
+                "v6_overlay_rules": st.v6_overlay_rules, "v6_prefixes": st.v6_prefixes,
+                "n_ext_rules": st.n_ext_rules, "n_ext_values": st.n_ext_values}

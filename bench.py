@@ -87,6 +87,7 @@ class _ChurnOps:
         self.rules = [r for r in wl.rules if r.get("from")]
         self.added = []
         self.issued = 0
+        self.log = []  # (1 add / 0 delete, rule id, IPv4 value, priority or -1): the oracle replays it
 
     def apply(self, k):
         rng, clf = self.rng, self.clf
@@ -94,6 +95,7 @@ class _ChurnOps:
         for _ in range(k):
             if self.added and rng.random() < 0.5:
                 rid, v, prio = self.added.pop(int(rng.integers(len(self.added))))
+                self.log.append((0, rid, v, -1 if prio is None else prio))
                 if fast:
                     fast(False, rid, "src", v, prio)
                 else:
@@ -106,6 +108,7 @@ class _ChurnOps:
                 else:
                     clf.add_policy_rule_address(r["flow_id"], "src", [_ip4(v)], r.get("priority"))
                 self.added.append((r["flow_id"], v, r.get("priority")))
+                self.log.append((1, r["flow_id"], v, -1 if r.get("priority") is None else r.get("priority")))
         self.issued += k
 
 
@@ -164,6 +167,21 @@ def _churn_converge(ops, wl, dev, world):
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
     return {"ops_applied": int(t.item()), "ranks_identical": bool(lo.item() == hi.item()),
             "digest": h.hexdigest()[:16]}
+
+
+LAUNCH_KINDS = ("group_tiles", "classify_egress", "classify_ingress", "classify_both", "unpermute", "v6_codes")
+
+
+def _gather_rank_launch_ms(launches, dev, world):
+    """N > 1: every rank's mean HIP-event ms per launch kind of its timed region (gpc_launch_times),
+    gathered to every rank in rank order (one all_gather; gloo on CPU in tests)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([float(launches.get(k, {}).get("mean_ms", -1.0)) for k in LAUNCH_KINDS], dtype=torch.float64,
+                     device=dev)
+    out = [torch.empty_like(v) for _ in range(world)]
+    dist.all_gather(out, v)
+    return [{k: round(float(x), 3) for k, x in zip(LAUNCH_KINDS, t.cpu().tolist()) if x >= 0} for t in out]
 
 
 def _pmc_pass(counters, args):
@@ -390,20 +408,22 @@ def main():
     if args.family == 6 and args.config in ("C4", "C5"):
         ap.error("--family 6: C1-C3 only (no IPv6 AntreaProxy stage / delta epochs)")
     churn = args.config == "C5"
-    if churn:  # the timed batch sees many epochs; see DESIGN.md for C5's correctness check
+    if churn:  # the timed batch sees many epochs: parity is checked on the final epoch (below)
         args.no_traffic = True
         args.no_cpu_baseline = True
-        args.no_parity = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:  # the CPU baseline is an N=1 figure; every N still gets rank 0's parity stamp
+        args.no_cpu_baseline = True
     worker = None
-    if world == 1 and not (args.no_parity and args.no_cpu_baseline):
+    if rank == 0 and not (args.no_parity and args.no_cpu_baseline):
         # the CPU oracle (oracle compiler + C classifier) is prepared in a spawned process while
-        # this one profiles and times the GPU; it never touches the GPU
+        # this one profiles and times the GPU; it never touches the GPU. C5: it keeps the oracle
+        # compiler and later replays the op log the run applied.
         from oracle.parity import OracleWorker
-        worker = OracleWorker("C3" if churn else args.config)
+        worker = OracleWorker("C3" if churn else args.config, churn=churn)
 
     import torch
     import torch.distributed as dist
@@ -515,6 +535,14 @@ def main():
     clf.set_launch_timing(0)
     for t in launches.values():
         t["per_step"] = t["launches"] / args.steps
+    rank_launches = _gather_rank_launch_ms(launches, dev, world) if world > 1 else None
+    if churn and worker is not None and not args.no_parity:
+        # parity of C5: the oracle replays the op prefix this rank applied (every op was committed
+        # before the control thread stopped), and the final epoch classifies the batch once more
+        _log("oracle replay of %d ops" % len(churn_ops.log))
+        update["oracle_replay"] = worker.churn(churn_ops.log)
+        classify(soa, n, out.data_ptr(), count=False, stream=sptr)
+        torch.cuda.synchronize(dev)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -546,7 +574,7 @@ def main():
         mix[stage] = {names[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
 
     parity = None
-    if worker is not None and not args.no_parity:
+    if worker is not None and not args.no_parity:  # rank 0 (its own shard at N > 1)
         k = min(n, PARITY_SAMPLE)
         idx_h = (torch.arange(k, dtype=torch.int64) * n) // k  # integer stride: every index < n
         assert int(idx_h.max()) < n and int(idx_h.min()) >= 0
@@ -555,8 +583,12 @@ def main():
         got = np.ascontiguousarray(v8[idx].cpu().numpy()).view(VERDICT_DTYPE).reshape(-1, 2)
         _log("parity check of %d sampled packets (waiting for the oracle process)" % len(idx))
         parity = worker.check(sample, got)
-        parity["sample"] = "%d packets, stride %.0f over the timed batch (last step's verdicts)%s" % (
-            len(idx), n / len(idx), "; IPv6 packets vs the IPv4 oracle (fd00:10::/96 embedding)" if v6 else "")
+        parity["sample"] = "%d packets, stride %.0f over the timed batch (%s)%s%s" % (
+            len(idx), n / len(idx),
+            "classified again on the final epoch, vs the oracle after replaying the %d applied ops" % len(churn_ops.log)
+            if churn else "last step's verdicts",
+            "; IPv6 packets vs the IPv4 oracle (fd00:10::/96 embedding)" if v6 else "",
+            "; rank 0's shard of %d" % world if world > 1 else "")
         if parity.get("mismatches"):
             print("PARITY FAILURE: %s" % json.dumps(parity), file=sys.stderr)
 
@@ -586,6 +618,7 @@ def main():
         "kernel_ms": round(kern_ms, 3),  # all launches of a step (HIP events on the launch stream)
         "launches_per_step": round(sum(t["per_step"] for t in launches.values()), 2),
         "kernel_ms_by_launch": {k: round(t["mean_ms"], 3) for k, t in launches.items()},
+        "kernel_ms_by_launch_per_rank": rank_launches,
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity,

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GPC_ABI_VERSION 4
+#define GPC_ABI_VERSION 5
 /* device slots of one context (gpc_create_multi) */
 #define GPC_MAX_DEVICES 16
 
@@ -138,7 +138,12 @@ typedef struct gpc_config {
   int32_t group_key;             /* grouping key of IPv4 batches (gpc_group_key; environment
                                     GPC_GROUP_KEY overrides): 0 = per image, SCAN when waves' scan
                                     lengths are very unequal (long driver lists), else ADDR       */
-  int32_t reserved[2];
+  int32_t launch_pacing;         /* gpc_classify* host-side wait (see gpc_classify): 0 = a call waits
+                                    until the call 8 calls before it on the same stream has
+                                    finished; > 0 = that many calls in flight per stream; < 0 = off
+                                    (never blocks: a caller that keeps its stream's queue full may
+                                    then delay gpc_commit's publish behind its blocking launches) */
+  int32_t reserved[1];
 } gpc_config;
 
 /* Order a grouped batch is classified in, inside every tile of 16384 packets (results never depend
@@ -317,6 +322,11 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
   uint64_t v6_full_builds, v6_delta_builds;
   uint32_t v6_overlay_rules;     /* live rules in the IPv6 journal                               */
   uint32_t v6_prefixes;          /* interned IPv6 prefixes (incl. those added by delta commits)  */
+  /* point extensions (ABI 5): rules whose change since the base only added exact values to one
+   * clause (AddPolicyRuleAddress of Pod IPs / ofports) keep their base record; the added values
+   * are probed per packet instead of walking a journal copy of the rule */
+  uint32_t n_ext_rules;          /* rules with point extensions                                  */
+  uint32_t n_ext_values;         /* added values they hold                                       */
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */
@@ -403,10 +413,14 @@ int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed);
 
 /* ---------------------------------------------------------------------------- data path */
 /* Publish the realized flow table to the device atomically (the bundle commit,
- * ofctrl_bridge.go:468-539). The rules whose flows changed in this commit are appended to an
- * append-only journal over the base image and their older copies tombstoned (a delta epoch: cost
- * proportional to the changed rules); past max(16384, base rules / 4) live journal rules the whole
- * image is rebuilt. Launches already queued keep the epoch they were launched with. */
+ * ofctrl_bridge.go:468-539). A rule whose change since the base image only added exact values to
+ * one clause (AddPolicyRuleAddress of Pod IPs, ofports, single ports) keeps its base record and the
+ * added values become point extensions (gpc_image_stats n_ext_*); the other changed rules are
+ * appended to an append-only journal over the base image and their older copies tombstoned (a
+ * delta epoch: cost proportional to the changed rules). A background compactor rebuilds the base
+ * once compact_after rules are extended or journaled; past max(16384, base rules / 4) live journal
+ * rules without one the whole image is rebuilt inline. Launches already queued keep the epoch they
+ * were launched with. */
 int gpc_commit(gpc_ctx* ctx);
 /* Same, but always rebuilds the whole image (compaction: empties the overlay). */
 int gpc_compact(gpc_ctx* ctx);
@@ -422,7 +436,12 @@ int gpc_replay(gpc_ctx* ctx);
  * library keeps per-stream scratch (packet grouping) and epoch-lifetime events, keyed by the
  * stream and, for hipStreamPerThread, by the calling thread as well. With group_packets == 0 a
  * batch whose grouping scratch cannot be allocated runs ungrouped; -GPC_ENOMEM only when
- * grouping was forced (group_packets > 0). */
+ * grouping was forced (group_packets > 0).
+ * The launch is asynchronous on `stream`, but the call may BLOCK ON THE HOST (launch pacing): it
+ * first waits, outside every lock, until the call gpc_config.launch_pacing (default 8) calls
+ * before it on the same stream and slot has finished, so that no launch blocks inside the lock a
+ * commit publishes under (a caller that keeps its stream's queue full would otherwise delay every
+ * gpc_commit by ~1 s). A caller that must never block sets launch_pacing < 0. */
 int gpc_classify(gpc_ctx* ctx, const gpc_pkt_soa* pkts, size_t n, gpc_verdict* out, int32_t count, void* stream);
 /* gpc_classify plus the AntreaProxy stage in front of the policy tables: packets to a Service
  * (ServiceLB flow hit) get an Endpoint from the group (select bucket by a symmetric L4 hash of the
@@ -490,10 +509,12 @@ int gpc_debug_service_image(gpc_ctx* ctx, const uint32_t** blob, size_t* n_words
 int gpc_debug_epoch(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
 /* The same for the IPv6 image's journal (IPv6 delta epochs). */
 int gpc_debug_epoch6(gpc_ctx* ctx, const uint32_t** pool, size_t* pool_words, uint32_t* jhdr);
-/* Test hook (fault injection): the next `n` device image uploads of gpc_commit / gpc_compact fail
- * with GPC_EDEV, as a device error would; the host shadow state keeps the new build, and the next
- * successful commit re-uploads every base the device slots do not hold (tests/test_gpu_ipv6_delta.py). */
-int gpc_debug_fail_uploads(int n);
+/* Test hook (fault injection): the next `n` device image uploads of this context's gpc_commit /
+ * gpc_compact / gpc_replay fail with GPC_EDEV, as a device error would (the background
+ * compactor's uploads and other contexts are unaffected); the host shadow state keeps the new
+ * build, and the next successful commit re-uploads every base the device slots do not hold
+ * (tests/test_gpu_ipv6_delta.py). */
+int gpc_debug_fail_uploads(gpc_ctx* ctx, int n);
 /* The epoch (gpc_image_stats.epoch) the last gpc_classify* launch on `stream` was bound to: with
  * classification concurrent to commits, every launch sees exactly this one committed epoch. */
 int gpc_stream_epoch(gpc_ctx* ctx, void* stream, uint64_t* epoch);

@@ -86,13 +86,30 @@ def service_flows(wl):
         del c
 
 
-def oracle_pipeline(wl, procs: Optional[int] = None):
+def oracle_pipeline(wl, procs: Optional[int] = None, flows=None):
     from .cls_c import CPipeline
     svc = service_flows(wl)
-    pipe = CPipeline(oracle_flows(wl) + (svc[0] if svc else []), tiers_of(wl), procs=procs)
+    pipe = CPipeline((oracle_flows(wl) if flows is None else flows) + (svc[0] if svc else []), tiers_of(wl), procs=procs)
     if svc:
         pipe.set_services(svc[1], svc[2])
     return pipe
+
+
+def _ip4(v: int) -> str:
+    return "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+def replay_churn(fnp, ops) -> int:
+    """Apply bench.py's C5 op log to the oracle compiler: (kind, rule id, IPv4 value, priority) with
+    kind 1 = AddPolicyRuleAddress, 0 = DeletePolicyRuleAddress of one /32 source peer
+    (network_policy.go:1661-1710), in the order the product applied them."""
+    for kind, rid, v, prio in ops:
+        prio = None if prio is None or prio < 0 else int(prio)
+        if kind:
+            fnp.add_policy_rule_address(int(rid), "src", [_ip4(int(v))], prio)
+        else:
+            fnp.delete_policy_rule_address(int(rid), "src", [_ip4(int(v))], prio)
+    return len(ops)
 
 
 def oracle_metrics(pipe) -> Dict[int, tuple]:
@@ -127,11 +144,19 @@ def compare(got: np.ndarray, want: np.ndarray, mask: Optional[np.ndarray] = None
 
 
 # ------------------------------------------------------------------------------ worker process
-def _serve(conn, config: str, procs: int):
+def _serve(conn, config: str, procs: int, churn: bool = False):
     from antrea_amd import workload
+    from . import compiler as oc
     t0 = time.time()
     wl = workload.CONFIGS[config]()
-    pipe = oracle_pipeline(wl, procs=procs)
+    fnp = None
+    if churn:  # keep the oracle compiler: the op log of the run is replayed on it afterwards
+        fnp = oc.FeatureNetworkPolicy()
+        fnp.initialize()
+        fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+        pipe = oracle_pipeline(wl, procs=procs, flows=fnp.dump_flows())
+    else:
+        pipe = oracle_pipeline(wl, procs=procs)
     conn.send({"ready": True, "setup_s": round(time.time() - t0, 1), "flows": pipe.n_flows})
     while True:
         try:
@@ -145,6 +170,14 @@ def _serve(conn, config: str, procs: int):
             res = compare(verdicts, want)
             res["oracle_s"] = round(time.time() - t, 2)
             conn.send(res)
+        elif msg[0] == "churn":  # replay the applied op prefix, then classify against its flows
+            t = time.time()
+            n = replay_churn(fnp, msg[1])
+            t_replay = time.time() - t
+            del pipe
+            pipe = oracle_pipeline(wl, procs=procs, flows=fnp.dump_flows())
+            conn.send({"ops": n, "replay_s": round(t_replay, 1), "rebuild_s": round(time.time() - t - t_replay, 1),
+                       "flows": pipe.n_flows})
         elif msg[0] == "baseline":
             _, seconds, chunk = msg
             conn.send(time_baseline(wl, pipe, seconds, chunk, procs))
@@ -184,13 +217,13 @@ def time_baseline(wl, pipe, seconds: float, chunk: int, threads: int) -> dict:
 class OracleWorker:
     """CPU oracle in a spawned process (bench.py: parity stamp + CPU baseline)."""
 
-    def __init__(self, config: str, procs: Optional[int] = None):
+    def __init__(self, config: str, procs: Optional[int] = None, churn: bool = False):
         import multiprocessing as mp
         ctx = mp.get_context("spawn")
         self.procs = procs or cpu_threads()
         self.conn, child = ctx.Pipe()
         # not a daemon: the worker forks a pool to convert large flow dumps
-        self.p = ctx.Process(target=_serve, args=(child, config, self.procs), daemon=False)
+        self.p = ctx.Process(target=_serve, args=(child, config, self.procs, churn), daemon=False)
         self.p.start()
         self.info = None
         import atexit
@@ -209,6 +242,12 @@ class OracleWorker:
         res = self.conn.recv()
         res["oracle_setup_s"] = info["setup_s"]
         return res
+
+    def churn(self, ops) -> dict:
+        """Replay an op log (replay_churn) in the worker; later checks classify against the result."""
+        self._ready()
+        self.conn.send(("churn", ops))
+        return self.conn.recv()
 
     def baseline(self, seconds: float, chunk: int = 4096) -> dict:
         self._ready()

@@ -35,11 +35,16 @@ using namespace gpc;
 extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_t* pool, uint32_t jhdr,
                             const uint32_t* svc, const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, uint32_t* lb_out,
                             unsigned long long* counters) {
-  View im{{blob, static_cast<const ImageHdr*>(hdr), nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr};
+  View im{{blob, static_cast<const ImageHdr*>(hdr), nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr, 0u};
+  int mode = kModeBase;  // as the device launch picks it (api.cpp: JournalHdr jflags)
   if (pool) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + jhdr);
-    if (jh->bdead_off) im.base.dead = pool + jh->bdead_off;
-    im.n_img = 2u;
+    im.ext = jh->ext_off;
+    mode = (jh->jflags & kJUsed) ? kModeJournal : kModeExt;
+    if (mode == kModeJournal) {
+      if (jh->bdead_off) im.base.dead = pool + jh->bdead_off;
+      im.n_img = 2u;
+    }
   }
   for (size_t i = 0; i < n; i++) {
     const uint32_t src = pk->src[i];
@@ -68,7 +73,10 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
     g_line_site.clear();
     const unsigned long long v0 = ::gpc_emu_stats[3], s0 = ::gpc_emu_stats[4], p0 = ::gpc_emu_stats[8],
                              q0 = ::gpc_emu_stats[9], r0 = ::gpc_emu_stats[10];
-    PacketOut o = classify_packet(im, p, dest, pk->ct_mark ? pk->ct_mark[i] : 0u);
+    const uint32_t cm = pk->ct_mark ? pk->ct_mark[i] : 0u;
+    PacketOut o = mode == kModeJournal ? classify_packet<kModeJournal>(im, p, dest, cm)
+                  : mode == kModeExt   ? classify_packet<kModeExt>(im, p, dest, cm)
+                                       : classify_packet<kModeBase>(im, p, dest, cm);
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     std::sort(g_lines.begin(), g_lines.end());
@@ -94,11 +102,12 @@ extern "C" int emu_classify(const uint32_t* blob, const void* hdr, const uint32_
 // gpc_trace's walk (core.hpp classify_packet<..., kTrace>) for packet 0 of the columns (no Service stage).
 extern "C" int emu_trace(const uint32_t* blob, const void* hdr, const uint32_t* pool, uint32_t jhdr, const gpc_pkt_soa* pk,
                          gpc_verdict* out, TraceStep* steps, uint32_t* n_steps) {
-  View im{{blob, static_cast<const ImageHdr*>(hdr), nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr};
+  View im{{blob, static_cast<const ImageHdr*>(hdr), nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr, 0u};
   if (pool) {
     const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + jhdr);
     if (jh->bdead_off) im.base.dead = pool + jh->bdead_off;
     im.n_img = 2u;
+    im.ext = jh->ext_off;
   }
   const uint32_t src = pk->src[0], dst = pk->dst[0];
   uint32_t pst[kPktWords];
@@ -108,7 +117,7 @@ extern "C" int emu_trace(const uint32_t* blob, const void* hdr, const uint32_t* 
            pk->ct_dst ? pk->ct_dst[0] : dst, pk->ct_state ? pk->ct_state[0] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
            view_bloom_axes(im));
   *n_steps = 0;
-  PacketOut o = classify_packet<true, 0, true>(im, p, pk->dest ? pk->dest[0] : 0u, pk->ct_mark ? pk->ct_mark[0] : 0u, steps,
+  PacketOut o = classify_packet<kModeJournal, 0, true>(im, p, pk->dest ? pk->dest[0] : 0u, pk->ct_mark ? pk->ct_mark[0] : 0u, steps,
                                                n_steps);
   uint32_t* w = reinterpret_cast<uint32_t*>(out);
   w[0] = o.e.conj;
@@ -122,7 +131,7 @@ extern "C" int emu_trace(const uint32_t* blob, const void* hdr, const uint32_t* 
 extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const uint32_t* pool, uint32_t jhdr,
                              const gpc_pkt_soa* pk, size_t n, gpc_verdict* out, unsigned long long* counters) {
   const ImageHdr* h = static_cast<const ImageHdr*>(hdr);
-  View im{{blob, h, nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr};
+  View im{{blob, h, nullptr, pool}, {pool, nullptr, nullptr, pool}, 1u, jhdr, 0u};
   const uint32_t* ovf = nullptr;
   uint32_t ovf_log2 = 0;
   if (pool) {  // an IPv6 delta epoch (gpc_debug_epoch6)
@@ -160,7 +169,7 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const uint32
              pk->svc_group ? pk->svc_group[i] : 0u, pk->tun_id ? pk->tun_id[i] : 0u, ct_src, ct_dst,
              pk->ct_state ? pk->ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK), view_bloom_axes(im));
     const uint32_t cm = pk->ct_mark ? pk->ct_mark[i] : 0u;
-    PacketOut o = pool ? classify_packet<true, 0>(im, p, dest, cm) : classify_packet<false, 0>(im, p, dest, cm);
+    PacketOut o = pool ? classify_packet<kModeJournal, 0>(im, p, dest, cm) : classify_packet<kModeBase, 0>(im, p, dest, cm);
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;

@@ -72,3 +72,62 @@ def test_grouping_label_from_launches():
     assert lab.startswith("key: top 8 bits of nw_src") and lab.endswith("results un-permuted")
     assert "IPv6 code columns" in bench._grouping_label(st, {"group_tiles": {}}, True)
     assert "scan-length" in bench._grouping_label({"group_key": gpc.GROUP_KEY_SCAN}, {"group_tiles": {}}, False)
+
+
+def _rank_launch_worker(rank, port, outdir):
+    import json
+    import os
+
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    # the classify call is stubbed: what gpc_launch_times would report for this rank's timed region
+    launches = {"classify_egress": {"mean_ms": 3.0 + rank, "launches": 10},
+                "classify_ingress": {"mean_ms": 4.5 + rank, "launches": 10}}
+    if rank == 1:
+        launches["group_tiles"] = {"mean_ms": 0.7, "launches": 10}
+    got = bench._gather_rank_launch_ms(launches, torch.device("cpu"), 2)
+    with open(os.path.join(outdir, "r%d.json" % rank), "w") as f:
+        json.dump(got, f)
+    dist.destroy_process_group()
+
+
+def test_rank_launch_times_world2(tmp_path):
+    """N > 1 line assembly: every rank's per-launch HIP-event times reach rank 0
+    in rank order, launch kinds a rank did not run are absent from its entry."""
+    import json
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_rank_launch_worker, args=(port, str(tmp_path)), nprocs=2, join=True)
+    for r in (0, 1):
+        got = json.load(open(tmp_path / ("r%d.json" % r)))
+        assert got == [{"classify_egress": 3.0, "classify_ingress": 4.5},
+                       {"group_tiles": 0.7, "classify_egress": 4.0, "classify_ingress": 5.5}]
+
+
+def test_churn_op_log_replays_on_the_oracle():
+    """C5 parity: the op log bench._ChurnOps records, replayed on the oracle
+    compiler, gives the flows the product compiler realized applying the same ops."""
+    import copy
+
+    from antrea_amd import gpc
+    from oracle import compiler as oc
+    from oracle.parity import replay_churn
+    wl = workload.config3(seed=5, n_policies_per_dir=6, rules_per_policy=10)
+    clf = gpc.Classifier(compact_after=-1)
+    clf.initialize()
+    clf.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    ops = bench._ChurnOps(clf, wl, seed=99)
+    for _ in range(40):
+        ops.apply(5)
+    assert len(ops.log) == 200 and {k for k, *_ in ops.log} == {0, 1}
+    fnp = oc.FeatureNetworkPolicy()
+    fnp.initialize()
+    fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    assert replay_churn(fnp, ops.log) == 200
+    assert sorted(fnp.dump_flows()) == sorted(clf.dump_flows())

@@ -86,11 +86,15 @@ def test_gpu_ingress_classifier(k8s):
     assert ((got[:, 1]["action"] == 6).sum() > n // 4) == k8s
 
 
-def test_gpu_lane_sort_delta_epochs(monkeypatch):
+@pytest.mark.parametrize("ext", [1, 0], ids=["extensions", "journal_only"])
+def test_gpu_lane_sort_delta_epochs(monkeypatch, ext):
     """GPC_LANE_SORT=1 read at commit: the lane-regrouping kernels run on delta epochs (journal +
-    tombstones + sorted lanes, the stage-2 live prefilter included); verdicts and counters equal
-    the host emulation of the same epoch."""
+    tombstones + sorted lanes, the stage-2 live prefilter included; with point extensions the
+    added addresses are extensions of base records beside the uninstalls' tombstones); verdicts
+    and counters equal the host emulation of the same epoch."""
     monkeypatch.setenv("GPC_LANE_SORT", "1")
+    if not ext:
+        monkeypatch.setenv("GPC_NO_EXTENSIONS", "1")
     wl = workload.config3(n_policies_per_dir=20, rules_per_policy=50)
     n = 60000
     cols = workload.gen_packets(wl, n, seed=41)
@@ -113,7 +117,8 @@ def test_gpu_lane_sort_delta_epochs(monkeypatch):
             live.append(r)
         c.commit()
     st = c.image_stats()
-    assert st["n_delta_builds"] >= 8 and st["n_overlay_rules"] > 0
+    assert st["n_delta_builds"] >= 8 and st["n_tombstones"] > 0
+    assert (st["n_ext_rules"] > 0 and st["n_overlay_rules"] == 0) if ext else st["n_overlay_rules"] > 0, st
     c.reset_counters()
     got = c.classify_host(cols, count=True)
     _, slots = c.counters()
@@ -201,7 +206,10 @@ def test_gpu_concurrent_commits_c3_vs_oracle():
     marker, while the main thread keeps launching classification on its own stream. For the first,
     a middle and the last commit, the control thread waits until a launch is bound to that epoch
     (gpc_stream_epoch); that launch's verdicts equal the C oracle over the ORACLE compiler's replay
-    of the same op prefix (make_churn_fixture.py verdicts_at_k / verdicts)."""
+    of the same op prefix (make_churn_fixture.py verdicts_at_k / verdicts). The background compactor
+    is on: after the middle check the control thread keeps committing until a
+    compacted base has been handed over, so the last checked epoch sits on a base the compactor
+    built while launches were in flight, with the rest of the log in its catch-up journal."""
     import torch
     from oracle import parity
     from tests.golden import make_churn_fixture as mcf
@@ -218,11 +226,13 @@ def test_gpu_concurrent_commits_c3_vs_oracle():
     signed = {4: np.int32, 2: np.int16, 1: np.uint8}
     dcols = {k: torch.as_tensor(np.ascontiguousarray(v).view(signed[v.dtype.itemsize])).to(dev) for k, v in cols.items()}
     soa = gpc.pkt_soa_device(dcols)
-    c = gpc.Classifier(compact_after=-1)
+    c = gpc.Classifier(compact_after=256)
     c.initialize()
     c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
     c.commit()
     want_epoch = {}  # commit number -> epoch published for it (checked ones)
+    bg_at = {}       # commit number -> background builds installed when it was checked
+    mid = sorted(check)[1]
     waiting = {"epoch": None}
     seen = threading.Event()
     stop, errors = threading.Event(), []
@@ -234,12 +244,21 @@ def test_gpu_concurrent_commits_c3_vs_oracle():
             c.commit()
             k[0] += 1
             if k[0] in check:
-                e = c.image_stats()["epoch"]
+                st = c.image_stats()
+                e = st["epoch"]
                 want_epoch[k[0]] = e
+                bg_at[k[0]] = st["n_background_builds"]
                 seen.clear()
                 waiting["epoch"] = e
                 if not seen.wait(120):
                     raise RuntimeError("no launch bound to epoch %d" % e)
+            if k[0] == mid:  # let a compaction finish and hand over (empty commits install it)
+                t0 = time.time()
+                while c.image_stats()["n_background_builds"] <= bg_at[mid]:
+                    if time.time() - t0 > 90:
+                        raise RuntimeError("no background compaction handed over")
+                    time.sleep(0.05)
+                    c.commit()
             time.sleep(0.001)
 
         try:
@@ -268,6 +287,8 @@ def test_gpu_concurrent_commits_c3_vs_oracle():
     assert not errors, errors
     st = c.image_stats()
     assert st["n_delta_builds"] >= n_commits - 2, st  # the log went through delta epochs
+    first, last = min(check), max(check)
+    assert bg_at[last] > bg_at[first], (bg_at, st)  # a compacted base was handed over between them
     for k, want in sorted(check.items()):
         got = bound[want_epoch[k]].cpu().numpy().view(gpc.VERDICT_DTYPE).reshape(n, 2)[:len(want)]
         res = parity.compare(got, want)
@@ -324,7 +345,8 @@ def test_gpu_replay_rebuilds_device_state():
     c.add_policy_rule_address(wl.rules[0]["flow_id"], "src", ["10.10.0.77", "fd00:10::10.10.0.77"],
                               wl.rules[0].get("priority"))
     c.commit()
-    assert c.image_stats()["n_overlay_rules"] > 0  # a delta epoch: the journal pool must travel too
+    st = c.image_stats()  # a delta epoch (IPv4: a point extension; IPv6: the journal): the pools must travel too
+    assert st["n_ext_rules"] > 0 and st["v6_overlay_rules"] > 0, st
     cols = workload.gen_packets(wl, 20000, seed=71)
     v4 = c.classify_host(cols, count=True)
     v6 = c.classify6_host(workload.packets_to_v6(cols))

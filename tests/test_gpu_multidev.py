@@ -68,7 +68,7 @@ def test_two_slots_and_two_contexts_same_delta_stream(group):
             assert multi.stream_epoch() == multi.image_stats()["epoch"]
     sm, ss = multi.image_stats(), single.image_stats()
     assert sm["epoch"] == ss["epoch"] and sm["n_delta_builds"] == ss["n_delta_builds"] >= 12
-    assert sm["n_overlay_rules"] == ss["n_overlay_rules"] > 0
+    assert sm["n_overlay_rules"] == ss["n_overlay_rules"] > 0 and sm["n_ext_rules"] == ss["n_ext_rules"]
     multi.reset_counters()
     single.reset_counters()
     multi.set_launch_timing(8)

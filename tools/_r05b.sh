@@ -1,0 +1,6 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r05b; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_gpu_fullscale.py tests/test_gpu_boundary.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+GPC_COMPACT_DEBUG=1 bash tools/c5_long.sh r05b 3500 2>&1 | tail -5
