@@ -742,6 +742,7 @@ struct JournalHdr {
   uint32_t v6_ovf_off, v6_ovf_log2;
   uint32_t ext_off;        // ExtHdr of this epoch's point extensions (0: none)
   uint32_t jflags;         // kJUsed: the journal holds records, tombstones or hard rules (else only extensions)
+  uint32_t live;           // bit t-1: table t has journal chains, always entries or hard rules
   JournalTable t[6];
 };
 constexpr uint32_t kJUsed = 1u;
@@ -1469,11 +1470,12 @@ GPC_HD TableResult finish_part(const uint32_t* base_blob, const uint32_t* ovl_bl
 GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
   const uint32_t* pool = v.ovl.blob;
   const JournalHdr* jh = reinterpret_cast<const JournalHdr*>(pool + v.jhdr);
+  TablePart res;
+  res.h = res.s = res.win = 0;
+  if (!((jh->live >> (table - 1)) & 1u)) return res;  // nothing of this table in the journal (uniform)
   const JournalTable& jt = jh->t[table - 1];
   const uint32_t* odead = jh->odead_off ? pool + jh->odead_off : nullptr;
   Img im{pool, nullptr, odead, pool};
-  TablePart res;
-  res.h = res.s = res.win = 0;
   uint32_t hprio = 0, hverdict = RV_MISS, htie = 0;
   bool hfound = false;
   for (uint32_t h = 0; h < jt.n_hard; h++) {
@@ -1604,22 +1606,63 @@ GPC_HD uint32_t ext_hash(uint32_t table, uint32_t axis, uint32_t v) {
   return mix32(v ^ mix32(((table << 4) | axis) * 0x9e3779b1u + 0x632be5abu));
 }
 
+// The presence words of a table's extended axes (at most two; more: scanned unconditionally),
+// loaded before the base walk so their latency hides behind it (ext_begin), tested after it
+// (ext_hits). Three registers live across the walk: the two words and their bit positions.
+struct ExtProbe {
+  uint32_t w0, w1;  // presence words of the first two extended axes
+  uint32_t bits;    // their bit positions: b0 | b1 << 8 (0xffff: no such axis)
+};
+GPC_HD ExtProbe ext_begin(const View& v, uint32_t table, const Pkt& p) {
+  const uint32_t* pool = v.ovl.blob;
+  const ExtHdr* eh = reinterpret_cast<const ExtHdr*>(pool + v.ext);
+  uint32_t axes = eh->axes[table - 1];
+  ExtProbe x;
+  x.w0 = x.w1 = 0;
+  x.bits = 0xffffu;
+  const uint32_t sh = 32u - eh->pres_log2;
+  for (uint32_t i = 0; i < 2 && axes; i++) {
+    const uint32_t a = uint32_t(__builtin_ctz(axes));
+    axes &= axes - 1u;
+    const uint32_t pb = ext_hash(table, a, p.ax[a]) >> sh;
+    GPC_TOUCH(pool + eh->pres_off + (pb >> 5), 4);
+    const uint32_t w = pool[eh->pres_off + (pb >> 5)];
+    if (i == 0) {
+      x.w0 = w;
+      x.bits = (x.bits & 0xff00u) | (pb & 31u);
+    } else {
+      x.w1 = w;
+      x.bits = (x.bits & 0x00ffu) | ((pb & 31u) << 8);
+    }
+  }
+  return x;
+}
+// Which extended axes the packet must scan: bit i = the i-th extended axis of the table (the first
+// two by their presence bits, the others always).
+GPC_HD uint32_t ext_hits(const View& v, uint32_t table, const ExtProbe& x) {
+  const ExtHdr* eh = reinterpret_cast<const ExtHdr*>(v.ovl.blob + v.ext);
+  const uint32_t axes = eh->axes[table - 1];
+  const uint32_t n = uint32_t(__builtin_popcount(axes));
+  const uint32_t b0 = (x.bits & 0xffu) != 0xffu ? (x.w0 >> (x.bits & 31u)) & 1u : 0u;
+  const uint32_t b1 = ((x.bits >> 8) & 0xffu) != 0xffu ? (x.w1 >> ((x.bits >> 8) & 31u)) & 1u : 0u;
+  return b0 | (b1 << 1) | (n > 2 ? ((1u << n) - 1u) & ~3u : 0u);
+}
+
 // Best completion among the extended rules the packet's values reach in this table (hard rules are
 // never extended): priority desc, conj id asc, and whether two rules completed at that level.
-GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p) {
+// hits: ext_hits.
+GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p, uint32_t hits) {
   TablePart res;
   res.h = res.s = res.win = 0;
   const uint32_t* pool = v.ovl.blob;
   const ExtHdr* eh = reinterpret_cast<const ExtHdr*>(pool + v.ext);
   uint32_t axes = eh->axes[table - 1];
   uint32_t best = 0, best_prio = 0, best_conj = 0, at_best = 0;
-  while (axes) {
+  for (uint32_t i = 0; axes; i++) {
     const uint32_t a = uint32_t(__builtin_ctz(axes));
     axes &= axes - 1u;
+    if (!((hits >> i) & 1u)) continue;
     const uint32_t val = p.ax[a], h = ext_hash(table, a, val);
-    const uint32_t pb = h >> (32u - eh->pres_log2);
-    GPC_TOUCH(pool + eh->pres_off + (pb >> 5), 4);
-    if (!((pool[eh->pres_off + (pb >> 5)] >> (pb & 31u)) & 1u)) continue;
     uint32_t e, end;
     GPC_TOUCH(pool + eh->bkt_off + (h & ((1u << eh->bkt_log2) - 1u)), 8);
     load_pair(pool + eh->bkt_off + (h & ((1u << eh->bkt_log2) - 1u)), &e, &end);
@@ -1627,30 +1670,27 @@ GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p) {
     for (; e < end; e++) {
       const uint32_t* en = pool + eh->ent_off + e * kExtEntWords;
       GPC_TOUCH(en, 16);
-      uint32_t ew[kExtEntWords];
 #if defined(__HIPCC__)
       const uint4 q = *reinterpret_cast<const uint4*>(en);
-      ew[0] = q.x, ew[1] = q.y, ew[2] = q.z, ew[3] = q.w;
 #else
-      for (uint32_t w = 0; w < kExtEntWords; w++) ew[w] = en[w];
+      const struct { uint32_t x, y, z, w; } q = {en[0], en[1], en[2], en[3]};
 #endif
-      if (ew[0] != val || (ew[1] & 0x7fu) != meta) continue;
-      const uint32_t prio = ew[3];
+      if (q.x != val || (q.y & 0x7fu) != meta) continue;
+      const uint32_t prio = q.w;
       if (best && prio < best_prio) continue;  // cannot change the decision
-      const uint32_t* rec = v.base.blob + ew[2];
+      const uint32_t* rec = v.base.blob + q.z;
       GPC_TOUCH(rec, 4 * kRecLine);
-      const RecLine hd = load_rec_line(rec);
-      const uint32_t conj = hd.w[0];
-      if (!rule_match(v.base, rec, hd.w[2], &hd.w[kRecFcd], 1u << (ew[1] >> 7), p)) continue;
+      const uint32_t conj = rec[0];
+      if (!rule_match(v.base, rec, rec[2], rec + kRecFcd, 1u << (q.y >> 7), p)) continue;
       if (!best || prio > best_prio) {
-        best = ew[2];
+        best = q.z;
         best_prio = prio;
         best_conj = conj;
         at_best = 1;
       } else if (conj != best_conj) {
         at_best++;
         if (conj < best_conj) {
-          best = ew[2];
+          best = q.z;
           best_conj = conj;
         }
       }
@@ -1679,7 +1719,11 @@ GPC_HD TablePart merge_ext(const View& v, const TablePart& a, const TablePart& e
       r.win = a.win;
       return r;
     }
-    const uint32_t ca = (a.s & kSNoAct) ? 0xffffffffu : ((a.s & kSImg) ? v.ovl.blob : v.base.blob)[a.win];
+    // (the blobs are read into values first: selecting between two fields of the View by address
+    // keeps the whole View in scratch memory)
+    const uint32_t* const ob = v.ovl.blob;
+    const uint32_t* const bb = v.base.blob;
+    const uint32_t ca = (a.s & kSNoAct) ? 0xffffffffu : (a.s & kSImg) ? ob[a.win] : bb[a.win];
     const uint32_t ce = v.base.blob[e.win];
     const bool pe = ce < ca;
     r.s = (pe ? e.s : a.s) | kSTie;
@@ -1698,9 +1742,15 @@ GPC_HD TablePart merge_ext(const View& v, const TablePart& a, const TablePart& e
 // instantiation compiles neither the journal nor the extension code.
 template <int kMode>
 GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
+  ExtProbe xp;  // point extensions: presence words in flight during the base walk
+  const bool ext = kMode >= kModeExt && v.ext;
+  if (ext) xp = ext_begin(v, table, p);
   TablePart acc = eval_part(v.base, table, p);
   if (kMode >= kModeJournal && v.n_img > 1) acc = combine_parts(v, acc, eval_journal(v, table, p));
-  if (kMode >= kModeExt && v.ext) acc = merge_ext(v, acc, eval_ext(v, table, p));
+  if (ext) {
+    const uint32_t hits = ext_hits(v, table, xp);
+    if (GPC_WAVE_ANY(hits != 0u)) acc = merge_ext(v, acc, eval_ext(v, table, p, hits));
+  }
   return finish_part(v.base.blob, kMode >= kModeJournal ? v.ovl.blob : nullptr, acc);
 }
 
@@ -1845,9 +1895,12 @@ GPC_HD StageOut walk_stage(const View& im, const Pkt& p, uint32_t t0, TraceStep*
   uint32_t conj = 0, ft = 0;  // ft = flags | tier << 8 (reg5/reg6 after a Pass keep its conj id and tier)
   for (uint32_t i = 0;; i++) {
     const uint32_t t = t0 + i;
-    // a table without rules (epochs without a journal: extended rules are base rules): a miss,
-    // without reading its header
-    if (kMode < kModeJournal && !kTrace && !((im.base.hdr->live >> (t - 1)) & 1u)) {
+    // a table without rules (base, or journal: neither the base nor the journal has any; extended
+    // rules are base rules): a miss, without reading its header
+    const uint32_t live = kMode < kModeJournal || im.n_img < 2
+                              ? im.base.hdr->live
+                              : im.base.hdr->live | reinterpret_cast<const JournalHdr*>(im.ovl.blob + im.jhdr)->live;
+    if (!kTrace && !((live >> (t - 1)) & 1u)) {
       if (i < 2) continue;
       StageOut o;
       o.slot = 0;

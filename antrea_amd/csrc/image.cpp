@@ -953,6 +953,75 @@ bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vect
 // C4 12.18 -> 11.38.
 constexpr size_t kCompositeMaxValues = 16;
 constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 24;  // 256 MB of entries at most
+// Band merging (round 5). Every sub-index is a probe -- a dependent bucket-offset load and an entry
+// load, lines of 25-30 MB arrays that miss L2 -- so a packet pays per band, not per entry. Per IP
+// axis of the band clause, the atoms of bands m.. are keyed at band m's granularity (one sub-index)
+// for the coarsest m whose (key, value) lists stay short: the entry-weighted mean list length
+// sum(len^2) / sum(len) over the exact (band-m key, value) pairs at most kMergeListMax -- and only
+// when the index's entries exceed kMergeMinBytes (an L2-resident index pays little per probe and
+// much per scanned entry). Measured (64M packets, profiles/r05e, r05f; the statistic in brackets):
+// C3 (CIDRs /8-/32 spread over the address space) 7.98 ms unmerged, 6.11 with m = 1 [6.2], 5.58
+// with m = 0 [11]; C4 7.58 -> 5.41 (m = 0); C2 (AddressGroup /32s inside a few /16s) 7.94 unmerged,
+// 29.2 with m = 3 [29-34], 73.5 with m = 1; C1 (0.08 MB image) 5.80 unmerged, 7.38 with m = 3 [3-4],
+// 8.07 with m = 0.
+constexpr double kMergeListMax = 16.0;
+constexpr uint64_t kMergeMinBytes = uint64_t(16) << 20;
+template <typename CE>
+void merge_bands(std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>>& sub, const std::vector<std::vector<uint32_t>>& xsets) {
+  std::set<uint8_t> axes;
+  uint64_t entries = 0;
+  for (auto& kv : sub) {
+    axes.insert(kv.first.first);
+    for (auto& e : kv.second) entries += atom_span(e.key) * xsets[e.xi].size();
+  }
+  if (entries * sizeof(Ent) < kMergeMinBytes) return;
+  for (uint8_t ax : axes) {
+    for (uint32_t m = 0; m + 1 < kIpBands; m++) {
+      const uint32_t sh = ip_band_shift(m);
+      std::vector<uint64_t> combos;
+      bool big = false;
+      for (auto& kv : sub) {
+        if (kv.first.first != ax || kv.first.second < m || big) continue;
+        for (auto& e : kv.second) {
+          for (uint64_t k = e.key.lo >> sh; k <= (e.key.hi >> sh) && !big; k++)
+            for (uint32_t x : xsets[e.xi]) combos.push_back((k << 32) | x);
+          big = combos.size() > kCompositeMaxEntries;
+        }
+      }
+      if (big || combos.empty()) continue;
+      std::sort(combos.begin(), combos.end());
+      double s1 = 0, s2 = 0;
+      for (size_t i = 0; i < combos.size();) {
+        size_t j = i;
+        while (j < combos.size() && combos[j] == combos[i]) j++;
+        const double c = double(j - i);
+        s1 += c;
+        s2 += c * c;
+        i = j;
+      }
+      const bool merge = s2 / s1 <= kMergeListMax;
+      if (std::getenv("GPC_IMAGE_DEBUG"))
+        std::fprintf(stderr, "composite axis %u: bands >= %u at band %u: %zu entries, mean list %.2f -> %s\n", ax, m, m,
+                     combos.size(), s2 / s1, merge ? "merged" : "kept");
+      if (!merge) continue;
+      std::vector<CE> moved;
+      for (auto it = sub.begin(); it != sub.end();) {
+        if (it->first.first == ax && it->first.second > m) {
+          for (auto& e : it->second) {
+            e.key.band = uint8_t(m);
+            moved.push_back(e);
+          }
+          it = sub.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      auto& dst = sub[{ax, uint8_t(m)}];
+      dst.insert(dst.end(), moved.begin(), moved.end());
+      break;
+    }
+  }
+}
 void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>& rec_off, const uint64_t* span, int t,
                      TableHdr& th, Blob& B, HostImage* out) {
   th.n_cidx = 0;
@@ -965,6 +1034,10 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     uint32_t xi;  // index of the rule's value list in xsets
     std::array<uint32_t, 4> ent;
   };
+  // GPC_CBAND_MERGE=m (experiments): key every band above m at band m's granularity, instead of the
+  // adaptive choice below
+  const char* mb = std::getenv("GPC_CBAND_MERGE");
+  const int merge_to = mb ? std::min(int(kIpBands) - 1, std::max(0, std::atoi(mb))) : int(kIpBands) - 1;
   for (int cb = 0; cb < 2; cb++) {
     const int ce = 1 - cb;
     int X = -1;
@@ -1017,11 +1090,14 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
           ok = false;
           break;
         }
+        if (key.band > merge_to) key.band = uint8_t(merge_to);  // keyed coarser: fewer probes per packet
         sub[{key.axis, key.band}].push_back({key, uint32_t(xsets.size()), ent});
       }
       xsets.push_back(std::move(xs));
     }
-    if (!ok || nsoft == 0 || X < 0 || sub.size() > size_t(kIdxPerClause)) continue;
+    if (!ok || nsoft == 0 || X < 0) continue;
+    if (!mb) merge_bands(sub, xsets);
+    if (sub.size() > size_t(kIdxPerClause)) continue;
     uint64_t total = 0;
     for (auto& kv : sub)
       for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size();
@@ -2146,6 +2222,9 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       h.t[t].hard_off = append(hard_offs_[t].data(), hard_offs_[t].size(), 4);
       h.t[t].n_hard = uint32_t(hard_offs_[t].size());
     }
+    const JournalTable& jt = h.t[t];
+    if (jt.n_kinds[0] || jt.n_kinds[1] || (jt.always[0] & 0xffffffu) || (jt.always[1] & 0xffffffu) || jt.n_hard)
+      h.live |= 1u << t;
   }
   hdr_off = append(reinterpret_cast<const uint32_t*>(&h), sizeof h / 4, 16);
   return GPC_OK;

@@ -186,6 +186,25 @@ def config2(seed=RULE_SEED) -> Workload:
     return _acnp_config("C2", 50, 10, peers, svc, seed)
 
 
+def config2g(seed=RULE_SEED, n_groups=16, group_size=10000) -> Workload:
+    """C2 at the stated group size (BASELINE configs[1]: "AddressGroups of 10k pod IPs"): the same
+    1k ACNP rules over 5 tiers, but every rule's From is one of `n_groups` AddressGroups of
+    `group_size` Pod IPs drawn from the 10.0.0.0/16 Pods (10M address atoms in all). Packets: 70% of
+    sources from the /16 (a Pod of the cluster, in the rule's group about 15% of the time)."""
+    pool = np.arange(1, 65535, dtype=np.uint32) + np.uint32(int(ipaddress.ip_address("10.0.0.0")))
+    rng0 = np.random.default_rng(seed + 2)
+    groups = [[_ip(v) for v in np.sort(rng0.choice(pool, size=group_size, replace=False))] for _ in range(n_groups)]
+
+    def peers(rng):
+        return groups[int(rng.integers(0, n_groups))], (int(pool[0]) & 0xFFFF0000, 16)
+
+    def svc(rng):
+        ports = rng.choice([80, 443, 8080, 8443, 3306, 5432, 6379, 9090], size=int(rng.integers(1, 4)), replace=False)
+        return [{"protocol": "TCP", "port": int(p)} for p in ports], 6, int(ports[0]), int(ports[0])
+
+    return _acnp_config("C2g", 50, 10, peers, svc, seed, local_base="10.1.0.0")
+
+
 def _rand_block(rng):
     plen = int(rng.integers(8, 33))
     base = int(rng.integers(0, 1 << 32)) & (((1 << plen) - 1) << (32 - plen)) if plen else 0
@@ -281,7 +300,7 @@ def config4(seed=RULE_SEED) -> Workload:
     return add_services(config3(seed), 10000, 10)
 
 
-CONFIGS = {"C1": config1, "C2": config2, "C3": config3, "C4": config4}
+CONFIGS = {"C1": config1, "C2": config2, "C2g": config2g, "C3": config3, "C4": config4}
 
 
 # ------------------------------------------------------------------------------------- packets

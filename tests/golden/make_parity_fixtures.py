@@ -37,6 +37,7 @@ SPECS = {  # config -> (packets, packet seed); "x": the workload with every opti
     "C3": (100_000, 0xF1C3),
     "C4": (100_000, 0xF1C4),
     "C3x": (100_000, 0xF1C5),
+    "C2g": (100_000, 0xF1C6),  # C2 with AddressGroups of 10k Pod IPs (BASELINE configs[1] as worded)
 }
 COLS = ("src", "dst", "sport", "dport", "proto", "out_port", "len")
 OPT_COLS = ("in_port", "tun_id", "ct_src", "ct_dst", "ct_state", "dest", "ct_mark", "svc_group")
@@ -78,7 +79,7 @@ def path(config: str) -> str:
 
 def packets(config: str, wl=None):
     n, seed = SPECS[config]
-    wl = wl or workload.CONFIGS[config.rstrip("x")]()
+    wl = wl or workload.CONFIGS[config[:-1] if config.endswith("x") else config]()
     cols = workload.gen_packets(wl, n, seed=seed)
     return wl, optional_columns(cols, seed) if config.endswith("x") else cols
 
