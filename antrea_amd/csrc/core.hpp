@@ -178,6 +178,35 @@ struct TableHdr {
   // from the header (scalar loads) without reading any record; n_hfast = 0: the record loop.
   uint32_t n_hfast;
   HardFast hf[kHardFast];
+  uint32_t bits_off;  // BitTable of the table's soft rules (0: none), see below
+};
+
+// Bit-parallel tables (round 5; north_star piece 4, "clause matches as bitsets ANDed across
+// dimensions"): a table of at most kBitRules soft rules whose atoms are single (axis, value, mask)
+// terms, on at most kBitProbes distinct (axis, mask, clause) triples, with every hard rule inline.
+// Per triple a 2-choice hash maps the packet's masked value to a 32-bit rule mask -- bit i: clause
+// k of soft rule i (rank order) holds an atom with that value -- so clause k of rule i holds iff
+// bit i of the OR over its triples (or of absent[k]: the rule has no clause k) is set. completed =
+// the AND over the clauses, restricted to the rules ranked above the hard match; the best-ranked
+// completed rule is the lowest set bit, a tie a second one in its priority level. One round of
+// independent 8-B loads replaces the driver lookup, candidate scan and verification rounds.
+constexpr uint32_t kBitRules = 32, kBitProbes = 6;
+struct BitProbe {
+  uint32_t ak;    // axis | clause << 8
+  uint32_t mask;  // term mask (key = value & mask)
+  uint32_t off;   // word offset of 2^lg slots {key, rule mask} (8 B; an empty slot is {0, 0})
+  uint32_t lg;    // <= 16
+};
+struct BitTable {
+  uint32_t n_probe;
+  uint32_t absent[kMaxClauses];     // rules without clause k
+  uint32_t hard_prefix[kHardFast];  // soft rules ranked above inline hard rule h
+  uint32_t pad[2];
+  BitProbe probe[kBitProbes];
+  uint32_t info[2 * kBitRules];     // soft rule i: record offset, priority | (last index of its level + 1) << 16
+};
+struct alignas(8) BitSlot {  // {key, rule mask}: one 8-B load
+  uint32_t x, y;
 };
 
 struct ImageHdr {
@@ -261,6 +290,7 @@ GPC_HD uint64_t mix64(uint64_t x) {  // splitmix64 finalizer
   x ^= x >> 31;
   return x;
 }
+GPC_HD uint32_t bit_hash(uint32_t q, uint32_t key) { return mix32(key ^ (q * 0x9e3779b1u + 0x51ed270bu)); }  // BitTable slots
 GPC_HD uint32_t proto_class(uint32_t proto) {
   switch (proto) {
     case 6: return 1;
@@ -1222,6 +1252,63 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     }
   }
   GPC_MARK(ST_DRV);
+  if (th.bits_off && !im.dead) {  // bit-parallel table (tombstones: the scan below honours them)
+    const BitTable& bt = *reinterpret_cast<const BitTable*>(im.blob + th.bits_off);
+    uint32_t s0 = bt.absent[0], s1 = bt.absent[1], s2 = bt.absent[2];
+    const uint32_t np = bt.n_probe;
+    constexpr uint32_t kBatch = 3;  // probes whose slot loads are in flight together (register budget)
+#pragma unroll
+    for (uint32_t q0 = 0; q0 < kBitProbes; q0 += kBatch) {
+      if (q0 >= np) break;
+      BitSlot c1[kBatch], c2[kBatch];
+      uint32_t key[kBatch];
+#pragma unroll
+      for (uint32_t j = 0; j < kBatch; j++) {  // every slot load of the batch issued before any is used
+        const uint32_t q = q0 + j;
+        key[j] = 0;
+        c1[j] = c2[j] = BitSlot{1u, 0u};
+        if (q < np) {
+          const BitProbe pr = bt.probe[q];
+          key[j] = p.ax[pr.ak & 15u] & pr.mask;
+          const uint32_t h = bit_hash(q, key[j]), m = (1u << pr.lg) - 1u;
+          const BitSlot* sl = reinterpret_cast<const BitSlot*>(im.blob + pr.off);
+          GPC_TOUCH(sl + (h & m), 8);
+          GPC_TOUCH(sl + ((h >> 16) & m), 8);
+          c1[j] = sl[h & m];
+          c2[j] = sl[(h >> 16) & m];
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kBatch; j++) {
+        const uint32_t q = q0 + j;
+        if (q < np) {
+          const uint32_t k = bt.probe[q].ak >> 8;
+          const uint32_t v = (c1[j].x == key[j] ? c1[j].y : 0u) | (c2[j].x == key[j] ? c2[j].y : 0u);
+          s0 |= k == 0 ? v : 0u;
+          s1 |= k == 1 ? v : 0u;
+          s2 |= k == 2 ? v : 0u;
+        }
+      }
+    }
+    uint32_t done = s0 & s1 & s2;
+    if (rH != th.end_off) {  // only rules ranked above the hard match
+      const uint32_t np_ = rH == th.hf[0].roff ? bt.hard_prefix[0] : bt.hard_prefix[1];
+      done &= np_ >= 32u ? 0xffffffffu : (1u << np_) - 1u;
+    }
+    if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
+    if (done) {
+      const uint32_t w = uint32_t(__builtin_ctz(done));
+      GPC_TOUCH(&bt.info[2 * w], 8);
+      uint32_t roff, pe;
+      load_pair(&bt.info[2 * w], &roff, &pe);
+      const uint32_t end = pe >> 16;  // rules w + 1 .. end - 1 share w's priority
+      const uint32_t later = end >= 32u ? 0xffffffffu : (1u << end) - 1u;
+      const bool tie = (done & later & ~((2u << w) - 1u)) != 0u;
+      res.s = (pe & 0xffffu) | kSHave | (tie ? kSTie : 0u);
+      res.win = roff;
+    }
+    return res;
+  }
   const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
   if (th.n_cidx == 0 && n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
     if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;

@@ -944,6 +944,101 @@ bool build_hash(const std::vector<uint64_t>& keys, uint32_t* log2_out, std::vect
   return false;
 }
 
+// Bit-parallel table (core.hpp BitTable): built when the table has 1..kBitRules soft rules, all with
+// conj_id action flows, whose atoms are single terms on at most kBitProbes (axis, mask, clause)
+// triples, and every hard rule is inline. The driver indexes stay (delta epochs with tombstones
+// scan them). GPC_NO_BITSET=1 turns it off.
+void build_bits(const std::vector<RuleB*>& rs, const std::vector<uint32_t>& rec_off, TableHdr& th, Blob& B) {
+  th.bits_off = 0;
+  if (std::getenv("GPC_NO_BITSET")) return;
+  if (th.n_hard != th.n_hfast) return;
+  std::vector<size_t> soft;  // rank indexes of the soft rules
+  std::vector<uint32_t> hard_prefix;
+  for (size_t r = 0; r < rs.size(); r++) {
+    if (rs[r]->hard) hard_prefix.push_back(uint32_t(soft.size()));
+    else soft.push_back(r);
+  }
+  if (soft.empty() || soft.size() > kBitRules || hard_prefix.size() > kHardFast) return;
+  BitTable bt{};
+  std::map<std::array<uint32_t, 3>, std::map<uint32_t, uint32_t>> probes;  // (axis, mask, clause) -> key -> rule mask
+  for (size_t i = 0; i < soft.size(); i++) {
+    const RuleB& r = *rs[soft[i]];
+    if (!r.has_act) return;
+    for (int k = 0; k < kMaxClauses; k++) {
+      if (k >= r.n) {
+        bt.absent[k] |= 1u << i;
+        continue;
+      }
+      for (const Atom& a : r.clause[k]) {
+        if (a.t.size() != 1 || a.t[0].axis >= AX_N) return;
+        const Term& t = a.t[0];
+        probes[{t.axis, t.mask, uint32_t(k)}][t.val & t.mask] |= 1u << i;
+      }
+    }
+  }
+  if (probes.empty() || probes.size() > kBitProbes) return;
+  for (size_t h = 0; h < hard_prefix.size(); h++) bt.hard_prefix[h] = hard_prefix[h];
+  for (size_t i = 0; i < soft.size(); i++) {
+    size_t end = i + 1;
+    while (end < soft.size() && rs[soft[end]]->prio == rs[soft[i]]->prio) end++;
+    bt.info[2 * i] = rec_off[soft[i]];
+    bt.info[2 * i + 1] = uint32_t(rs[soft[i]]->prio) | (uint32_t(end) << 16);
+  }
+  uint32_t q = 0;
+  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> tabs;  // (probe, slots) emitted after the header
+  for (auto& kv : probes) {
+    const auto& keys = kv.second;
+    uint32_t lg = 4;
+    while ((uint64_t(1) << lg) < 2 * keys.size()) lg++;
+    bool placed_all = false;
+    std::vector<uint32_t> slots;
+    for (; lg <= 16 && !placed_all; lg++) {
+      const uint32_t m = (1u << lg) - 1u;
+      slots.assign(size_t(2) << lg, 0u);
+      std::vector<bool> used(size_t(1) << lg, false);
+      placed_all = true;
+      std::mt19937 rng(7 + lg);
+      for (auto& e : keys) {
+        uint32_t key = e.first, val = e.second;
+        bool done = false;
+        for (int kick = 0; kick < 500 && !done; kick++) {
+          const uint32_t h = bit_hash(q, key), b[2] = {h & m, (h >> 16) & m};
+          for (uint32_t bb : b)
+            if (!used[bb]) {
+              used[bb] = true;
+              slots[2 * bb] = key;
+              slots[2 * bb + 1] = val;
+              done = true;
+              break;
+            }
+          if (done) break;
+          const uint32_t v = b[rng() & 1];  // evict and re-place the resident
+          std::swap(key, slots[2 * v]);
+          std::swap(val, slots[2 * v + 1]);
+        }
+        if (!done) {
+          placed_all = false;
+          break;
+        }
+      }
+      if (placed_all) break;
+    }
+    if (!placed_all) return;
+    // an empty slot {0, 0} whose key equals a packet's masked value contributes no rule bit
+    BitProbe& pr = bt.probe[q];
+    pr.ak = kv.first[0] | (kv.first[2] << 8);
+    pr.mask = kv.first[1];
+    pr.lg = lg;
+    tabs.push_back({q, std::move(slots)});
+    q++;
+  }
+  bt.n_probe = q;
+  for (auto& tb : tabs) bt.probe[tb.first].off = B.put(tb.second.data(), tb.second.size(), 16);
+  th.bits_off = B.put(reinterpret_cast<const uint32_t*>(&bt), sizeof bt / 4, 16);
+  if (std::getenv("GPC_IMAGE_DEBUG"))
+    std::fprintf(stderr, "bit-parallel table: %zu soft rules, %u probes\n", soft.size(), bt.n_probe);
+}
+
 // Composite driver (core.hpp TableHdr cidx): built when every soft rule of the table has, in clause
 // 1 - cb, at most kCompositeMaxValues exact values on one common axis (AppliedTo ofports, Pod IPs)
 // and, in clause cb, only IP atoms the driver index can key. Each rule is listed under (band key,
@@ -2415,6 +2510,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
       th.n_hfast = uint32_t(hard_fast.size());
       for (size_t h = 0; h < hard_fast.size(); h++) th.hf[h] = hard_fast[h];
     }
+    build_bits(rs, rec_off, th, B);
     if (std::getenv("GPC_IMAGE_DEBUG"))
       std::fprintf(stderr, "table %d: %zu rules, %u hard (%u inline)\n", t, rs.size(), th.n_hard, th.n_hfast);
     T_.lap(1);

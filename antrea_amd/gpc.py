@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import ipaddress
+import socket
 import os
 from typing import Dict, List, Optional
 
@@ -218,6 +219,10 @@ def _check(rc, what):
 
 
 # ------------------------------------------------------------------------------ marshalling
+_ADDR_NP = np.dtype([("kind", "u1"), ("family", "u1"), ("prefix_len", "u1"), ("reserved", "u1"), ("value", "<u4"),
+                     ("ip", "u1", 16)])  # gpc_addr
+
+
 def _addr(a) -> gpc_addr:
     out = gpc_addr()
     if isinstance(a, str):
@@ -297,9 +302,19 @@ class RuleBuf:
     def _addrs(self, lst):
         if lst is None:
             return -1, None
-        arr = (gpc_addr * max(1, len(lst)))(*[_addr(a) for a in lst])
+        n = len(lst)
+        if n >= 64 and all(type(a) is str and a.count(".") == 3 and "/" not in a for a in lst):
+            # large lists of IPv4 Pod addresses (AddressGroups): filled as one numpy record array
+            # in gpc_addr's layout, the dotted quads parsed by inet_aton (C) instead of ipaddress
+            buf = np.zeros(n, dtype=_ADDR_NP)
+            buf["kind"] = ADDR_KINDS["ip"]
+            buf["family"] = 4
+            buf["ip"][:, :4] = np.frombuffer(b"".join(socket.inet_aton(a) for a in lst), np.uint8).reshape(n, 4)
+            self.keep.append(buf)
+            return n, (gpc_addr * n).from_buffer(buf)
+        arr = (gpc_addr * max(1, n))(*[_addr(a) for a in lst])
         self.keep.append(arr)
-        return len(lst), arr
+        return n, arr
 
     def _fill(self, g: gpc_rule, r: dict):
         g.direction = 1 if r["direction"] == "Out" else 0

@@ -74,6 +74,22 @@ def test_device_vs_oracle_fullscale(config, group):
     assert {1, 2} <= acts and (3 in acts or 5 in acts), acts
 
 
+def test_device_vs_oracle_c2g():
+    """BASELINE configs[1] as worded: 1k ACNP rules whose From clauses are
+    AddressGroups of 10k Pod IPs each (16 groups over the 10.0.0.0/16 Pods, 10M conjunctive match
+    flows). Verdicts and metrics of 100k packets equal the C oracle's (fixture built from the
+    oracle compiler's 10M flows, tests/golden/parity_C2g.npz)."""
+    f, wl, cols = _inputs("C2g")
+    c = _classifier(wl)
+    assert c.image_stats()["n_flows"] > 10_000_000
+    got = c.classify_host(cols, count=True)
+    res = parity.compare(got, f["verdicts"])
+    assert res["mismatches"] == 0, res
+    assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
+    acts = set(int(a) for a in np.unique(got["action"]))
+    assert {1, 2, 3} <= acts, acts
+
+
 @pytest.mark.parametrize("config", ["C2", "C3"])
 def test_device_vs_oracle_fullscale_plain_driver(config, monkeypatch):
     """The same parity with the composite driver index turned off (GPC_COMPOSITE=0, read at image

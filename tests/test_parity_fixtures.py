@@ -18,7 +18,7 @@ from tests import emu
 from tests.golden import make_parity_fixtures as fx
 
 
-@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4", "C3x"])
+@pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4", "C3x", "C2g"])
 def test_fixture_inputs_stable(config):
     f = fx.load(config)
     wl, cols = fx.packets(config)
