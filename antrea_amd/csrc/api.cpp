@@ -325,9 +325,8 @@ static void lane_sort_tables(const HostImage& h, uint8_t* sort_table) {
       double s1 = th.always_n[th.cband], s2 = s1 * s1;
       for (uint32_t i = 0; i < th.n_cidx; i++) {
         const SubIdx& si = th.cidx[i];
-        const uint32_t* o = h.blob.data() + si.off;
         for (uint64_t b = 0; b < (1ull << si.bits); b++) {
-          const double len = double(o[b + 1] - o[b]);
+          const double len = double(sub_bucket_len(h.blob.data(), si, uint32_t(b)));
           s1 += len;
           s2 += len * len;
         }

@@ -134,14 +134,23 @@ constexpr uint32_t kEntExactX = 1u << 31;
 GPC_HD uint32_t ent_off(uint32_t x) { return ((x & ~kEntExactX) >> 8) << 4; }
 
 struct SubIdx {  // one (axis, band) bucket index of a driver clause
-  uint8_t axis, band, bits, reserved;
-  uint32_t off;   // word offset of 2^bits + 1 bucket offsets (in entries, relative to `ent`)
+  uint8_t axis, band, bits, fmt;
+  uint32_t off;   // fmt 0: word offset of 2^bits + 1 bucket offsets (in entries, relative to `ent`);
+                  // fmt 1 (composite sub-indexes, round 5): word offset of the bucket directory
   uint32_t ent;   // word offset (multiple of 4) of the Ent entries, ascending record offset per bucket
-  uint32_t pres;  // composite sub-indexes: word offset of a 2^bits-bit map of the non-empty buckets
-                  // (0: none). It is small enough to stay in L2 (C3: 256 KB per sub-index) and most
-                  // buckets are empty (C3: 72-81 %), so the offset pair -- a random line of a
-                  // 25 MB array -- is fetched only for the ~1/4 of the probes that can list a rule.
+  uint32_t pres;  // fmt 0 composite sub-indexes: word offset of a 2^bits-bit map of the non-empty
+                  // buckets (0: none): the offset pair -- a random line of a 25 MB array -- is
+                  // fetched only for the probes that can list a rule.
 };
+// Bucket directory (SubIdx fmt 1, round 5): per 32 buckets one 16-B block {count bit 0, count bit 1,
+// count bit 2, first entry}: bucket b's list starts at first + the counts of the block's earlier
+// buckets (three popcounts) and holds its 3-bit count of entries. So one load -- a line of an array
+// 1/8 the size of the offset pairs it replaces (C3: ~1 MB per table, L2-resident) -- settles both
+// "empty?" and "where", and a probe of a non-empty bucket costs one line miss (its entries) instead
+// of two (offset pair, then entries). Count 7: the bucket's first slot is a pointer entry
+// {0, overflow index, count, 0} to a list kept after the main entries (lists of 7 or more rules
+// under one (key, value): a rare, second dependent load). A zero entry is inert in the scan.
+constexpr uint32_t kDirCountMax = 7;  // dir_list below
 
 // An inline hard pseudo-rule (TableHdr.hf): its record's fast descriptors, plus the two (value,
 // mask) terms of an FK_MK2 clause (two single-term boxes, e.g. the ct_state bypass flows
@@ -375,6 +384,30 @@ extern "C" void gpc_emu_touch(const void* p, unsigned bytes, int line);
 #define GPC_TOUCH(p, n) ((void)0)
 #endif
 
+// core.hpp SubIdx fmt 1: bucket b's entry range [lo, hi) from its directory block
+GPC_HD void dir_list(const uint32_t* blob, const SubIdx& si, uint32_t b, uint32_t* lo, uint32_t* hi) {
+  const uint32_t* d = blob + si.off + 4u * (b >> 5);
+  GPC_TOUCH(d, 16);
+#if defined(__HIPCC__)
+  const uint4 q = *reinterpret_cast<const uint4*>(d);
+#else
+  const struct { uint32_t x, y, z, w; } q = {d[0], d[1], d[2], d[3]};
+#endif
+  const uint32_t sh = b & 31u, m = (1u << sh) - 1u;
+  const uint32_t c = ((q.x >> sh) & 1u) | (((q.y >> sh) & 1u) << 1) | (((q.z >> sh) & 1u) << 2);
+  const uint32_t start = q.w + uint32_t(__builtin_popcount(q.x & m)) + 2u * uint32_t(__builtin_popcount(q.y & m)) +
+                         4u * uint32_t(__builtin_popcount(q.z & m));
+  *lo = si.ent / 4u + start;
+  *hi = *lo + c;
+}
+// Entries listed under bucket b of a sub-index (either format; host statistics).
+GPC_HD uint32_t sub_bucket_len(const uint32_t* blob, const SubIdx& si, uint32_t b) {
+  if (!si.fmt) return blob[si.off + b + 1] - blob[si.off + b];
+  uint32_t lo, hi;
+  dir_list(blob, si, b, &lo, &hi);
+  return hi - lo == kDirCountMax ? blob[4 * lo + 2] : hi - lo;
+}
+
 // Region stamps (diagnostic builds only, -DGPC_STAMPS; tools/stamps.py): from GPC_MARK(r) on, the
 // wave's s_memtime cycles are charged to region r; the kernel adds each wave's totals to
 // gpc_stamp_acc. Never defined in the product build.
@@ -436,28 +469,37 @@ struct V6Len {
 GPC_HD uint32_t v6_len(const V6Len& d) { return d.meta & 0xffu; }
 GPC_HD uint32_t v6_kw(const V6Len& d) { return (d.meta >> 8) & 0xffu; }
 GPC_HD uint32_t v6_log2(const V6Len& d) { return d.meta >> 16; }
+constexpr uint32_t kV6MaxTags = 16;
 struct V6Lpm {
   uint32_t n_lens;
-  uint32_t l1_off;            // region table (0: none): 2^16 entries of 4 words, see v6_codes
-  uint32_t l1_c;              // its tag length c: regions are the /c+16 blocks under the tag
-  uint32_t reserved;
+  uint32_t l1_off;            // region tables (0: none): per tag 2^16 entries of 4 words, see v6_codes
+  uint32_t l1_c;              // the tag length c: regions are the /c+16 blocks under a tag
+  uint32_t n_tags;            // tags (1..kV6MaxTags) with a region table each, in l1_tag order
   uint32_t lens[kV6MaxLens];  // distinct prefix lengths of the tree (root excluded), ascending
   V6Len d[kV6MaxLens];        // d[i]: the table of lens[i]
-  uint32_t l1_tag[4];         // the top c bits every prefix shares, right-aligned (v6_key(a, c))
+  uint32_t l1_tag[kV6MaxTags][4];  // the top c bits of the prefixes of length >= c, right-aligned (v6_key(a, c))
 };
-// Region table (image.cpp build_image6): when every prefix of the tree lies under one /c (C3 in
-// fd00:10::/96: c = 96), an address under it is first looked up by its next 16 bits (one 16-B load,
-// a 1-MB table): entry {code of the deepest prefix no longer than c + 16 holding the region,
+// Region tables (image.cpp build_image6): when every prefix of the tree no shorter than c lies under
+// one of at most kV6MaxTags /c blocks (the tags; C3 in fd00:10::/96: one tag, c = 96; rule sets over
+// several /48s: c = 48, a tag per /48), an address under a tag is first looked up by its next 16
+// bits in that tag's table (one 16-B load, 1 MB per tag; shorter prefixes are folded into the
+// entries as region bases): entry {code of the deepest prefix no longer than c + 16 holding the region,
 // number n of the lengths longer than c + 16 present in the region | kV6L1Global, the indexes of
 // those lengths, 8 bits each}; the binary search then runs over those n lengths only (regional
 // markers are in the per-length tables; a marker carries the best match at its length whatever
 // search tree placed it, so extra markers never mislead the global search). kV6L1Global: more
 // than 8 lengths, search them all.
 constexpr uint32_t kV6L1Bits = 16, kV6L1Global = 16u, kV6L1MaxLens = 8;
-// Bucket: two slots; slot = key (kw words), code, padding to 2 / 4 / 8 words: 16 / 32 / 64-B buckets.
+// Bucket (kw 2 / 4): two slots; slot = key (kw words), code, padding to 4 / 8 words: 32 / 64-B
+// buckets, both choices loaded in one step. kw = 1 (round 5, "line buckets"): one 64-B line per
+// bucket -- word 0 a flag (some key whose first choice is this bucket lives in its second choice),
+// then 7 slots {key, code} -- so a step reads the first choice's line only, and the second choice
+// only where the flag says a key may be there (rare: the builder places keys in their first choice
+// whenever it has room). Halves the lines a step reads (C3 in IPv6: every table is kw = 1).
 constexpr uint32_t kV6BucketWords = 16;  // the largest bucket (and the overflow table's)
+constexpr uint32_t kV6LineSlots = 7;
 GPC_HD uint32_t v6_slot_words(uint32_t kw) { return kw == 4u ? 8u : 2u * kw; }
-GPC_HD uint32_t v6_bucket_words(uint32_t kw) { return 2u * v6_slot_words(kw); }
+GPC_HD uint32_t v6_bucket_words(uint32_t kw) { return kw == 1u ? 16u : 2u * v6_slot_words(kw); }
 // Wide slot of the delta epochs' overflow table (journal): masked address (4 words), len | kV6Valid,
 // code, 2 pad; 2 slots per 64-B bucket, two choices.
 constexpr uint32_t kV6SlotWords = 8, kV6BucketSlots = 2, kV6Valid = 0x100u;
@@ -528,11 +570,11 @@ GPC_HD bool v6_probe_needed(const V6Len& d, const uint32_t* r) {
 // (no data-dependent slot index, which the compiler would turn into a private-memory array).
 GPC_HD bool v6_bucket_find(const uint32_t* w, uint32_t kw, const uint32_t* r, uint32_t* code) {
   uint32_t c = 0, any = 0;
-  if (kw == 1u) {
+  if (kw == 1u) {  // a line bucket: flag word, then kV6LineSlots slots
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const uint32_t mt = 0u - uint32_t(w[2 * s] == r[3]);
-      c |= w[2 * s + 1] & mt;
+    for (uint32_t s = 0; s < kV6LineSlots; s++) {
+      const uint32_t mt = 0u - uint32_t(w[1 + 2 * s] == r[3]);
+      c |= w[2 + 2 * s] & mt;
       any |= mt;
     }
   } else if (kw == 2u) {
@@ -608,9 +650,13 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       const uint32_t c = L->l1_c;
       uint32_t t[4] = {0u, 0u, 0u, 0u}, x[4];
       if (c) v6_key(a[k], c, t);
-      if (t[0] == L->l1_tag[0] && t[1] == L->l1_tag[1] && t[2] == L->l1_tag[2] && t[3] == L->l1_tag[3]) {
+      uint32_t ti = 0xffffffffu;  // the address's tag (uniform loop over the few tags, scalar operands)
+      for (uint32_t j = 0; j < L->n_tags; j++)
+        if (t[0] == L->l1_tag[j][0] && t[1] == L->l1_tag[j][1] && t[2] == L->l1_tag[j][2] && t[3] == L->l1_tag[j][3])
+          ti = j;
+      if (ti != 0xffffffffu) {
         v6_key(a[k], c + kV6L1Bits, x);
-        const uint32_t* e = blob + L->l1_off + 4 * size_t(x[3] & ((1u << kV6L1Bits) - 1u));
+        const uint32_t* e = blob + L->l1_off + (size_t(ti) << (kV6L1Bits + 2)) + 4 * size_t(x[3] & ((1u << kV6L1Bits) - 1u));
         GPC_TOUCH(e, 16);
 #if defined(__HIPCC__)
         const uint4 ev = *reinterpret_cast<const uint4*>(e);
@@ -631,7 +677,9 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
 #pragma unroll
     for (int k = 0; k < K; k++) any |= lo[k] <= hi[k];
     if (!any) break;
+    GPC_STAT(11, 1);  // dependent search rounds of the K-address group
     uint32_t r[K][4], kw[K], w[K][2][kV6BucketWords];
+    const uint32_t* b2[K];  // the second choice's bucket (line buckets: loaded only when flagged)
     bool probe[K];
     uint32_t m[K][kOvf ? 4 : 1], len[K], ow[K][kOvf ? 2 : 1][kOvf ? kV6BucketWords : 1];
 #pragma unroll
@@ -646,11 +694,12 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       probe[k] = live && v6_probe_needed(d, r[k]);
       uint32_t bk[2];
       v6_buckets(d, r[k], &bk[0], &bk[1]);
+      b2[k] = blob + d.tab_off + size_t(bk[1]) * v6_bucket_words(kw[k]);
 #pragma unroll
       for (int c = 0; c < 2; c++) {
         const uint32_t bw = v6_bucket_words(kw[k]);
         const uint32_t* b = blob + d.tab_off + size_t(bk[c]) * bw;
-        if (probe[k]) {
+        if (probe[k] && (c == 0 || kw[k] != 1u)) {  // line buckets: the first choice only
           GPC_TOUCH(b, bw * 4);
           v6_load_bucket(b, bw, w[k][c]);
         }
@@ -672,7 +721,15 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       bool hit = false;
       if (probe[k]) {
         hit = v6_bucket_find(w[k][0], kw[k], r[k], &code[k]);
-        hit = v6_bucket_find(w[k][1], kw[k], r[k], &code[k]) || hit;
+        if (kw[k] != 1u) {
+          hit = v6_bucket_find(w[k][1], kw[k], r[k], &code[k]) || hit;
+        } else if (GPC_WAVE_ANY(!hit && w[k][0][0] != 0u)) {  // flagged line bucket: the second choice
+          if (!hit && w[k][0][0] != 0u) {
+            GPC_TOUCH(b2[k], 64);
+            v6_load_bucket(b2[k], 16u, w[k][1]);
+            hit = v6_bucket_find(w[k][1], 1u, r[k], &code[k]);
+          }
+        }
       }
       if constexpr (kOvf) {
         hit = v6_wide_find(ow[k][0], m[k], len[k], &code[k]) || hit;
@@ -1105,9 +1162,8 @@ GPC_HD uint32_t scan_estimate(const Img& im, uint32_t table, const Pkt& p) {
     uint32_t c = th.always_n[th.cband];
     for (uint32_t i = 0; i < th.n_cidx && i < uint32_t(kIdxPerClause); i++) {
       const SubIdx& si = th.cidx[i];
-      uint32_t ob, oe;
-      load_pair(im.blob + si.off + cbucket_of(si.band, si.bits, p.ax[si.axis], p.ax[th.cx]), &ob, &oe);
-      c += oe - ob;
+      const uint32_t bk = cbucket_of(si.band, si.bits, p.ax[si.axis], p.ax[th.cx]);
+      c += sub_bucket_len(im.blob, si, bk);
     }
     return c;
   }
@@ -1329,6 +1385,49 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     const bool xin = (im.blob[th.xmap_off + (xb >> 5)] >> (xb & 31u)) & 1u;  // else no soft rule can match
     always_n = xin ? th.always_n[d] : 0u;
     uint32_t cnt = always_n;
+    if (th.cidx[0].fmt) {
+      // bucket directories: one 16-B block per sub-index (and a pointer entry where a bucket
+      // overflowed), read in the value-map word's round (fmt 1) or, where the map filters most
+      // packets, only for the packets in it (fmt 2). The branch is wave-uniform, so the fmt-1 loads
+      // do not wait for the map word.
+      bool ovf = false;
+#pragma unroll
+      for (int i = 0; i < kIdxPerClause; i++) lo0[i] = hi0[i] = lo1[i] = hi1[i] = 0;
+      if (th.cidx[0].fmt == 1) {
+#pragma unroll
+        for (int i = 0; i < kIdxPerClause; i++)
+          if (uint32_t(i) < nc) {
+            const SubIdx& si = th.cidx[i];
+            dir_list(im.blob, si, cbucket_of(si.band, si.bits, p.ax[si.axis], xv), &lo0[i], &hi0[i]);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kIdxPerClause; i++)
+          if ((uint32_t(i) < nc) & xin) {
+            const SubIdx& si = th.cidx[i];
+            dir_list(im.blob, si, cbucket_of(si.band, si.bits, p.ax[si.axis], xv), &lo0[i], &hi0[i]);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < kIdxPerClause; i++) {
+        if (!xin) hi0[i] = lo0[i];
+        ovf = ovf | (hi0[i] - lo0[i] == kDirCountMax);
+      }
+      if (GPC_WAVE_ANY(ovf)) {
+        const Ent* E = reinterpret_cast<const Ent*>(im.blob);
+#pragma unroll
+        for (int i = 0; i < kIdxPerClause; i++) {
+          if ((uint32_t(i) < nc) && hi0[i] - lo0[i] == kDirCountMax) {
+            GPC_TOUCH(&E[lo0[i]], 16);
+            const Ent pe = E[lo0[i]];
+            lo0[i] = th.cidx[i].ent / 4u + pe.y;
+            hi0[i] = lo0[i] + pe.lo;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kIdxPerClause; i++) cnt += hi0[i] - lo0[i];
+    } else {
     // presence words (L2-resident) are read in the value-map word's round; an offset pair only
     // for a present bucket of a packet whose value is in the map
     uint32_t bk[kIdxPerClause], pw[kIdxPerClause];
@@ -1359,6 +1458,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
         hi0[i] = si.ent / 4 + oe;
         cnt += hi0[i] - lo0[i];
       }
+    }
     }
     GPC_STAT(0, 1);
     GPC_STAT(1, cnt);

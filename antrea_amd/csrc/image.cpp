@@ -1060,6 +1060,7 @@ constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 24;  // 256 MB of entri
 // 29.2 with m = 3 [29-34], 73.5 with m = 1; C1 (0.08 MB image) 5.80 unmerged, 7.38 with m = 3 [3-4],
 // 8.07 with m = 0.
 constexpr double kMergeListMax = 16.0;
+constexpr uint32_t kV6DefaultTags = 4;
 constexpr uint64_t kMergeMinBytes = uint64_t(16) << 20;
 template <typename CE>
 void merge_bands(std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>>& sub, const std::vector<std::vector<uint32_t>>& xsets) {
@@ -1203,6 +1204,11 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     // GPC_COMPOSITE_EXTRA_BITS overrides (experiments)
     const char* xe = std::getenv("GPC_COMPOSITE_EXTRA_BITS");
     const uint32_t extra = xe ? uint32_t(std::min(3, std::max(0, std::atoi(xe)))) : 1u;
+    // core.hpp SubIdx fmt: bucket directories (1: read in the value-map word's round, where the map
+    // cannot filter -- an exact non-IP value axis; 2: after it, an IP value axis). GPC_COMPOSITE_DIR
+    // overrides (experiments): 0 = offset pairs (+ presence maps), 1 or 2 for every table
+    const char* de = std::getenv("GPC_COMPOSITE_DIR");
+    const int dir_fmt = de ? std::min(2, std::max(0, std::atoi(de))) : (X > AX_CTDST ? 1 : 2);
     for (auto& kv : sub) {
       const uint8_t axis = kv.first.first, band = kv.first.second;
       uint64_t n = 0;
@@ -1227,14 +1233,50 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       ents.reserve(4 * be.size());
       for (auto& e : be) offs[e.first + 1]++;
       for (uint32_t b = 0; b < nb; b++) offs[b + 1] += offs[b];
-      for (auto& e : be) ents.insert(ents.end(), e.second.begin(), e.second.end());
       SubIdx& si = th.cidx[th.n_cidx++];
       si.axis = axis;
       si.band = band;
       si.bits = uint8_t(bits);
+      si.pres = 0;
+      si.fmt = uint8_t(dir_fmt);
+      if (dir_fmt) {
+        // core.hpp dir_list: a 16-B block per 32 buckets; lists of kDirCountMax or more entries
+        // move behind the main ones, their bucket holding a pointer entry and 6 inert zero entries
+        std::vector<uint32_t> dir(size_t(nb) / 8, 0u), ovf;
+        uint32_t main_n = 0;
+        for (uint32_t b = 0; b < nb; b++)
+          main_n += std::min(offs[b + 1] - offs[b], kDirCountMax);
+        ents.assign(size_t(4) * main_n, 0u);
+        uint32_t slot = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+          uint32_t* d = &dir[4 * (b >> 5)];
+          if ((b & 31u) == 0) d[3] = slot;
+          const uint32_t n = offs[b + 1] - offs[b], c = std::min(n, kDirCountMax);
+          for (int k = 0; k < 3; k++) d[k] |= ((c >> k) & 1u) << (b & 31u);
+          if (n < kDirCountMax) {
+            for (uint32_t e = offs[b]; e < offs[b + 1]; e++, slot++)
+              std::copy(be[e].second.begin(), be[e].second.end(), &ents[4 * size_t(slot)]);
+          } else {
+            const uint32_t at = main_n + uint32_t(ovf.size() / 4);
+            ents[4 * size_t(slot) + 1] = at;  // {0, overflow index, count, 0}
+            ents[4 * size_t(slot) + 2] = n;
+            slot += kDirCountMax;
+            for (uint32_t e = offs[b]; e < offs[b + 1]; e++) ovf.insert(ovf.end(), be[e].second.begin(), be[e].second.end());
+          }
+        }
+        ents.insert(ents.end(), ovf.begin(), ovf.end());
+        si.off = B.put(dir.data(), dir.size(), 16);
+        si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
+        out->bytes_bucket_offsets += 4ull * dir.size();
+        out->bytes_entries += 4ull * ents.size();
+        if (std::getenv("GPC_IMAGE_DEBUG"))
+          std::fprintf(stderr, "table %d composite clause %d x axis %d: axis %u band %u bits %u entries %zu dir fmt %d (%zu overflow)\n",
+                       t, cb, X, axis, band, bits, be.size(), dir_fmt, ovf.size() / 4);
+        continue;
+      }
+      for (auto& e : be) ents.insert(ents.end(), e.second.begin(), e.second.end());
       si.off = B.put(offs.data(), offs.size(), 16);
       si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
-      si.pres = 0;
       // core.hpp SubIdx.pres, where the value map cannot filter and several bands are probed: an
       // exact non-IP axis (AppliedTo ofports: every ingress packet goes to a local Pod, so its value
       // is always in the map) with >= 2 sub-indexes. With an IP value axis (egress: the Pod IPs) the
@@ -1497,6 +1539,48 @@ static bool v6_hash_build(const std::vector<std::array<uint32_t, 8>>& slots6, do
 // Key words kw = the fewest of 1 / 2 / 4 whose complement (the tag) all entries share; the empty-slot
 // key is one no entry has. 2-choice cuckoo placement over buckets of two slots, a larger table when
 // it does not converge. Fills d (except tab_off) and tab.
+// kw = 1: line buckets (core.hpp kV6LineSlots): each key in its first choice while that has room,
+// else in its second choice with the first one's flag set; the table doubles until every key fits.
+static bool v6_line_table_build(uint32_t len, const std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>& ents,
+                                V6Len* d, std::vector<uint32_t>* tab) {
+  std::set<uint32_t> used;
+  for (auto& e : ents) used.insert(e.first[3]);
+  uint32_t empty = ~0u;
+  while (used.count(empty)) empty--;
+  for (uint32_t w = 0; w < 3; w++) d->pat[w] = ents.empty() ? 0u : ents[0].first[w];
+  d->pat[3] = empty;
+  d->seed = v6_seed(len, 1, d->pat);
+  uint32_t lg = 0;
+  while (double(kV6LineSlots << lg) * 0.4 < double(ents.size() + 1)) lg++;
+  for (int attempt = 0; attempt < 8; attempt++, lg++) {
+    const uint32_t nb = 1u << lg;
+    d->meta = len | 1u << 8 | lg << 16;
+    tab->assign(size_t(nb) * 16, 0u);
+    std::vector<uint8_t> n_in(nb, 0);
+    for (size_t b = 0; b < nb; b++)
+      for (uint32_t s = 0; s < kV6LineSlots; s++) (*tab)[b * 16 + 1 + 2 * s] = empty;
+    bool ok = true;
+    for (size_t n = 0; n < ents.size() && ok; n++) {
+      uint32_t bs[2];
+      v6_buckets(*d, ents[n].first.data(), &bs[0], &bs[1]);
+      uint32_t b = bs[0];
+      if (n_in[b] >= kV6LineSlots) {
+        (*tab)[size_t(bs[0]) * 16] = 1u;  // flag: look at the second choice too
+        b = bs[1];
+      }
+      if (n_in[b] >= kV6LineSlots) {
+        ok = false;
+        break;
+      }
+      (*tab)[size_t(b) * 16 + 1 + 2 * n_in[b]] = ents[n].first[3];
+      (*tab)[size_t(b) * 16 + 2 + 2 * n_in[b]] = ents[n].second;
+      n_in[b]++;
+    }
+    if (ok) return true;
+  }
+  return false;
+}
+
 static bool v6_len_table_build(uint32_t len, const std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>& ents,
                                V6Len* d, std::vector<uint32_t>* tab) {
   *d = V6Len{};
@@ -1510,6 +1594,7 @@ static bool v6_len_table_build(uint32_t len, const std::vector<std::pair<std::ar
       break;
     }
   }
+  if (kw == 1u) return v6_line_table_build(len, ents, d, tab);
   const uint32_t sw = v6_slot_words(kw), ns = 2, bw = v6_bucket_words(kw);
   std::set<std::array<uint32_t, 4>> used;
   for (auto& e : ents) {
@@ -1619,54 +1704,77 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
       lo = mid + 1;
     }
   }
-  // Region table (core.hpp kV6L1Bits): when all prefixes share their top c bits (c <= the shortest
-  // length, c + 16 <= 128), every /c+16 region gets the best match no longer than c + 16 and the
-  // list of longer lengths present under it, plus the markers of that shorter search.
+  // Region tables (core.hpp kV6L1Bits): the tag length c is the longest (c + 16 <= 128) at which the
+  // prefixes no shorter than c fall under at most kV6DefaultTags distinct /c blocks (GPC_V6_MAX_TAGS:
+  // 1..kV6MaxTags). More tags mean finer regions (shorter searches) and more region-table bytes:
+  // C3 in IPv6 (64M packets, profiles/r05j) code launch 3.90 ms with one tag (c = 96), 3.26 ms with
+  // four (c = 98), 3.46 ms with sixteen (c = 100). Per tag, every /c+16 region gets the best match no longer than c + 16 (prefixes
+  // shorter than c cover whole tags) and the list of longer lengths present under it, plus the
+  // markers of that shorter search.
   uint32_t l1_c = 0;
   bool l1 = codes.nodes.size() > 1;
   std::vector<uint32_t> l1_tab;
-  u128 tag_v = 0;
+  std::vector<u128> tags;
+  std::map<u128, uint32_t> tag_ix;
+  uint32_t max_tags = kV6DefaultTags;
+  if (const char* e = std::getenv("GPC_V6_MAX_TAGS")) max_tags = uint32_t(std::min<long>(kV6MaxTags, std::max<long>(1, std::atol(e))));
   if (l1) {
-    const u128 v0 = codes.nodes[1].v;
-    int c = 128;
-    for (size_t n = 1; n < codes.nodes.size(); n++) {
-      const auto& N = codes.nodes[n];
-      c = std::min(c, N.len);
-      const u128 x = N.v ^ v0;
-      int lcp = 0;
-      while (lcp < 128 && !((x >> (127 - lcp)) & 1)) lcp++;
-      c = std::min(c, lcp);
+    int maxlen = 0;
+    for (size_t n = 1; n < codes.nodes.size(); n++) maxlen = std::max(maxlen, codes.nodes[n].len);
+    l1 = false;
+    for (int c = std::min(maxlen, 128 - int(kV6L1Bits)); c >= 1 && !l1; c--) {
+      std::set<u128> ts;
+      for (size_t n = 1; n < codes.nodes.size() && ts.size() <= max_tags; n++)
+        if (codes.nodes[n].len >= c) ts.insert(codes.nodes[n].v & v6_prefix_mask(c));
+      if (ts.empty() || ts.size() > max_tags) continue;
+      l1 = true;
+      l1_c = uint32_t(c);
+      tags.assign(ts.begin(), ts.end());
     }
-    l1_c = uint32_t(c);
-    l1 = c + int(kV6L1Bits) <= 128;
-    tag_v = c ? (v0 & v6_prefix_mask(c)) : 0;
+    for (size_t t = 0; t < tags.size(); t++) tag_ix[tags[t]] = uint32_t(t);
   }
   if (l1) {
-    const uint32_t s_len = l1_c + kV6L1Bits, nreg = 1u << kV6L1Bits;
+    const uint32_t s_len = l1_c + kV6L1Bits, nreg = 1u << kV6L1Bits, nt = uint32_t(tags.size());
     auto region = [&](u128 v) { return uint32_t(v >> (128 - s_len)) & (nreg - 1u); };
-    std::vector<uint32_t> base(nreg, 0u), base_len(nreg, 0u);
-    std::vector<std::vector<uint32_t>> reg_lens(nreg);  // length indexes > s_len present
+    auto tag_of = [&](u128 v) { return tag_ix.at(v & v6_prefix_mask(int(l1_c))); };
+    std::vector<uint32_t> base(size_t(nt) * nreg, 0u), base_len(size_t(nt) * nreg, 0u);
+    std::vector<std::vector<uint32_t>> reg_lens(size_t(nt) * nreg);  // length indexes > s_len present
+    // prefixes shorter than c: the deepest one covering each tag is every region's starting base
+    for (uint32_t t = 0; t < nt; t++) {
+      uint32_t bc = 0, bl = 0;
+      for (size_t n = 1; n < codes.nodes.size(); n++) {
+        const auto& N = codes.nodes[n];
+        if (uint32_t(N.len) < l1_c && (tags[t] & v6_prefix_mask(N.len)) == N.v && uint32_t(N.len) >= bl) {
+          bc = pad(N);
+          bl = uint32_t(N.len);
+        }
+      }
+      std::fill(base.begin() + size_t(t) * nreg, base.begin() + size_t(t + 1) * nreg, bc);
+      std::fill(base_len.begin() + size_t(t) * nreg, base_len.begin() + size_t(t + 1) * nreg, bl);
+    }
     for (size_t n = 1; n < codes.nodes.size(); n++) {
       const auto& N = codes.nodes[n];
+      if (uint32_t(N.len) < l1_c) continue;
       const uint32_t li = uint32_t(std::lower_bound(lens.begin(), lens.end(), uint32_t(N.len)) - lens.begin());
+      const size_t tb = size_t(tag_of(N.v)) * nreg;
       if (uint32_t(N.len) > s_len) {
-        reg_lens[region(N.v)].push_back(li);
+        reg_lens[tb + region(N.v)].push_back(li);
         continue;
       }
-      // a prefix no longer than c + 16 covers 2^(c+16-len) whole regions: the deepest one wins
+      // a prefix no longer than c + 16 covers 2^(c+16-len) whole regions of its tag: the deepest wins
       const uint32_t r0 = region(N.v), span = 1u << (s_len - uint32_t(N.len));
       for (uint32_t r = r0; r < r0 + span; r++)
-        if (uint32_t(N.len) >= base_len[r]) {
-          base[r] = pad(N);
-          base_len[r] = uint32_t(N.len);
+        if (uint32_t(N.len) >= base_len[tb + r]) {
+          base[tb + r] = pad(N);
+          base_len[tb + r] = uint32_t(N.len);
         }
     }
-    l1_tab.assign(size_t(nreg) * 4, 0u);
-    for (uint32_t r = 0; r < nreg; r++) {
+    l1_tab.assign(size_t(nt) * nreg * 4, 0u);
+    for (size_t r = 0; r < size_t(nt) * nreg; r++) {
       auto& L = reg_lens[r];
       std::sort(L.begin(), L.end());
       L.erase(std::unique(L.begin(), L.end()), L.end());
-      uint32_t* e = l1_tab.data() + 4 * size_t(r);
+      uint32_t* e = l1_tab.data() + 4 * r;
       e[0] = base[r];
       if (L.size() > kV6L1MaxLens) {
         e[1] = kV6L1Global;
@@ -1679,7 +1787,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     for (size_t n = 1; n < codes.nodes.size(); n++) {
       const auto& P = codes.nodes[n];
       if (uint32_t(P.len) <= s_len) continue;
-      const auto& L = reg_lens[region(P.v)];
+      const auto& L = reg_lens[size_t(tag_of(P.v)) * nreg + region(P.v)];
       if (L.size() > kV6L1MaxLens) continue;
       const uint32_t li = uint32_t(std::lower_bound(lens.begin(), lens.end(), uint32_t(P.len)) - lens.begin());
       const int t = int(std::lower_bound(L.begin(), L.end(), li) - L.begin());
@@ -1701,6 +1809,8 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
         lo = mid + 1;
       }
     }
+    if (std::getenv("GPC_IMAGE_DEBUG"))
+      std::fprintf(stderr, "IPv6 region tables: c = %u, %u tags\n", l1_c, nt);
   }
   // one table per length (core.hpp V6Len), appended after the V6Lpm block
   std::vector<std::vector<std::pair<std::array<uint32_t, 4>, uint32_t>>> per_len(lens.size());
@@ -1735,8 +1845,12 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     while (b.size() % 16) b.push_back(0u);
     L.l1_off = uint32_t(b.size());
     L.l1_c = l1_c;
-    const uint32_t tg[4] = {uint32_t(tag_v >> 96), uint32_t(tag_v >> 64), uint32_t(tag_v >> 32), uint32_t(tag_v)};
-    if (l1_c) v6_key(tg, l1_c, L.l1_tag);
+    L.n_tags = uint32_t(tags.size());
+    for (size_t t = 0; t < tags.size(); t++) {
+      const u128 tv = tags[t];
+      const uint32_t tg[4] = {uint32_t(tv >> 96), uint32_t(tv >> 64), uint32_t(tv >> 32), uint32_t(tv)};
+      if (l1_c) v6_key(tg, l1_c, L.l1_tag[t]);
+    }
     b.insert(b.end(), l1_tab.begin(), l1_tab.end());
     tab_words += l1_tab.size();
   }
@@ -2596,6 +2710,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         si.axis = axis;
         si.band = band;
         si.bits = uint8_t(bits);
+        si.fmt = 0;  // offset pairs (bucket directories: composite sub-indexes)
         si.off = B.put(offs.data(), offs.size(), 16);
         si.ent = ents.empty() ? si.off : B.put(ents.data(), ents.size(), 16);
         si.pres = 0;

@@ -408,23 +408,46 @@ V6_EMBED = int(ipaddress.IPv6Address("fd00:10::"))
 _V6_PREFIX12 = np.frombuffer(V6_EMBED.to_bytes(16, "big")[:12], dtype=np.uint8)
 
 
-def _v6_addr(a):
+# Embeddings of the IPv4 workloads in IPv6, both prefix-preserving for IPv4 prefixes of length >= 2
+# (a in P <=> emb(a) in emb(P)), so the IPv4 oracle's verdicts apply to the embedded packets:
+#   "96"      a -> fd00:10::a (one /96; an IPv4 /L is an IPv6 /96+L)
+#   "multi48" the top 2 bits of a pick one of four /48s fd00:0:k::/48, the other 30 bits follow the
+#             /48 (an IPv4 /L is an IPv6 /46+L): rule sets spread over several /48s
+V6_MULTI48 = int(ipaddress.IPv6Address("fd00::"))
+
+
+def v6_embed(v4: int, embed: str = "96") -> int:
+    if embed == "96":
+        return V6_EMBED | v4
+    return V6_MULTI48 | ((v4 >> 30) << 80) | ((v4 & 0x3FFFFFFF) << 50)
+
+
+def v6_embed_len(plen: int, embed: str = "96") -> int:
+    if embed == "96":
+        return 96 + plen
+    if plen < 2:
+        raise ValueError("multi48 embeds IPv4 prefixes of length >= 2 only")
+    return 46 + plen
+
+
+def _v6_addr(a, embed="96"):
     if isinstance(a, str):
         if "." not in a:
             return a
         if "/" in a:
-            return _v6_addr({"ipnet": a})["ipnet"]
-        return str(ipaddress.IPv6Address(V6_EMBED | int(ipaddress.ip_address(a))))
+            return _v6_addr({"ipnet": a}, embed)["ipnet"]
+        return str(ipaddress.IPv6Address(v6_embed(int(ipaddress.ip_address(a)), embed)))
     (k, v), = a.items()
     if k in ("ip", "ctip"):
-        return {k: str(ipaddress.IPv6Address(V6_EMBED | int(ipaddress.ip_address(v))))}
+        return {k: str(ipaddress.IPv6Address(v6_embed(int(ipaddress.ip_address(v)), embed)))}
     if k in ("ipnet", "ctipnet"):
         n = ipaddress.ip_network(v, strict=False)
-        return {k: "%s/%d" % (ipaddress.IPv6Address(V6_EMBED | int(n.network_address)), 96 + n.prefixlen)}
+        return {k: "%s/%d" % (ipaddress.IPv6Address(v6_embed(int(n.network_address), embed)),
+                              v6_embed_len(n.prefixlen, embed))}
     return a
 
 
-def to_ipv6(wl: Workload, dual=False) -> Workload:
+def to_ipv6(wl: Workload, dual=False, embed="96") -> Workload:
     """The workload with its addresses in IPv6 (dual=True: both families in every peer list)."""
     import copy
     out = Workload(wl.name + ("dual" if dual else "v6"))
@@ -433,41 +456,51 @@ def to_ipv6(wl: Workload, dual=False) -> Workload:
         r6 = copy.deepcopy(r)
         for side in ("from", "to"):
             if r.get(side) is not None:
-                mapped = [_v6_addr(a) for a in r[side]]
+                mapped = [_v6_addr(a, embed) for a in r[side]]
                 r6[side] = (list(r[side]) + [m for m, a in zip(mapped, r[side]) if m != a]) if dual else mapped
         out.rules.append(r6)
     return out
 
 
-def v6_bytes(v4: np.ndarray) -> np.ndarray:
-    """(n,) IPv4 addresses -> (n, 16) uint8 network-order IPv6 addresses in fd00:10::/96."""
+def v6_bytes(v4: np.ndarray, embed="96") -> np.ndarray:
+    """(n,) IPv4 addresses -> (n, 16) uint8 network-order IPv6 addresses (the embedding above)."""
     v4 = np.asarray(v4, dtype=np.uint32)
-    tail = v4.astype(">u4").view(np.uint8).reshape(-1, 4)
-    return np.ascontiguousarray(np.concatenate([np.broadcast_to(_V6_PREFIX12, (len(v4), 12)), tail], axis=1))
+    if embed == "96":
+        tail = v4.astype(">u4").view(np.uint8).reshape(-1, 4)
+        return np.ascontiguousarray(np.concatenate([np.broadcast_to(_V6_PREFIX12, (len(v4), 12)), tail], axis=1))
+    return np.array([list(v6_embed(int(a), embed).to_bytes(16, "big")) for a in v4], dtype=np.uint8).reshape(-1, 16)
 
 
-def packets_to_v6(cols: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+def packets_to_v6(cols: Dict[str, np.ndarray], embed="96") -> Dict[str, np.ndarray]:
     """IPv4 packet columns -> the IPv6 batch of the same packets (ICMP -> ICMPv6)."""
     out = {k: v for k, v in cols.items() if k not in ("src", "dst", "ct_src", "ct_dst")}
     for k in ("src", "dst", "ct_src", "ct_dst"):
         if k in cols:
-            out[k + "6"] = v6_bytes(cols[k])
+            out[k + "6"] = v6_bytes(cols[k], embed)
     out["proto"] = np.where(cols["proto"] == 1, 58, cols["proto"]).astype(np.uint8)
     return out
 
 
-def packets_to_v6_torch(cols):
-    """Device version of packets_to_v6 (bench): (n, 16) uint8 address columns in fd00:10::/96."""
+def packets_to_v6_torch(cols, embed="96"):
+    """Device version of packets_to_v6 (bench): (n, 16) uint8 address columns (the embedding above)."""
     import torch
     out = {k: v for k, v in cols.items() if k not in ("src", "dst", "ct_src", "ct_dst")}
+    be32 = lambda x: torch.stack([(x >> 24) & 255, (x >> 16) & 255, (x >> 8) & 255, x & 255], dim=1)
     for k in ("src", "dst", "ct_src", "ct_dst"):
         if k not in cols:
             continue
         v = cols[k].to(torch.int64) & 0xFFFFFFFF
         n = v.shape[0]
-        tail = torch.stack([(v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255], dim=1).to(torch.uint8)
-        head = torch.as_tensor(_V6_PREFIX12.copy(), device=v.device).expand(n, 12)
-        out[k + "6"] = torch.cat([head, tail], dim=1).contiguous()
+        if embed == "96":
+            head = torch.as_tensor(_V6_PREFIX12.copy(), device=v.device).expand(n, 12)
+            out[k + "6"] = torch.cat([head, be32(v).to(torch.uint8)], dim=1).contiguous()
+            continue
+        # multi48: fd00:0:k::/48 (k = top 2 bits), then the other 30 bits at bits 79..50
+        z = torch.zeros((n, 16), dtype=torch.int64, device=v.device)
+        z[:, 0] = 0xFD
+        z[:, 5] = v >> 30
+        z[:, 6:10] = be32(((v & 0x3FFFFFFF) << 2) & 0xFFFFFFFF)
+        out[k + "6"] = z.to(torch.uint8).contiguous()
     p = cols["proto"]
     out["proto"] = torch.where(p == 1, torch.full_like(p, 58), p)
     return out

@@ -397,6 +397,8 @@ def main():
                     help="gpc_config.group_packets: 0 = auto (batches >= 2^18 against images >= 4 MB), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),
                     help="6: the workload's addresses embedded in fd00:10::/96, IPv6 packets (gpc_classify6)")
+    ap.add_argument("--v6-embed", default="96", choices=("96", "multi48"),
+                    help="--family 6: fd00:10::/96, or four /48s chosen by the top 2 IPv4 bits (workload.v6_embed)")
     ap.add_argument("--multidev", type=int, default=0,
                     help="one process over N devices (gpc_create_multi: the agent's shape, one control plane per "
                          "node) instead of one process per GPU; N slots, one stream and host thread per slot")
@@ -459,7 +461,7 @@ def main():
     v6 = args.family == 6
     clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6, group_packets=args.group)
     clf.initialize()
-    clf.batch_install_policy_rule_flows(workload.to_ipv6(wl).rules if v6 else wl.rules)
+    clf.batch_install_policy_rule_flows(workload.to_ipv6(wl, embed=args.v6_embed).rules if v6 else wl.rules)
     if getattr(wl, "services", None):
         workload.install_services(clf, wl)
     clf.commit()
@@ -467,7 +469,7 @@ def main():
 
     n = args.packets
     cols4 = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + rank, device=dev)
-    cols = workload.packets_to_v6_torch(cols4) if v6 else cols4
+    cols = workload.packets_to_v6_torch(cols4, embed=args.v6_embed) if v6 else cols4
     classify = clf.classify6_device if v6 else clf.classify_device
     out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
     soa = gpc.pkt_soa_device(cols)
@@ -587,7 +589,8 @@ def main():
             len(idx), n / len(idx),
             "classified again on the final epoch, vs the oracle after replaying the %d applied ops" % len(churn_ops.log)
             if churn else "last step's verdicts",
-            "; IPv6 packets vs the IPv4 oracle (fd00:10::/96 embedding)" if v6 else "",
+            "; IPv6 packets vs the IPv4 oracle (%s embedding)" % ("fd00:10::/96" if args.v6_embed == "96" else
+                                                                 "four /48s") if v6 else "",
             "; rank 0's shard of %d" % world if world > 1 else "")
         if parity.get("mismatches"):
             print("PARITY FAILURE: %s" % json.dumps(parity), file=sys.stderr)
@@ -631,7 +634,7 @@ def main():
     if v6:
         res["metric"] = "Mpps classified (IPv6 5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW"
         res["config"]["family"] = 6
-        res["config"]["v6_embedding"] = "fd00:10::/96"
+        res["config"]["v6_embedding"] = "fd00:10::/96" if args.v6_embed == "96" else "fd00:0:k::/48, k = top 2 bits"
     if update is not None:
         res["update"] = update
         res["metric"] = "Mpps classified under AddPolicyRuleAddress/DeletePolicyRuleAddress churn @100k rules"

@@ -173,6 +173,7 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const uint32
     std::sort(g_lines.begin(), g_lines.end());
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;
+    for (auto& kv : g_line_site) gpc_emu_site_lines[kv.second & 2047]++;
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);

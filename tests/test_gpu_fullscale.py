@@ -117,6 +117,18 @@ def test_device_ipv6_vs_oracle_fullscale_c3(group):
     assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
 
 
+def test_device_ipv6_multi48_vs_oracle_fullscale_c3():
+    """Full C3 embedded over four /48s (workload "multi48": the top 2 IPv4 bits pick the /48) -- the
+    device LPM's region tables then have one table per tag (rule sets over several
+    /48s) -- equals the C oracle's IPv4 verdicts of the same packets."""
+    f, wl, cols = _inputs("C3")
+    c = _classifier(wl, ipv6=True, rules=workload.to_ipv6(wl, embed="multi48").rules)
+    got = c.classify6_host(workload.packets_to_v6(cols, embed="multi48"), count=True)
+    res = parity.compare(got, f["verdicts"])
+    assert res["mismatches"] == 0, res
+    assert _nonzero(c.network_policy_metrics()) == _nonzero(f["metrics"])
+
+
 @pytest.mark.parametrize("dual", [False, True])
 def test_device_ipv6_vs_python_oracle_c1(dual):
     """gpc_classify6 directly against the Python oracle over the oracle compiler's IPv6 flows

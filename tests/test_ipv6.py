@@ -76,6 +76,20 @@ def test_ipv6_metamorphic_vs_ipv4(name):
     _cmp(got, want, cols)
 
 
+@pytest.mark.parametrize("max_tags", ["16", "1"])
+def test_ipv6_metamorphic_multi48(max_tags, monkeypatch):
+    """The rule set spread over four /48s (embedding "multi48"): IPv6 verdicts == IPv4 verdicts,
+    with one region table per /c tag (core.hpp V6Lpm, up to 16) and with a single tag allowed (then
+    no tag length qualifies below the /48 split and every lookup runs the global search)."""
+    monkeypatch.setenv("GPC_V6_MAX_TAGS", max_tags)
+    wl = workload.config3(n_policies_per_dir=50, rules_per_policy=100)
+    n = 20000
+    cols = workload.gen_packets(wl, n, seed=7)
+    want = emu.classify(_classifier(wl.rules, ipv6=False), cols)
+    got = emu.classify6(_classifier(workload.to_ipv6(wl, embed="multi48").rules), workload.packets_to_v6(cols, embed="multi48"))
+    _cmp(got, want, cols)
+
+
 def test_ipv6_metamorphic_full_c3():
     """Full C3 (100k rules, 245k nested CIDRs) in IPv6: the prefix tree fits 32-bit codes and the
     verdicts equal the IPv4 image's."""

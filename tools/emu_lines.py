@@ -17,25 +17,33 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
     ap.add_argument("--packets", type=int, default=20000)
+    ap.add_argument("--family", type=int, default=4, choices=(4, 6))
+    ap.add_argument("--v6-embed", default="96", choices=("96", "multi48"))
     args = ap.parse_args()
+    v6 = args.family == 6
     from antrea_amd import gpc, workload
     from tests import emu
     wl = workload.CONFIGS[args.config]()
-    c = gpc.Classifier()
+    c = gpc.Classifier(ipv4=not v6, ipv6=v6)
     c.initialize()
-    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    c.batch_install_policy_rule_flows(workload.to_ipv6(wl, embed=args.v6_embed).rules if v6 else copy.deepcopy(wl.rules))
     if getattr(wl, "services", None):
         workload.install_services(c, wl)
     emu.commit_host(c)
     cols = workload.gen_packets(wl, args.packets, seed=5)
     emu.stats(reset=True)
     emu.site_lines(reset=True)
-    emu.classify(c, cols)
+    if v6:
+        emu.classify6(c, workload.packets_to_v6(cols, embed=args.v6_embed))
+    else:
+        emu.classify(c, cols)
     s, sites = emu.stats(), emu.site_lines()
     n = s[7] or 1
     src = open(os.path.join(os.path.dirname(gpc.HERE), "antrea_amd", "csrc", "core.hpp")).read().split("\n")
     print("%s: %.2f distinct lines / packet; %.2f table lookups, %.2f entries scanned, %.3f verifications "
           "(%.3f failed) per packet" % (args.config, s[6] / n, s[0] / n, s[4] / n, s[3] / n, s[5] / n))
+    if v6:
+        print("IPv6 codes: %.2f dependent search rounds per packet (src and dst searched together)" % (s[11] / n))
     for line, v in sorted(sites.items(), key=lambda kv: -kv[1]):
         if v / n >= 0.01:
             print("  core.hpp:%-5d %6.2f  %s" % (line, v / n, src[line - 1].strip()[:70]))
