@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <random>
 #include <queue>
@@ -1711,7 +1712,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
   // four (c = 98), 3.46 ms with sixteen (c = 100). Per tag, every /c+16 region gets the best match no longer than c + 16 (prefixes
   // shorter than c cover whole tags) and the list of longer lengths present under it, plus the
   // markers of that shorter search.
-  uint32_t l1_c = 0;
+  uint32_t l1_c = 0, n_short = 0;
   bool l1 = codes.nodes.size() > 1;
   std::vector<uint32_t> l1_tab;
   std::vector<u128> tags;
@@ -1738,7 +1739,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     auto region = [&](u128 v) { return uint32_t(v >> (128 - s_len)) & (nreg - 1u); };
     auto tag_of = [&](u128 v) { return tag_ix.at(v & v6_prefix_mask(int(l1_c))); };
     std::vector<uint32_t> base(size_t(nt) * nreg, 0u), base_len(size_t(nt) * nreg, 0u);
-    std::vector<std::vector<uint32_t>> reg_lens(size_t(nt) * nreg);  // length indexes > s_len present
+    std::vector<std::vector<uint32_t>> reg_nodes(size_t(nt) * nreg);  // nodes longer than s_len, per region
     // prefixes shorter than c: the deepest one covering each tag is every region's starting base
     for (uint32_t t = 0; t < nt; t++) {
       uint32_t bc = 0, bl = 0;
@@ -1755,10 +1756,9 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     for (size_t n = 1; n < codes.nodes.size(); n++) {
       const auto& N = codes.nodes[n];
       if (uint32_t(N.len) < l1_c) continue;
-      const uint32_t li = uint32_t(std::lower_bound(lens.begin(), lens.end(), uint32_t(N.len)) - lens.begin());
       const size_t tb = size_t(tag_of(N.v)) * nreg;
       if (uint32_t(N.len) > s_len) {
-        reg_lens[tb + region(N.v)].push_back(li);
+        reg_nodes[tb + region(N.v)].push_back(uint32_t(n));
         continue;
       }
       // a prefix no longer than c + 16 covers 2^(c+16-len) whole regions of its tag: the deepest wins
@@ -1769,27 +1769,74 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
           base_len[tb + r] = uint32_t(N.len);
         }
     }
+    // Entries (core.hpp v6_codes): a leaf carries its base and the list of longer lengths present
+    // (kV6L1Global past kV6L1MaxLens); a block whose list exceeds kV6LeafLens is split into 256
+    // sub-blocks (kV6L1Child) while it is shorter than /128. GPC_V6_LEAF_LENS overrides the split
+    // threshold (experiments; 8 = round-5 regions without sub-tables).
+    uint32_t leaf_max = kV6LeafLens;
+    if (const char* e = std::getenv("GPC_V6_LEAF_LENS")) leaf_max = uint32_t(std::min<long>(kV6L1MaxLens, std::max<long>(0, std::atol(e))));
     l1_tab.assign(size_t(nt) * nreg * 4, 0u);
-    for (size_t r = 0; r < size_t(nt) * nreg; r++) {
-      auto& L = reg_lens[r];
-      std::sort(L.begin(), L.end());
-      L.erase(std::unique(L.begin(), L.end()), L.end());
-      uint32_t* e = l1_tab.data() + 4 * r;
-      e[0] = base[r];
-      if (L.size() > kV6L1MaxLens) {
-        e[1] = kV6L1Global;
-        continue;
-      }
-      e[1] = uint32_t(L.size());
-      for (size_t j = 0; j < L.size(); j++) e[2 + j / 4] |= L[j] << (8 * (j % 4));
-    }
-    // markers of the regional searches (nodes longer than c + 16 in regions with a list)
+    std::vector<std::vector<uint32_t>> leaf_L(size_t(nt) * nreg);  // per entry: its search list (leaves)
+    size_t n_sub = 0, sub_bytes = 0;
+    auto len_ix = [&](uint32_t len) { return uint32_t(std::lower_bound(lens.begin(), lens.end(), len) - lens.begin()); };
+    std::function<void(size_t, uint32_t, uint32_t, uint32_t, std::vector<uint32_t>&)> fill =
+        [&](size_t ei, uint32_t ll, uint32_t bc, uint32_t bl, std::vector<uint32_t>& ns) {
+          std::vector<uint32_t> L;
+          for (uint32_t n : ns) L.push_back(len_ix(uint32_t(codes.nodes[n].len)));
+          std::sort(L.begin(), L.end());
+          L.erase(std::unique(L.begin(), L.end()), L.end());
+          if (L.size() > leaf_max && ll < 128u) {
+            const uint32_t st = v6_sub_bits(ll), sl = ll + st, nsub = 1u << st;
+            const size_t child = l1_tab.size() / 4;
+            l1_tab.resize(l1_tab.size() + 4 * size_t(nsub), 0u);
+            leaf_L.resize(l1_tab.size() / 4);
+            n_sub++;
+            sub_bytes += 16ull * nsub;
+            l1_tab[4 * ei + 1] = kV6L1Child;
+            l1_tab[4 * ei + 2] = uint32_t(4 * child);
+            std::vector<uint32_t> sb(nsub, bc), sbl(nsub, bl);
+            std::vector<std::vector<uint32_t>> sn(nsub);
+            auto sub = [&](u128 v) { return uint32_t(v >> (128 - sl)) & (nsub - 1u); };
+            for (uint32_t n : ns) {
+              const auto& N = codes.nodes[n];
+              if (uint32_t(N.len) > sl) {
+                sn[sub(N.v)].push_back(n);
+                continue;
+              }
+              const uint32_t s0 = sub(N.v), span = 1u << (sl - uint32_t(N.len));
+              for (uint32_t q = s0; q < s0 + span; q++)
+                if (uint32_t(N.len) >= sbl[q]) {
+                  sb[q] = pad(N);
+                  sbl[q] = uint32_t(N.len);
+                }
+            }
+            for (uint32_t q = 0; q < nsub; q++) fill(child + q, sl, sb[q], sbl[q], sn[q]);
+            return;
+          }
+          l1_tab[4 * ei] = bc;
+          if (L.size() > kV6L1MaxLens) {
+            l1_tab[4 * ei + 1] = kV6L1Global;
+            return;
+          }
+          l1_tab[4 * ei + 1] = uint32_t(L.size());
+          for (size_t q = 0; q < L.size(); q++) l1_tab[4 * ei + 2 + q / 4] |= L[q] << (8 * (q % 4));
+          leaf_L[ei] = std::move(L);
+        };
+    for (size_t r = 0; r < size_t(nt) * nreg; r++) fill(r, s_len, base[r], base_len[r], reg_nodes[r]);
+    // markers of the regional searches: each node longer than its leaf's block, along the leaf's list
     for (size_t n = 1; n < codes.nodes.size(); n++) {
       const auto& P = codes.nodes[n];
       if (uint32_t(P.len) <= s_len) continue;
-      const auto& L = reg_lens[size_t(tag_of(P.v)) * nreg + region(P.v)];
-      if (L.size() > kV6L1MaxLens) continue;
-      const uint32_t li = uint32_t(std::lower_bound(lens.begin(), lens.end(), uint32_t(P.len)) - lens.begin());
+      size_t ei = size_t(tag_of(P.v)) * nreg + region(P.v);
+      uint32_t ll = s_len;
+      while (l1_tab[4 * ei + 1] & kV6L1Child) {
+        const uint32_t st = v6_sub_bits(ll);
+        ll += st;
+        ei = l1_tab[4 * ei + 2] / 4 + (uint32_t(P.v >> (128 - ll)) & ((1u << st) - 1u));
+      }
+      if (uint32_t(P.len) <= ll || (l1_tab[4 * ei + 1] & kV6L1Global)) continue;  // folded into the base / global search
+      const auto& L = leaf_L[ei];
+      const uint32_t li = len_ix(uint32_t(P.len));
       const int t = int(std::lower_bound(L.begin(), L.end(), li) - L.begin());
       int lo = 0, hi = int(L.size()) - 1;
       while (lo <= hi) {
@@ -1809,6 +1856,32 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
         lo = mid + 1;
       }
     }
+    // markers of the searches of addresses under no tag: over the lengths shorter than c only
+    n_short = uint32_t(std::lower_bound(lens.begin(), lens.end(), l1_c) - lens.begin());
+    for (size_t n = 1; n < codes.nodes.size(); n++) {
+      const auto& P = codes.nodes[n];
+      if (uint32_t(P.len) >= l1_c) continue;
+      const int t = int(len_ix(uint32_t(P.len)));
+      int lo = 0, hi = int(n_short) - 1;
+      while (lo <= hi) {
+        const int mid = (lo + hi) / 2;
+        if (mid == t) break;
+        if (mid > t) {
+          hi = mid - 1;
+          continue;
+        }
+        const uint32_t M = lens[size_t(mid)];
+        const std::pair<u128, uint32_t> key{P.v & v6_prefix_mask(int(M)), M};
+        if (!lpm_map.count(key)) {
+          int a = P.parent;
+          while (a > 0 && codes.nodes[size_t(a)].len > int(M)) a = codes.nodes[size_t(a)].parent;
+          lpm_map[key] = a > 0 ? pad(codes.nodes[size_t(a)]) : 0u;
+        }
+        lo = mid + 1;
+      }
+    }
+    if (std::getenv("GPC_IMAGE_DEBUG"))
+      std::fprintf(stderr, "IPv6 sub-region tables: %zu (%.1f MB)\n", n_sub, double(sub_bytes) / 1e6);
     if (std::getenv("GPC_IMAGE_DEBUG"))
       std::fprintf(stderr, "IPv6 region tables: c = %u, %u tags\n", l1_c, nt);
   }
@@ -1846,6 +1919,7 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     L.l1_off = uint32_t(b.size());
     L.l1_c = l1_c;
     L.n_tags = uint32_t(tags.size());
+    L.n_short = n_short;
     for (size_t t = 0; t < tags.size(); t++) {
       const u128 tv = tags[t];
       const uint32_t tg[4] = {uint32_t(tv >> 96), uint32_t(tv >> 64), uint32_t(tv >> 32), uint32_t(tv)};

@@ -174,6 +174,19 @@ extern "C" int emu_classify6(const uint32_t* blob, const void* hdr, const uint32
     ::gpc_emu_stats[6] += std::unique(g_lines.begin(), g_lines.end()) - g_lines.begin();  // distinct 64-B lines
     ::gpc_emu_stats[7] += 1;
     for (auto& kv : g_line_site) gpc_emu_site_lines[kv.second & 2047]++;
+    if (i < (1u << 20) && !ovf) {  // search rounds of src and dst alone (the code kernel: one address per lane)
+      const unsigned long long r0 = ::gpc_emu_stats[11], l0 = ::gpc_emu_stats[12], g0 = ::gpc_emu_stats[13];
+      uint32_t a1[1][4], c1;
+      v6_words(pk->src6 + 16 * i, a1[0]);
+      v6_codes<1>(blob, h->v6_lpm, a1, &c1);
+      gpc_emu_pkt_iter[i] = unsigned(::gpc_emu_stats[11] - r0);
+      v6_words(pk->dst6 + 16 * i, a1[0]);
+      v6_codes<1>(blob, h->v6_lpm, a1, &c1);
+      gpc_emu_pkt_search[i] = unsigned(::gpc_emu_stats[11] - r0) - gpc_emu_pkt_iter[i];
+      ::gpc_emu_stats[11] = r0;
+      ::gpc_emu_stats[12] = l0;
+      ::gpc_emu_stats[13] = g0;
+    }
     if (counters)
       count_packet(o, pk->len ? pk->len[i] : 0u, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { counters[w] += v; });
     uint32_t* w = reinterpret_cast<uint32_t*>(out + 2 * i);

@@ -90,6 +90,21 @@ def test_ipv6_metamorphic_multi48(max_tags, monkeypatch):
     _cmp(got, want, cols)
 
 
+@pytest.mark.parametrize("embed", ["96", "multi48"])
+@pytest.mark.parametrize("leaf", ["0", "2", "8"])
+def test_ipv6_sub_region_tables(leaf, embed, monkeypatch):
+    """Sub-region tables (core.hpp kV6L1Child) at other split thresholds than the default (1):
+    0 (every block holding a longer prefix split down to /128: no hash probe below the tables),
+    2, and 8 (split only where a search would go global). IPv6 verdicts == IPv4 verdicts."""
+    monkeypatch.setenv("GPC_V6_LEAF_LENS", leaf)
+    wl = workload.config3(n_policies_per_dir=50, rules_per_policy=100)
+    n = 20000
+    cols = workload.gen_packets(wl, n, seed=9)
+    want = emu.classify(_classifier(wl.rules, ipv6=False), cols)
+    got = emu.classify6(_classifier(workload.to_ipv6(wl, embed=embed).rules), workload.packets_to_v6(cols, embed=embed))
+    _cmp(got, want, cols)
+
+
 def test_ipv6_metamorphic_full_c3():
     """Full C3 (100k rules, 245k nested CIDRs) in IPv6: the prefix tree fits 32-bit codes and the
     verdicts equal the IPv4 image's."""

@@ -43,7 +43,17 @@ def main():
     print("%s: %.2f distinct lines / packet; %.2f table lookups, %.2f entries scanned, %.3f verifications "
           "(%.3f failed) per packet" % (args.config, s[6] / n, s[0] / n, s[4] / n, s[3] / n, s[5] / n))
     if v6:
-        print("IPv6 codes: %.2f dependent search rounds per packet (src and dst searched together)" % (s[11] / n))
+        print("IPv6 codes: %.2f dependent search rounds per packet (src and dst searched together); per address: "
+              "%.2f lengths in the regional search, %.3f global searches" % (s[11] / n, s[12] / (2 * n), s[13] / (2 * n)))
+        import ctypes as C
+        import numpy as np
+        lib = emu.load()
+        m = min(args.packets, 1 << 20) // 64 * 64
+        for col, name in (("gpc_emu_pkt_iter", "src"), ("gpc_emu_pkt_search", "dst")):
+            r = np.ctypeslib.as_array((C.c_uint * (1 << 20)).in_dll(lib, col))[:m].copy()
+            w = r.reshape(-1, 64).max(axis=1)
+            print("  %s: rounds per address mean %.2f, per 64-lane wave (max) mean %.2f, histogram of wave max %s" % (
+                name, r.mean(), w.mean(), np.bincount(w).tolist()))
     for line, v in sorted(sites.items(), key=lambda kv: -kv[1]):
         if v / n >= 0.01:
             print("  core.hpp:%-5d %6.2f  %s" % (line, v / n, src[line - 1].strip()[:70]))
