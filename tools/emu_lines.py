@@ -54,6 +54,16 @@ def main():
             w = r.reshape(-1, 64).max(axis=1)
             print("  %s: rounds per address mean %.2f, per 64-lane wave (max) mean %.2f, histogram of wave max %s" % (
                 name, r.mean(), w.mean(), np.bincount(w).tolist()))
+    if not v6:
+        import ctypes as C
+        import numpy as np
+        lib = emu.load()
+        m = min(args.packets, 1 << 20) // 64 * 64
+        for col, name in (("gpc_emu_pkt_pass", "scan passes"), ("gpc_emu_pkt_iter", "scan iterations"),
+                          ("gpc_emu_pkt_search", "verifier search steps"), ("gpc_emu_pkt_verif", "verifications")):
+            r = np.ctypeslib.as_array((C.c_uint * (1 << 20)).in_dll(lib, col))[:m].copy()
+            w = r.reshape(-1, 64).max(axis=1)
+            print("  %-22s per packet mean %.2f, per 64-lane wave (max) mean %.2f" % (name, r.mean(), w.mean()))
     for line, v in sorted(sites.items(), key=lambda kv: -kv[1]):
         if v / n >= 0.01:
             print("  core.hpp:%-5d %6.2f  %s" % (line, v / n, src[line - 1].strip()[:70]))

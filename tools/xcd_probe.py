@@ -1,8 +1,8 @@
 """GPU experiment (no product code): would a stage launch gain if each XCD's L2 only ever saw 1/8 of
 the stage's driver index? The same C3 batch is classified in three orders: as generated, and
 permuted so that the blocks sharing an XCD (blocks b with equal b % 8 under round-robin dispatch,
-MI355X_MICROARCH.md "Workgroup dispatch") get only packets whose driver band key -- egress: dst /8,
-ingress: src /8 (C3's composite tables are keyed at /8) -- hashes to that residue. The permutation is
+MI355X_MICROARCH.md "Workgroup dispatch") get only packets whose driver band key -- egress: dst /12,
+ingress: src /12 (C3's composite tables are keyed at band 0, /12) -- hashes to that residue. The permutation is
 made with torch before the timed region; verdicts do not depend on the order.
 
     python tools/xcd_probe.py [--packets 67108864] [--steps 10]
@@ -35,8 +35,8 @@ def main():
     def i64(t):
         return t.view(torch.int32).to(torch.int64) & 0xFFFFFFFF if t.dtype == torch.uint32 else t.to(torch.int64)
 
-    def part(t):  # residue of the /8 key (a multiplicative hash, so that 10.x etc. spread)
-        return ((((i64(t) >> 24) * 0x9E3779B1) & 0xFFFFFFFF) >> 29)
+    def part(t):  # core.hpp cbucket_class of the band-0 key (/12): the slice of the index it touches
+        return ((((i64(t) >> 20) * 0x9E3779B1) & 0xFFFFFFFF) >> 29)
 
     def order(p):
         srt = torch.argsort(p, stable=True)
@@ -53,10 +53,16 @@ def main():
         return {k: (v.view(torch.int32)[idx].view(v.dtype) if v.dtype == torch.uint32 else v[idx]).contiguous()
                 for k, v in cols.items()}
 
+    # control: a batch of class-0 packets only (every XCD touches the same 1/8 slice)
+    def only(p, r=0):
+        idx = (p == r).nonzero().squeeze(1)
+        return idx[: idx.numel() // (8 * B) * (8 * B)]
+
     pe, ne = order(part(cols["dst"]))
     pi, ni = order(part(cols["src"]))
     N = args.packets
-    cases = [("generated", torch.arange(N, device=dev)), ("egress-key XCD partition", pe), ("ingress-key XCD partition", pi)]
+    cases = [("generated", torch.arange(N, device=dev)), ("egress-key XCD partition", pe), ("ingress-key XCD partition", pi),
+             ("egress-key class 0 only", only(part(cols["dst"]))), ("ingress-key class 0 only", only(part(cols["src"])))]
     out = torch.empty(2 * N * 8, dtype=torch.uint8, device=dev)
     ref = None
     for name, idx in cases:
