@@ -303,25 +303,25 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
                                              uint4* __restrict__ lb_out, unsigned long long* __restrict__ counters, int count,
                                              const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
                                              uint2* __restrict__ gout, uint4* __restrict__ park, uint32_t* pkt_lane,
-                                             uint32_t pkt_stride) {
+                                             uint32_t pkt_stride, uint32_t i_hi) {
   // Ingress launch: only the egress action of the egress half is read here; nothing of it is held
   // over the walk (the result is stored as a half).
   uint32_t ea = 0;
   if (kStage == 2) ea = (orig ? mid[i].y : reinterpret_cast<const uint2*>(out)[2 * i].y) & 0xffu;
   // caller index of this packet (loaded where a result is stored: no register held over the walk)
-  auto at = [&]() -> uint64_t { return orig ? uint64_t(orig[i]) : i; };
+  auto at = [&](uint64_t k) -> uint64_t { return orig ? uint64_t(orig[k]) : k; };
   // the ingress launch's result: its half of the verdict pair in grouped order into gout
   // (unpermute_kernel joins it with the egress half in mid and stores the pair in caller order with
   // whole-line stores); ungrouped, the ingress half of the pair the egress launch stored; grouped
   // without the un-permute, the pair at the caller index with the egress half re-read from mid
-  auto store2 = [&](uint32_t conj, uint32_t packed) {
+  auto store2 = [&](uint64_t k, uint32_t conj, uint32_t packed) {
     if (gout) {
-      gout[i] = make_uint2(conj, packed);
+      gout[k] = make_uint2(conj, packed);
     } else if (orig) {
-      const uint2 e = mid[i];
-      out[at()] = make_uint4(e.x, e.y, conj, packed);
+      const uint2 e = mid[k];
+      out[at(k)] = make_uint4(e.x, e.y, conj, packed);
     } else {
-      reinterpret_cast<uint2*>(out)[2 * i + 1] = make_uint2(conj, packed);
+      reinterpret_cast<uint2*>(out)[2 * k + 1] = make_uint2(conj, packed);
     }
   };
   uint32_t src = pk.src[i], dst = pk.dst[i];
@@ -344,7 +344,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
     uint32_t lb[4];
     const uint32_t f = lb_stage(ep.svc, src, dst, sport, dport, proto, svc_group, out_port, dest, lb);
     // grouped with the un-permute (gout): results in grouped order, unpermute_kernel stores them
-    if (lb_out) lb_out[gout ? i : at()] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
+    if (lb_out) lb_out[gout ? i : at(i)] = make_uint4(lb[0], lb[1], lb[2], lb[3]);
     if (kStage == 1) park[i] = make_uint4(dst, (dport & 0xffffu) | (dest << 16), out_port, svc_group);
     if (f & GPC_LB_NO_ENDPOINT) {  // EndpointDNAT serviceNoEndpointFlow: rejected before the policy stages
       const uint32_t rj = pack_verdict(GPC_ACT_REJECT, GPC_VTABLE_ENDPOINT_DNAT, 0, 0);
@@ -356,16 +356,16 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
       } else if (kStage == 1) {
         out[i] = make_uint4(0u, rj, 0u, 0u);
       } else {
-        out[at()] = make_uint4(0u, rj, 0u, 0u);
+        out[at(i)] = make_uint4(0u, rj, 0u, 0u);
       }
       return;
     }
   } else if (kStage != 2 && lb_out) {
-    lb_out[at()] = make_uint4(0u, 0u, 0u, 0u);
+    lb_out[at(i)] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
-      if (orig) store2(0u, 0u);  // ingress NONE
+      if (orig) store2(i, 0u, 0u);  // ingress NONE
       return;
     }
     if (kSvc) {  // the fields the egress launch's Service stage rewrote
@@ -377,7 +377,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
       svc_group = pv.w;
     }
     if (const uint32_t b = ingress_bypass(ep.hdr->isc, dest, ct_mark)) {  // IngressSecurityClassifier
-      store2(0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
+      store2(i, 0u, pack_verdict(b & 0xffu, 0, 0, (b >> 8) ? 2u : 0u));
       return;
     }
   }
@@ -394,9 +394,18 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   make_pkt(p, src, dst, sport, dport, proto, out_port, pk.in_port ? pk.in_port[i] : 0u, svc_group,
            pk.tun_id ? pk.tun_id[i] : 0u, ct_src, ct_dst, pk.ct_state ? pk.ct_state[i] : uint32_t(GPC_CT_NEW | GPC_CT_TRK),
            view_bloom_axes(im));
-  auto count_one = [&](const StageOut& s) {  // a stage's Metric-table counters
+  // The packet index is parked in the lane's LDS column for the walk and read back after it
+  // ("memory" clobber: the reload, and that of the packet's ct_state in count_stage, cannot be
+  // forwarded from the registers they were stored from), so neither is held in a VGPR over the
+  // walk -- they were the base kernels' only spills (20-28 B of scratch per lane).
+  pkt_lane[kPktWords * pkt_stride] = uint32_t(i);
+  auto late = [&]() -> uint64_t {
+    asm volatile("" ::: "memory");
+    return (uint64_t(i_hi) << 32) | pkt_lane[kPktWords * pkt_stride];
+  };
+  auto count_one = [&](const StageOut& s, uint64_t k) {  // a stage's Metric-table counters
     if (!count || !s.counted) return;
-    const uint32_t len = pk.len ? pk.len[i] : 0u;
+    const uint32_t len = pk.len ? pk.len[k] : 0u;
     unsigned long long* const copy = counters + size_t(blockIdx.x & ep.ctr_mask) * ep.ctr_stride;
     count_stage(s.v, s.slot, len, p.ax[AX_CTST], [&](uint32_t w, unsigned long long v) { atomicAdd(&copy[w], v); });
   };
@@ -405,10 +414,11 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
     // ingress walk, so nothing of it is held over that walk.
     const uint32_t byp = ingress_bypass(ep.hdr->isc, dest, ct_mark);
     const StageOut s1 = walk_stage<kDelta, false>(im, p, 1u, nullptr, nullptr);
-    count_one(s1);
+    const uint64_t i1 = late();
+    count_one(s1, i1);
     uint2* const o2 = reinterpret_cast<uint2*>(out);
-    if (gout) mid[i] = make_uint2(s1.v.conj, s1.v.packed);  // grouped order (un-permuted afterwards)
-    else o2[2 * at()] = make_uint2(s1.v.conj, s1.v.packed);
+    if (gout) mid[i1] = make_uint2(s1.v.conj, s1.v.packed);  // grouped order (un-permuted afterwards)
+    else o2[2 * at(i1)] = make_uint2(s1.v.conj, s1.v.packed);
     const uint32_t a1 = s1.v.packed & 0xffu;
     uint32_t gc = 0u, gp = 0u;  // ingress NONE: dropped in egress
     if (a1 != RV_DROP && a1 != RV_REJECT && a1 != RV_ISO_DROP) {
@@ -416,21 +426,23 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
         gp = pack_verdict(byp & 0xffu, 0, 0, (byp >> 8) ? 2u : 0u);
       } else {
         const StageOut s2 = walk_stage<kDelta, false>(im, p, 4u, nullptr, nullptr);
-        count_one(s2);
+        count_one(s2, late());
         gc = s2.v.conj;
         gp = s2.v.packed;
       }
     }
-    if (gout) gout[i] = make_uint2(gc, gp);
-    else o2[2 * at() + 1] = make_uint2(gc, gp);
+    const uint64_t i2 = late();
+    if (gout) gout[i2] = make_uint2(gc, gp);
+    else o2[2 * at(i2) + 1] = make_uint2(gc, gp);
     return;
   }
   const StageOut s = walk_stage<kDelta, false>(im, p, kStage == 2 ? 4u : 1u, nullptr, nullptr);
-  count_one(s);
+  const uint64_t il = late();
+  count_one(s, il);
   const VerdictOut e = s.v, g = s.v;
-  if (kStage == 2) store2(g.conj, g.packed);
-  else if (kStage == 1 && orig) mid[i] = make_uint2(e.conj, e.packed);
-  else out[i] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
+  if (kStage == 2) store2(il, g.conj, g.packed);
+  else if (kStage == 1 && orig) mid[il] = make_uint2(e.conj, e.packed);
+  else out[il] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
 }
 
 // kDelta: the epoch mode (core.hpp kModeBase / kModeExt / kModeJournal).
@@ -440,7 +452,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
     uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
-  __shared__ uint32_t pkt_lds[kPktWords * block_threads<kSort>()];
+  __shared__ uint32_t pkt_lds[(kPktWords + 1) * block_threads<kSort>()];  // + the parked packet index
 #if defined(GPC_STAMPS)
   {
     uint32_t* st = gpc_stamp_lds();
@@ -458,7 +470,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
   if constexpr (kSort) i = sorted_index<kStage>(ep, pk, n, out, mid, block_base, pkt_lds);  // own instantiation: the plain kernel has no barrier
   if (i >= n) return;
   classify_one<kDelta, kSvc, kStage>(ep, pk, i, out, lb_out, counters, count, orig, mid, gout, park,
-                                     pkt_lds + threadIdx.x, block_threads<kSort>());
+                                     pkt_lds + threadIdx.x, block_threads<kSort>(), uint32_t(block_base >> 32));
 #if defined(GPC_STAMPS)
   };
   body();
