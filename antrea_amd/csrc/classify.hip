@@ -400,7 +400,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   // walk -- they were the base kernels' only spills (20-28 B of scratch per lane).
   pkt_lane[kPktWords * pkt_stride] = uint32_t(i);
   auto late = [&]() -> uint64_t {
-    asm volatile("" ::: "memory");
+    lds_reload();
     return (uint64_t(i_hi) << 32) | pkt_lane[kPktWords * pkt_stride];
   };
   auto count_one = [&](const StageOut& s, uint64_t k) {  // a stage's Metric-table counters
@@ -412,9 +412,12 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   if constexpr (kStage == 0) {
     // Both stages in one launch (Services): the egress half is counted and stored before the
     // ingress walk, so nothing of it is held over that walk.
-    const uint32_t byp = ingress_bypass(ep.hdr->isc, dest, ct_mark);
+    // (the ingress bypass is parked next to the index: nothing of the Service stage is held in a
+    // register over the egress walk)
+    pkt_lane[(kPktWords + 1) * pkt_stride] = ingress_bypass(ep.hdr->isc, dest, ct_mark);
     const StageOut s1 = walk_stage<kDelta, false>(im, p, 1u, nullptr, nullptr);
     const uint64_t i1 = late();
+    const uint32_t byp = pkt_lane[(kPktWords + 1) * pkt_stride];
     count_one(s1, i1);
     uint2* const o2 = reinterpret_cast<uint2*>(out);
     if (gout) mid[i1] = make_uint2(s1.v.conj, s1.v.packed);  // grouped order (un-permuted afterwards)
@@ -452,7 +455,7 @@ __global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
     uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
   // per-lane packet axes / filter bits: a [word][lane] table in LDS (core.hpp Pkt)
-  __shared__ uint32_t pkt_lds[(kPktWords + 1) * block_threads<kSort>()];  // + the parked packet index
+  __shared__ uint32_t pkt_lds[(kPktWords + 2) * block_threads<kSort>()];  // + the parked index and bypass
 #if defined(GPC_STAMPS)
   {
     uint32_t* st = gpc_stamp_lds();

@@ -258,6 +258,9 @@ struct Pkt {
   uint32_t l4m;  // filter bit of (proto class, tp_dst block) (bits 20-31)
   GPC_HD Pkt(uint32_t* store, uint32_t stride) : ax{store, stride}, fm{store + AX_N * stride, stride}, l4m(0) {}
 };
+// Compiler barrier: values stored to LDS before it are reloaded after it, not forwarded from the
+// registers they were stored from (so those registers are free during the code in between).
+GPC_HD void lds_reload() { asm volatile("" ::: "memory"); }
 
 // Partial decision of one image for one table, packed (it is live across the table loop):
 //   h   = best hard match: priority | verdict << 16 | found << 24 | tie << 25
@@ -1957,7 +1960,10 @@ GPC_HD TablePart merge_ext(const View& v, const TablePart& a, const TablePart& e
 // instantiation compiles neither the journal nor the extension code.
 template <int kMode>
 GPC_HD TableResult eval_table(const View& v, uint32_t table, const Pkt& p) {
-  ExtProbe xp;  // point extensions: presence words in flight during the base walk
+  // point extensions: presence words in flight during the base walk. (Waiting for them first and
+  // parking the result in LDS (Pkt::park) cut the extension kernels' spills from 9-10 to 8 VGPRs
+  // but made C5 1 ms slower per step: the wait costs more than the scratch traffic.)
+  ExtProbe xp;
   const bool ext = kMode >= kModeExt && v.ext;
   if (ext) xp = ext_begin(v, table, p);
   TablePart acc = eval_part(v.base, table, p);

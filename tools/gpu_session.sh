@@ -7,7 +7,7 @@
 #   tests   pytest -m gpu (one process, per-test timeout)
 #   smoke   __graft_entry__.smoke()
 #   bench   python bench.py (default C3 line: PMC passes, parity stamp, CPU baseline)
-#   cfg:X   bench.py --config X (C1, C2, C4, C5) ; v6 = C3 in IPv6
+#   cfg:X   bench.py --config X (C1, C2, C2g, C4, C5) ; v6 = C3 in IPv6, v6m48 = the same over four /48s
 #   kt      rocprofv3 --kernel-trace --stats over a short bench run
 #   sq[:X]  rocprofv3 SQ counters (config X, default C3) ; tcc[:X] TCC hit / miss / EA read requests
 #   fetch / write  FETCH_SIZE / WRITE_SIZE of C3
@@ -49,9 +49,15 @@ for s in $STEPS; do
       cat "$O/bench.json" ;;
     cfg:*)
       c=${s#cfg:}; step "bench $c"
-      if [ "$c" = v6 ]; then a="--family 6"; else a="--config $c"; fi
-      timeout -k 10 900 python -u bench.py $a --keep-pmc "$O/pmc_bench" > "$O/bench_$c.json" 2> "$O/bench_$c.err" || { tail -20 "$O/bench_$c.err"; exit 1; }
-      cat "$O/bench_$c.json" ;;
+      case $c in
+        v6) a="--family 6" ;;
+        v6m48) a="--family 6 --v6-embed multi48 --no-cpu-baseline" ;;
+        C2g) a="--config C2g --no-cpu-baseline" ;;
+        C5) a="--config C5 --steps ${C5_STEPS:-3500} --warmup 20" ;;
+        *) a="--config $c" ;;
+      esac
+      timeout -k 10 900 python -u bench.py $a --keep-pmc "$O/pmc_$c" > "$O/bench_$c.json" 2> "$O/bench_$c.err" || { tail -20 "$O/bench_$c.err"; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'], d['kernel_ms_by_launch'], (d.get('parity') or {}).get('mismatches'))" "$O/bench_$c.json" $c ;;
     kt)
       step "rocprof kernel trace"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- \

@@ -12,7 +12,7 @@ for l in sys.stdin:
     if m:
         name = m.group(1)
         t = re.search(r"classify_kernelIL([bi]\d)EL(b\d)ELi(\d)EL(b\d)E", name)
-        cur = {"kernel": "classify<delta=%s,svc=%s,stage=%s,sort=%s>" % (t.group(1)[1], t.group(2)[1], t.group(3),
+        cur = {"kernel": "classify<mode=%s,svc=%s,stage=%s,sort=%s>" % (t.group(1)[1], t.group(2)[1], t.group(3),
                t.group(4)[1]) if t else re.sub(r"^_ZN3gpc\d+", "", name)[:40]}
         rows.append(cur)
         continue
