@@ -1339,6 +1339,9 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     }
   }
   GPC_MARK(ST_DRV);
+  // the hard match is packed now: of it only rH stays live (the scan's bound), and "found" is
+  // res.h's kHFound bit (a separate flag was the base kernels' last spilled register)
+  if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
   if (th.bits_off && !im.dead) {  // bit-parallel table (tombstones: the scan below honours them)
     const BitTable& bt = *reinterpret_cast<const BitTable*>(im.blob + th.bits_off);
     uint32_t s0 = bt.absent[0], s1 = bt.absent[1], s2 = bt.absent[2];
@@ -1378,11 +1381,10 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       }
     }
     uint32_t done = s0 & s1 & s2;
-    if (rH != th.end_off) {  // only rules ranked above the hard match
+    if (res.h & kHFound) {  // only rules ranked above the hard match
       const uint32_t np_ = rH == th.hf[0].roff ? bt.hard_prefix[0] : bt.hard_prefix[1];
       done &= np_ >= 32u ? 0xffffffffu : (1u << np_) - 1u;
     }
-    if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
     if (done) {
       const uint32_t w = uint32_t(__builtin_ctz(done));
       GPC_TOUCH(&bt.info[2 * w], 8);
@@ -1397,10 +1399,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     return res;
   }
   const uint32_t n0 = th.n_idx[0], n1 = th.n_idx[1];
-  if (th.n_cidx == 0 && n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) {  // no soft rules
-    if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
-    return res;
-  }
+  if (th.n_cidx == 0 && n0 == 0 && th.always_n[0] == 0 && n1 == 0 && th.always_n[1] == 0) return res;  // no soft rules
   // --- driver clause: the composite driver when the table has one (a subset of either plain
   // driver's candidates, table-uniform branch), else the clause with fewer candidate records
   uint32_t lo0[kIdxPerClause], hi0[kIdxPerClause], lo1[kIdxPerClause], hi1[kIdxPerClause];
@@ -1590,7 +1589,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       if (rec_has_act(w2)) {
         have = 1;
         win = off;
-      } else if (rH != th.end_off) {
+      } else if (res.h & kHFound) {
         have = 1;
         noact = kSNoAct;
       }
@@ -1598,7 +1597,6 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     if (!more) done = true;
   }
   GPC_MARK(ST_TAIL);
-  if (rH != th.end_off) res.h = hprio | (hverdict << 16) | kHFound | htie;
   if (have) {
     res.s = level | kSHave | noact | (level_done > 1 ? kSTie : 0u);
     res.win = win;
