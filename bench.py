@@ -498,7 +498,9 @@ def main():
             time.sleep(0.01)
         lat.clear()
     _log("timed region: %d steps of %d packets" % (args.steps, n))
-    clf.set_launch_timing(args.steps)  # HIP events around each kernel of the timed calls (gpc_launch_times)
+    # HIP events around each kernel of the timed calls (gpc_launch_times; the library keeps at most
+    # 4096 calls: a longer run, e.g. C5 over 30 s, is timed per kernel over its first 4096 steps)
+    clf.set_launch_timing(min(args.steps, 4096))
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for i in range(args.steps):
