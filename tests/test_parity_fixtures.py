@@ -56,6 +56,24 @@ def test_emu_vs_oracle_fixture(config, composite, monkeypatch):
     assert m == {k: v for k, v in f["metrics"].items() if any(v)}
 
 
+@pytest.mark.parametrize("config", ["C2", "C3"])
+@pytest.mark.parametrize("layout", ["0", "1", "2"])
+def test_emu_vs_oracle_fixture_bucket_layouts(config, layout, monkeypatch):
+    """Composite sub-index layouts (core.hpp SubIdx.fmt), each against the oracle fixture:
+    "0" round-4 offset pairs + presence maps, "1" bucket directories read eagerly, "2" directories
+    read after the value map (the default picks 1 or 2 per table). C3's directories hold overflow
+    buckets (7 or more entries under one (key, value): pointer entry + separate list)."""
+    monkeypatch.setenv("GPC_COMPOSITE_DIR", layout)
+    f = fx.load(config)
+    wl, cols = fx.packets(config)
+    c = gpc.Classifier()
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    emu.commit_host(c)
+    res = parity.compare(emu.classify(c, cols), f["verdicts"])
+    assert res["mismatches"] == 0, res
+
+
 def test_c_oracle_metrics_parse_like_the_reference():
     """The C oracle's Metric dump parses with the reference parser restated in oracle/compiler.py
     into the same metrics the Python oracle reports for the same packets (C1)."""
