@@ -73,9 +73,9 @@ enum Axis : uint8_t {
 //   SK_IVAL  2n words, sorted disjoint [lo,hi]     SK_XIVAL  1 word: offset of the 2n words
 //   SK_PTS   n words, sorted points                SK_XPTS   1 word: offset of the n words
 //   SK_BOX   7n words (val[3], mask[3], axes|nt)   SK_XBOX   1 word: offset of the 7n words
-//   SK_HASH  no data: the clause's values on `axis` live in the image-wide point hash, key
-//            (record offset, axis, v) -- clauses that are large sets of exact values (AddressGroup
-//            members, Pod ofports); driver entries probe it during the candidate scan
+//   SK_HASH  1 word: the high word of the clause's point-set keys (set_key). The clause's values on
+//            `axis` live in the image-wide point hash -- clauses that are large sets of exact values
+//            (AddressGroup members, Pod ofports); driver entries probe it during the candidate scan
 //   SK_ALWAYS
 enum SegKind : uint8_t { SK_ALWAYS = 0, SK_IVAL = 1, SK_PTS = 2, SK_HASH = 3, SK_BOX = 4, SK_XIVAL = 5, SK_XPTS = 6, SK_XBOX = 7 };
 enum RuleKind : uint8_t { RK_SOFT = 0, RK_HARD = 1 };
@@ -344,11 +344,12 @@ GPC_HD uint32_t cbucket_of(uint32_t band, uint32_t bits, uint32_t v, uint32_t x)
   const uint32_t key = v >> ip_band_shift(band);
   return mix32((key * 0x9e3779b1u) ^ cx_hash(x) ^ (band * 0x68e31da4u)) >> (32 - bits);
 }
-// Point-hash key of value v on `axis` of the record at word offset `off` (16-word aligned, < 2^28):
-// (off / 16) << 4 | axis in the high word. ~0 (empty slot) is never a key.
-GPC_HD uint64_t point_key(uint32_t off, uint32_t axis, uint32_t v) {
-  return (uint64_t(((off >> 4) << 4) | axis) << 32) | v;
-}
+// Point-hash key of value v in point set `sid` on `axis` (round 5: sets are interned per image, so
+// the rules that share an AddressGroup share its keys -- C2g: 16 sets of 10 000 members instead of
+// 10 M (record, value) keys): high word 1 << 31 | sid << 4 | axis. ~0 (empty slot) is never a key.
+constexpr uint32_t kPointSetMax = 1u << 20;  // set ids fit the 20 filter bits of a probe entry
+GPC_HD uint32_t set_key_hi(uint32_t sid, uint32_t axis) { return 0x80000000u | (sid << 4) | axis; }
+GPC_HD uint64_t set_key(uint32_t hi, uint32_t v) { return (uint64_t(hi) << 32) | v; }
 constexpr uint32_t kHashSlots = 2;  // 16-B buckets, two choices: one 16-B load per choice
 // The two cuckoo choices take the low and the high half of one mix (one 64-bit mix per probe).
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
@@ -1014,7 +1015,7 @@ GPC_HD bool clause_match(const Img& im, uint32_t roff, const W* c, const Pkt& p)
       case SK_ALWAYS: return true;
       case SK_IVAL: hit = ival_hit(w, n, p.ax[axis]); w += 2 * n; break;
       case SK_PTS: hit = pts_hit(w, n, p.ax[axis]); w += n; break;
-      case SK_HASH: hit = hash_contains(im, point_key(roff, axis, p.ax[axis])); break;
+      case SK_HASH: GPC_TOUCH(w, 4); hit = hash_contains(im, set_key(*w, p.ax[axis])); w++; break;
       case SK_BOX: hit = box_hit(w, n, p); w += kBoxWords * n; break;
       case SK_XIVAL: GPC_TOUCH(w, 4); hit = ival_hit(blob + *w, n, p.ax[axis]); w++; break;
       case SK_XPTS: GPC_TOUCH(w, 4); hit = pts_hit(blob + *w, n, p.ax[axis]); w++; break;
@@ -1083,7 +1084,7 @@ GPC_HD bool rule_match(const Img& im, const W* rec, uint32_t w2, const uint32_t*
     const uint32_t roff = uint32_t(rec - blob);
 #pragma unroll
     for (int k = 0; k < kMaxClauses; k++)
-      if (ok & ((hsh >> k) & 1u)) ok = hash_contains(im, point_key(roff, (dsc[3 * k] >> 4) & 15u, x[k]));
+      if (ok & ((hsh >> k) & 1u)) ok = hash_contains(im, set_key(dsc[3 * k + 1], x[k]));
   }
   // array clauses: window [l, h) of elements still to look at, per clause, in lock step
   while (GPC_WAVE_ANY(ok & ((h[0] > l[0]) | (h[1] > l[1]) | (h[2] > l[2])))) {
@@ -1160,7 +1161,7 @@ GPC_HD bool hard_fast_match(const Img& im, const HardFast& hf, const Pkt& p) {
     const uint32_t A = hf.d[3 * k], B = hf.d[3 * k + 1], C = hf.d[3 * k + 2], kind = A & 15u;
     const uint32_t v = p.ax[(A >> 4) & 15u];
     if (kind == FK_HASH) {
-      ok = ok & hash_contains(im, point_key(hf.roff, (A >> 4) & 15u, v));
+      ok = ok & hash_contains(im, set_key(B, v));
     } else {
       const bool r = kind == FK_IV1 ? (B <= v) & (v <= C)
                      : kind == FK_MK1 ? (v & C) == B
@@ -1173,11 +1174,15 @@ GPC_HD bool hard_fast_match(const Img& im, const HardFast& hf, const Pkt& p) {
 }
 
 // xv: the packet's value of the table's composite axis (exact-value entries; any value elsewhere).
+// kSetProbes (base images): a probe entry's low 20 bits are its point set's id, not Bloom bits --
+// the probe itself is the test (a set large enough for the point hash saturates 20 Bloom bits).
+template <bool kSetProbes = true>
 GPC_HD bool entry_pass(const Pkt& p, const Ent& e, uint32_t xv) {  // branch-free
   const uint32_t bax = e.x & 15u, iax = (e.x >> 4) & 15u;
   const bool l4 = (e.y & p.l4m) != 0u;
-  // Bloom axis < 8: IP / exact-axis bits; 8..14 (probe entry): second service Bloom; 15: none
-  const bool bl = (bax == kFiltNoAxis) | ((e.y & p.fm[bax & 7u]) != 0u);
+  // Bloom axis < 8: IP / exact-axis bits; 8..14 (probe entry): set id (base) or the probed clause's
+  // Bloom bits (journal); 15: none
+  const bool bl = (bax == kFiltNoAxis) | (kSetProbes & (bax >= 8u)) | ((e.y & p.fm[bax & 7u]) != 0u);
   const uint32_t v = p.ax[iax < AX_N ? iax : 0];
   const bool iv = (iax == kFiltNoAxis) | ((e.lo <= v) & (v <= e.hi));
   return ((e.x & kEntExactX) ? e.y == xv : l4 & bl) & iv;
@@ -1266,7 +1271,7 @@ GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const ui
         const uint32_t pax = (ev[u].x & 15u) - 8u;
         const bool need = ps[u] & (pax < 7u);
         if (GPC_WAVE_ANY(need)) {
-          if (need) ps[u] = hash_contains(im, point_key(ent_off(ev[u].x), pax, p.ax[pax]));
+          if (need) ps[u] = hash_contains(im, set_key(set_key_hi(ev[u].y & (kPointSetMax - 1u), pax), p.ax[pax]));
         }
       }
     }
@@ -1767,7 +1772,7 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
       f.y = ew[5];
       f.lo = ew[6];
       f.hi = ew[7];
-      if (!entry_pass(p, f, 0u)) continue;  // (journal entries are never exact-value entries)
+      if (!entry_pass<false>(p, f, 0u)) continue;  // (journal entries are never exact-value entries)
       const uint32_t off = ew[3];
       const uint32_t* rec = pool + off;
       GPC_TOUCH(rec, 4 * kRecLine);

@@ -84,6 +84,7 @@ struct RuleB {
   bool counted = false;
   uint8_t tier = 0;
   bool pin = false;  // the action flow sends the packet to the controller (DNS interception)
+  uint32_t set_hi[kMaxClauses] = {0, 0, 0};  // base images: key word of a point-hash clause's set
 };
 
 // Point extensions (core.hpp ExtHdr, Journal::apply): an atom's identity and a rule's record
@@ -442,6 +443,7 @@ struct PendingSeg {
   uint8_t kind = SK_ALWAYS, axis = 0;
   std::vector<uint32_t> data;  // IVAL: lo,hi pairs ; PTS / HASH: points ; BOX: 7 words per box
   uint32_t n = 0;
+  uint32_t key_hi = 0;         // HASH: the interned point set's key word (core.hpp set_key_hi)
 };
 
 // A clause that is a large set of exact values on one axis (AddressGroup members as /32s, Pod
@@ -545,6 +547,7 @@ std::vector<uint32_t> encode_clause(const std::vector<PendingSeg>& segs, std::ve
                     (kind == SK_BOX && s.n > kInlineBoxes);
     if (external) kind = kind == SK_IVAL ? SK_XIVAL : kind == SK_PTS ? SK_XPTS : SK_XBOX;
     w.push_back(kind | (uint32_t(s.axis) << 4) | (s.n << 8));
+    if (kind == SK_HASH) w.push_back(s.key_hi);
     if (kind == SK_ALWAYS || kind == SK_HASH) continue;
     if (external) {
       while (ext->size() % 16) ext->push_back(0);
@@ -578,6 +581,7 @@ Fcd fast_clause(const std::vector<PendingSeg>& segs) {
       return f;
     case SK_HASH:
       f.a = FK_HASH | ax;
+      f.b = s.key_hi;
       return f;
     case SK_IVAL:
     case SK_PTS:
@@ -875,8 +879,10 @@ std::array<uint32_t, 4> entry_of(const RuleB& r, int d, uint32_t off, const uint
   bool have_ip = false, have_l4 = false;
   uint8_t pax;
   const int pc = probe_clause(r, d, &pax);
-  if (pc >= 0) {  // probe entry: the Bloom bits are the probed clause's (probe_clause checked them)
+  if (pc >= 0) {  // probe entry: the probed set's id in base images (core.hpp entry_pass), else
+                   // the Bloom bits of the probed clause (probe_clause checked them)
     filt_clause_ip(r.clause[pc], &axis, &ipbits);
+    if (r.set_hi[pc]) ipbits = (r.set_hi[pc] >> 4) & (kPointSetMax - 1u);
     axis = 8u + pax;
     have_ip = true;
   }
@@ -2528,6 +2534,18 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
   B.w.reserve(1 << 20);
   for (int i = 0; i < 16; i++) B.w.push_back(0);  // keep offset 0 unused
   std::vector<uint64_t> hash_keys;
+  // point sets (core.hpp set_key), interned over the image: rules sharing an AddressGroup share keys
+  std::map<std::pair<uint8_t, std::vector<uint32_t>>, uint32_t> point_sets;
+  auto intern_set = [&](uint8_t axis, const std::vector<uint32_t>& pts) -> uint32_t {
+    auto it = point_sets.find({axis, pts});
+    if (it != point_sets.end()) return it->second;
+    const uint32_t sid = uint32_t(point_sets.size());
+    if (sid >= kPointSetMax) return 0u;
+    const uint32_t hi = set_key_hi(sid, axis);
+    point_sets.emplace(std::make_pair(axis, pts), hi);
+    for (uint32_t v : pts) hash_keys.push_back(set_key(hi, v));
+    return hi;
+  };
   uint32_t next_rid = 0;
   for (int t = 1; t <= 6; t++) {
     std::vector<RuleB*> rs;
@@ -2589,14 +2607,21 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
       // encode clauses, smallest first in the record
       std::vector<std::vector<uint32_t>> cw(r.n);
       std::vector<std::vector<std::pair<uint32_t, uint32_t>>> cp(r.n);
-      std::vector<PendingSeg> hsegs;  // point-hash segments: keys need the record offset
       Fcd fcd[3];
       uint32_t mk2[3][4] = {};  // FK_MKN with two boxes: their (value, mask) terms (inline hard rules)
       for (int k = 0; k < r.n; k++) {
         std::vector<PendingSeg> ps;
         clause_segments(r.clause[k], &ps);
+        r.set_hi[k] = 0;
         for (auto& sg : ps)
-          if (sg.kind == SK_HASH) hsegs.push_back(sg);
+          if (sg.kind == SK_HASH) {
+            sg.key_hi = intern_set(sg.axis, sg.data);
+            if (!sg.key_hi) {
+              out->error = "too many distinct point sets";
+              return -GPC_EINVAL;
+            }
+            r.set_hi[k] = sg.key_hi;
+          }
         cw[k] = encode_clause(ps, &ext, &cp[k]);
         fcd[k] = fast_clause(ps);
         if ((fcd[k].a & 15u) == FK_MKN && (fcd[k].a >> 8) == 2u) {
@@ -2647,8 +2672,6 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
         return -GPC_ENOMEM;
       }
       rec_off[rank] = base;
-      for (auto& sg : hsegs)
-        for (uint32_t v : sg.data) hash_keys.push_back(point_key(base, sg.axis, v));
       B.w.insert(B.w.end(), rec.begin(), rec.end());
       if (r.hard) {
         // inline copy for TableHdr.hf (core.hpp HardFast), if every clause has a one-word kind

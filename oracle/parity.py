@@ -231,8 +231,14 @@ class OracleWorker:
 
     def _ready(self, timeout=1800):
         if self.info is None:
-            if not self.conn.poll(timeout):
-                raise TimeoutError("oracle worker setup")
+            import sys
+            import time
+            t0 = time.time()
+            # a progress line every 30 s: a long setup (C2g: ~10 M flows) must not look like a hang
+            while not self.conn.poll(30):
+                if time.time() - t0 > timeout:
+                    raise TimeoutError("oracle worker setup")
+                print("[oracle] still setting up (%.0f s)" % (time.time() - t0), file=sys.stderr, flush=True)
             self.info = self.conn.recv()
         return self.info
 

@@ -22,8 +22,12 @@ def load():
     core = os.path.join(ROOT, "antrea_amd", "csrc", "core.hpp")
     os.makedirs(OUT, exist_ok=True)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(src), os.path.getmtime(core)):
+        # built under a private name and renamed into place: parallel test workers that rebuild at
+        # the same time never load a half-written library
+        tmp = "%s.%d.tmp" % (LIB, os.getpid())
         subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"),
-                        "-I" + os.path.join(ROOT, "antrea_amd", "csrc"), src, "-o", LIB], check=True)
+                        "-I" + os.path.join(ROOT, "antrea_amd", "csrc"), src, "-o", tmp], check=True)
+        os.replace(tmp, LIB)
     _lib = C.CDLL(LIB)
     _lib.gpc_emu_stats_arr = (C.c_ulonglong * 16).in_dll(_lib, "gpc_emu_stats")
     _lib.gpc_emu_site_arr = (C.c_ulonglong * 2048).in_dll(_lib, "gpc_emu_site_lines")
