@@ -1206,11 +1206,13 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size();
     if (total > kCompositeMaxEntries) continue;
     std::vector<std::pair<uint32_t, std::array<uint32_t, 4>>> be;
-    // 2^extra buckets per entry: fewer hash collisions per probe. Measured (64M packets, C3 / C2):
-    // extra 0 -> 10.48 / 10.98 ms, 1 -> 10.12 / 10.25 ms, 2 -> 10.10 / 10.05 ms with 40 % more image;
+    // 2^extra buckets per entry: fewer hash collisions per probe. Round 4 (offset pairs, C3 / C2):
+    // extra 0 -> 10.48 / 10.98 ms, 1 -> 10.12 / 10.25 ms, 2 -> 10.10 / 10.05 ms with 40 % more image.
+    // Round 5 (bucket directories: a bucket costs 0.5 B of directory, not 4 B of offsets): 1 -> 4.756
+    // / 7.402 ms, 2 -> 4.718 / 7.193 ms for 2-4 MB more image (profiles/r05zd_extra_bits.txt).
     // GPC_COMPOSITE_EXTRA_BITS overrides (experiments)
     const char* xe = std::getenv("GPC_COMPOSITE_EXTRA_BITS");
-    const uint32_t extra = xe ? uint32_t(std::min(3, std::max(0, std::atoi(xe)))) : 1u;
+    const uint32_t extra = xe ? uint32_t(std::min(3, std::max(0, std::atoi(xe)))) : 2u;
     // core.hpp SubIdx fmt: bucket directories (1: read in the value-map word's round, where the map
     // cannot filter -- an exact non-IP value axis; 2: after it, an IP value axis). GPC_COMPOSITE_DIR
     // overrides (experiments): 0 = offset pairs (+ presence maps), 1 or 2 for every table
