@@ -28,6 +28,7 @@ Rank 0 at N = 1 also (all after the timed region, none of it timed):
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import re
 import os
@@ -376,9 +377,190 @@ def _roofline(pmc, kern_ms, n, b_in, b_out, lbar, launches):
     return rl
 
 
-def main():
+class _HipPath:
+    """The product data path of one rank: gpc_classify* on this rank's GPU (the HIP kernels of
+    libgpc.so), timed with HIP events on the launch stream, counters all-reduced over RCCL."""
+    label = None
+
+    def __init__(self, local):
+        import torch
+        self.torch = torch
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+
+    def init_dist(self):
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=self.dev)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def stream(self, own):
+        return self.torch.cuda.Stream(self.dev) if own else self.torch.cuda.current_stream(self.dev)
+
+    def event(self):
+        return self.torch.cuda.Event(enable_timing=True)
+
+    def bind(self, clf, v6):
+        self.clf = clf
+        self.fn = clf.classify6_device if v6 else clf.classify_device
+
+    def commit(self):
+        self.clf.commit()
+
+    def classify(self, soa, n, out, count, stream):
+        self.fn(soa, n, out.data_ptr(), count=count, stream=stream.cuda_stream)
+
+    def reset_counters(self):
+        self.clf.reset_counters()
+
+    def set_launch_timing(self, k):
+        self.clf.set_launch_timing(k)
+
+    def launch_times(self):
+        return self.clf.launch_times()
+
+    def counters(self):
+        """The library's device counters, wrapped zero-copy (None when counting is off)."""
+        from antrea_amd import dist as gdist
+        ptr, slots = self.clf.counters()
+        return gdist.device_counters(ptr, len(slots), self.dev) if ptr and slots else None
+
+
+class _HostEmuPath(_HipPath):
+    """TEST-ONLY stand-in for _HipPath (GPC_BENCH_HOST_EMU=1; tests/test_bench_host.py): runs
+    bench's multi-rank plumbing -- rank launch, gloo rendezvous, per-rank launch times, counter
+    all-reduce, rank-0 parity stamp -- on a host without a GPU. The classify call is the host
+    emulation of the same committed image (tests/emu: core.hpp compiled with g++), so the parity
+    stamp is still a real comparison. Refuses to run where a GPU is visible, and the line says
+    data: "host-emulation test stub": it is never a measurement."""
+    label = "host-emulation test stub (not a measurement)"
+
+    def __init__(self, local):
+        import torch
+        if torch.cuda.is_available():
+            raise SystemExit("GPC_BENCH_HOST_EMU is a CPU test hook; unset it on a GPU host")
+        from tests import emu
+        self.torch, self.emu = torch, emu
+        self.dev = torch.device("cpu")
+        self.times = []
+        self.timing = 0
+        self.cnt = None
+
+    def init_dist(self):
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    def sync(self):
+        pass
+
+    def stream(self, own):
+        return None
+
+    def event(self):
+        class Ev:
+            def record(self, stream=None):
+                self.t = time.perf_counter()
+
+            def elapsed_time(self, other):
+                return (other.t - self.t) * 1e3
+        return Ev()
+
+    def bind(self, clf, v6):
+        if v6:
+            raise SystemExit("GPC_BENCH_HOST_EMU: IPv4 only")
+        self.clf = clf
+
+    def commit(self):
+        self.emu.commit_host(self.clf)
+        n = self.clf.image_stats()["n_counter_slots"]
+        if self.cnt is None or len(self.cnt) < 3 * n:
+            self.cnt = self.torch.zeros(3 * max(1, n), dtype=self.torch.int64)
+
+    def classify(self, soa, n, out, count, stream):
+        import numpy as np
+        from antrea_amd import gpc
+        t0 = time.perf_counter()
+        cols = {}
+        for name, dt in gpc.PKT_COLUMNS.items():
+            p = getattr(soa, name)
+            if p:
+                cols[name] = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                                   shape=(n,))
+        c = self.cnt.numpy().view(np.uint64) if count else None
+        v = self.emu.classify(self.clf, cols, counters=c)
+        out.numpy()[:] = np.ascontiguousarray(v).view(np.uint8).reshape(-1)
+        if self.timing and len(self.times) < self.timing:
+            self.times.append((time.perf_counter() - t0) * 1e3)
+
+    def reset_counters(self):
+        self.cnt.zero_()
+
+    def set_launch_timing(self, k):
+        self.timing, self.times = k, []
+
+    def launch_times(self):
+        if not self.times:
+            return {}
+        return {"classify_both": {"launches": len(self.times), "total_ms": sum(self.times),
+                                  "mean_ms": sum(self.times) / len(self.times), "dropped": 0}}
+
+    def counters(self):
+        return self.cnt
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK,
+    LOCAL_RANK = GPU ordinal, WORLD_SIZE, MASTER_ADDR / a free MASTER_PORT), as
+    torch.distributed.run would. This process never imports torch nor touches a GPU (no exec:
+    the ranks are children). Rank 0's JSON line is printed; the first rank to fail stops the
+    others and its exit code is returned."""
+    import subprocess
+    import tempfile
+    port = _free_port()
+    procs = []
+    out0 = tempfile.TemporaryFile(mode="w+")
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=out0 if r == 0 else sys.stderr.fileno()))
+    _log("launched %d ranks (pids %s, port %d)" % (n, [p.pid for p in procs], port))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                _log("rank %d exited with %d: stopping the others" % (procs.index(p), code))
+                for q in live:
+                    q.kill()
+    out0.seek(0)
+    for line in out0.read().splitlines():  # the JSON line to stdout, anything a library printed to stderr
+        if rc == 0 and line.startswith("{"):
+            print(line, flush=True)
+        else:
+            print(line, file=sys.stderr)
+    return rc
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="N GPUs of this node, one rank per GPU (default: WORLD_SIZE, else 1); without a "
+                         "launcher bench.py starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3")
@@ -404,9 +586,18 @@ def main():
                          "node) instead of one process per GPU; N slots, one stream and host thread per slot")
     ap.add_argument("--multidev-devices", default="",
                     help="HIP ordinals of the --multidev slots (default 0..N-1; e.g. 0,0 = two slots on one GPU)")
-    args = ap.parse_args()
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
     if args.multidev:
         return main_multidev(args)
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is not None and args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%s (one rank per GPU)" % (args.gpus, env_world), file=sys.stderr)
+        return 2
+    if env_world is None and (args.gpus or 1) > 1:
+        return launch_ranks(args.gpus, argv)
     if args.family == 6 and args.config in ("C4", "C5"):
         ap.error("--family 6: C1-C3 only (no IPv6 AntreaProxy stage / delta epochs)")
     churn = args.config == "C5"
@@ -417,8 +608,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:  # the CPU baseline is an N=1 figure; every N still gets rank 0's parity stamp
+    host_emu = os.environ.get("GPC_BENCH_HOST_EMU") == "1"
+    if world > 1 or host_emu:  # the CPU baseline is an N=1 figure; every N still gets rank 0's parity stamp
         args.no_cpu_baseline = True
+    if host_emu:
+        args.no_traffic = True
     worker = None
     if rank == 0 and not (args.no_parity and args.no_cpu_baseline):
         # the CPU oracle (oracle compiler + C classifier) is prepared in a spawned process while
@@ -439,15 +633,12 @@ def main():
         for p in passes:
             pmc.update({k: v for k, v in (p or {}).items() if k != "by_kernel"})
         pmc["_passes"] = passes
+    dp = (_HostEmuPath if host_emu else _HipPath)(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dp.init_dist()
+    dev = dp.dev
 
-    from antrea_amd import dist as gdist
     from antrea_amd import gpc, workload
     from antrea_amd.build import build
     if rank == 0 or world == 1:
@@ -460,31 +651,30 @@ def main():
     wl = workload.CONFIGS["C3" if churn else args.config]()
     v6 = args.family == 6
     clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6, group_packets=args.group)
+    dp.bind(clf, v6)
     clf.initialize()
     clf.batch_install_policy_rule_flows(workload.to_ipv6(wl, embed=args.v6_embed).rules if v6 else wl.rules)
     if getattr(wl, "services", None):
         workload.install_services(clf, wl)
-    clf.commit()
+    dp.commit()
     t_build = time.time() - t0
 
     n = args.packets
     cols4 = workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED + rank, device=dev)
     cols = workload.packets_to_v6_torch(cols4, embed=args.v6_embed) if v6 else cols4
-    classify = clf.classify6_device if v6 else clf.classify_device
     out = torch.empty(2 * n * 8, dtype=torch.uint8, device=dev)
     soa = gpc.pkt_soa_device(cols)
     count = not args.no_count
-    stream = torch.cuda.Stream(dev) if churn else torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+    stream = dp.stream(own=churn)
     for _ in range(args.warmup):
-        classify(soa, n, out.data_ptr(), count=count, stream=sptr)
-    clf.reset_counters()
-    torch.cuda.synchronize(dev)
+        dp.classify(soa, n, out, count, stream)
+    dp.reset_counters()
+    dp.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    dp.sync()
+    starts = [dp.event() for _ in range(args.steps)]
+    ends = [dp.event() for _ in range(args.steps)]
     lat, th = [], None
     if churn:
         import threading
@@ -500,17 +690,17 @@ def main():
     _log("timed region: %d steps of %d packets" % (args.steps, n))
     # HIP events around each kernel of the timed calls (gpc_launch_times; the library keeps at most
     # 4096 calls: a longer run, e.g. C5 over 30 s, is timed per kernel over its first 4096 steps)
-    clf.set_launch_timing(min(args.steps, 4096))
-    torch.cuda.synchronize(dev)
+    dp.set_launch_timing(min(args.steps, 4096))
+    dp.sync()
     t_start = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
-        classify(soa, n, out.data_ptr(), count=count, stream=sptr)
+        dp.classify(soa, n, out, count, stream)
         ends[i].record(stream)
-    torch.cuda.synchronize(dev)
+    dp.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    dp.sync()
     elapsed = time.perf_counter() - t_start
     update = None
     if churn:
@@ -535,8 +725,8 @@ def main():
         if world > 1:
             update["ranks"] = _churn_converge(churn_ops, wl, dev, world)
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
-    launches = clf.launch_times()
-    clf.set_launch_timing(0)
+    launches = dp.launch_times()
+    dp.set_launch_timing(0)
     for t in launches.values():
         t["per_step"] = t["launches"] / args.steps
     rank_launches = _gather_rank_launch_ms(launches, dev, world) if world > 1 else None
@@ -545,19 +735,21 @@ def main():
         # before the control thread stopped), and the final epoch classifies the batch once more
         _log("oracle replay of %d ops" % len(churn_ops.log))
         update["oracle_replay"] = worker.churn(churn_ops.log)
-        classify(soa, n, out.data_ptr(), count=False, stream=sptr)
-        torch.cuda.synchronize(dev)
+        dp.classify(soa, n, out, False, stream)
+        dp.sync()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    counters_reduced = None
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         # per-rule counters: the path's only collective (RCCL all-reduce). The
         # library's device counters are wrapped zero-copy and reduced in place.
-        ptr, slots = clf.counters()
-        if count and ptr and slots:
-            cnt = gdist.device_counters(ptr, len(slots), dev)
-            torch.cuda.synchronize(dev)
+        cnt = dp.counters() if count else None
+        if cnt is not None:
+            from antrea_amd import dist as gdist
+            dp.sync()
             gdist.allreduce_counters(cnt)
-            torch.cuda.synchronize(dev)
+            dp.sync()
+            counters_reduced = {"slots": len(cnt) // 3, "packets": int(cnt.view(-1, 3)[:, 0].sum().item())}
     elapsed = float(t.item())
 
     total = n * args.steps * world
@@ -565,7 +757,7 @@ def main():
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
-        return
+        return 0
 
     import numpy as np
     from antrea_amd.gpc import VERDICT_DTYPE
@@ -613,7 +805,7 @@ def main():
         "metric": "Mpps classified (5-tuple->rule verdict) @100k rules, 1-8 MI355X; % HBM BW",
         "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "u32", "data": dp.label or "synthetic",
         "config": {"workload": args.config, "rules": len(wl.rules), "packets_per_gpu": n,
                    "flows": st["n_flows"],
                    "image_mb": round((clf.debug_image6()[1] * 4 if v6 else st["device_bytes"]) / 1e6, 1),
@@ -624,6 +816,7 @@ def main():
         "launches_per_step": round(sum(t["per_step"] for t in launches.values()), 2),
         "kernel_ms_by_launch": {k: round(t["mean_ms"], 3) for k, t in launches.items()},
         "kernel_ms_by_launch_per_rank": rank_launches,
+        "counters_allreduced": counters_reduced,
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity,
@@ -641,8 +834,10 @@ def main():
         res["update"] = update
         res["metric"] = "Mpps classified under AddPolicyRuleAddress/DeletePolicyRuleAddress churn @100k rules"
     print(json.dumps(res))
+    sys.stdout.flush()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def main_multidev(args):
@@ -769,4 +964,4 @@ def main_multidev(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

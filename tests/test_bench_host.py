@@ -131,3 +131,43 @@ def test_churn_op_log_replays_on_the_oracle():
     fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
     assert replay_churn(fnp, ops.log) == 200
     assert sorted(fnp.dump_flows()) == sorted(clf.dump_flows())
+
+
+def _run_bench(args, env_extra, timeout=600):
+    import json
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, cwd=root,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, (json.loads(line[-1]) if line else None), p.stderr
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself
+    (RANK / WORLD_SIZE / MASTER_* set by bench.py), they rendezvous (gloo here: the classify call
+    is the host emulation of the committed image, GPC_BENCH_HOST_EMU), all-reduce the per-rule
+    counters, gather every rank's launch times, and rank 0 prints the one line with n_gpus == 2
+    and its parity stamp against the oracle."""
+    rc, res, err = _run_bench(["--gpus", "2", "--config", "C1", "--packets", "4096", "--steps", "3", "--warmup", "1"],
+                              {"GPC_BENCH_HOST_EMU": "1"})
+    assert rc == 0, err[-3000:]
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"].endswith("x2, rules replicated")
+    assert res["data"].startswith("host-emulation")
+    per_rank = res["kernel_ms_by_launch_per_rank"]
+    assert len(per_rank) == 2 and all("classify_both" in r for r in per_rank)
+    assert res["parity"]["checked"] == 4096 and res["parity"]["mismatches"] == 0
+    assert "rank 0's shard of 2" in res["parity"]["sample"]
+    assert res["counters_allreduced"]["slots"] > 0 and res["counters_allreduced"]["packets"] > 0
+    assert res["value"] > 0 and res["steps"] == 3
+
+
+def test_bench_gpus_mismatch_with_launcher_fails():
+    """--gpus that disagrees with the launcher's WORLD_SIZE is an error, not a silent 1-GPU line."""
+    rc, res, err = _run_bench(["--gpus", "4", "--config", "C1", "--packets", "1024"],
+                              {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "GPC_BENCH_HOST_EMU": "1"}, timeout=120)
+    assert rc == 2 and res is None and "WORLD_SIZE=2" in err
