@@ -375,13 +375,14 @@ static uint32_t group_axes(const HostImage& h) {
 // kPaceDepth) calls before it on the same stream has finished; the device still has that many calls
 // queued, and no launch blocks. The per-stream queues are bounded like the grouping scratch: past
 // kPaceStreams streams, the queues whose events have all completed (idle streams, exited threads of
-// hipStreamPerThread) are dropped and their events destroyed.
+// hipStreamPerThread) are dropped and their events destroyed. The trim runs only when a call brings
+// a new stream (not on every launch), and it queries one event per queue: events of a
+// queue were recorded in stream order, so the newest one completing means the queue is idle.
 constexpr size_t kPaceDepth = 8, kPaceStreams = 64;
 static void pace_trim(gpc_ctx* ctx) {  // pace_mu held
   if (ctx->pace.size() <= kPaceStreams) return;
   for (auto it = ctx->pace.begin(); it != ctx->pace.end();) {
-    bool idle = true;
-    for (hipEvent_t e : it->second) idle = idle && hipEventQuery(e) == hipSuccess;
+    const bool idle = it->second.empty() || hipEventQuery(it->second.back()) == hipSuccess;
     if (!idle) {
       (void)hipGetLastError();
       ++it;
@@ -402,8 +403,9 @@ struct Pace {
     const size_t depth = cfg > 0 ? size_t(cfg) : kPaceDepth;
     {
       std::lock_guard<std::mutex> p(ctx->pace_mu);
-      pace_trim(ctx);
-      auto& q = ctx->pace[{slot, stream_key(st)}];
+      const auto key = std::make_pair(slot, stream_key(st));
+      if (!ctx->pace.count(key)) pace_trim(ctx);
+      auto& q = ctx->pace[key];
       if (q.size() >= depth) {
         ev = q.front();
         q.pop_front();

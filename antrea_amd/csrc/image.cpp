@@ -99,6 +99,20 @@ uint64_t rule_sig(const RuleB& r, bool counted, uint32_t slot) {
                      uint64_t(r.tier) << 48);
   return mix64(h ^ (uint64_t(r.has_act) | uint64_t(r.pin) << 1 | uint64_t(counted) << 2 | uint64_t(slot) << 8));
 }
+// One copy per distinct sorted hash list (BaseRule::atoms).
+struct AtomSetInterner {
+  std::unordered_map<uint64_t, std::vector<std::shared_ptr<const std::vector<uint64_t>>>> by_digest;
+  std::shared_ptr<const std::vector<uint64_t>> intern(std::vector<uint64_t>&& v) {
+    uint64_t d = 0xcbf29ce484222325ull ^ v.size();
+    for (uint64_t x : v) d = (d ^ x) * 0x100000001b3ull;
+    auto& bucket = by_digest[d];
+    for (const auto& p : bucket)
+      if (*p == v) return p;
+    bucket.push_back(std::make_shared<const std::vector<uint64_t>>(std::move(v)));
+    return bucket.back();
+  }
+};
+
 std::vector<uint64_t> clause_hashes(const std::vector<Atom>& atoms) {
   std::vector<uint64_t> v;
   v.reserve(atoms.size());
@@ -1068,6 +1082,13 @@ constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 24;  // 256 MB of entri
 // 8.07 with m = 0.
 constexpr double kMergeListMax = 16.0;
 constexpr uint32_t kV6DefaultTags = 4;
+// Sub-region tables (kV6L1Child) cost 4 KB per split and a block keeps splitting while it holds
+// more than kV6LeafLens lengths, so rule sets mixing many long prefix lengths under distinct blocks
+// could grow them without bound (a /64 holding a /96 and a /128 under c = 48 costs
+// 16 KB). Budget: 1 KB per prefix of the tree, at least 128 MB, at most 1 GB (C3: 245 k prefixes,
+// 94.5 MB of sub-tables). Past it a block keeps its length list (or the global search), which is
+// the unsplit round-5 layout: exact, only slower for the addresses under it.
+constexpr size_t kV6SubBytesPerPrefix = 1024, kV6SubMinBudget = size_t(128) << 20, kV6SubMaxBudget = size_t(1) << 30;
 constexpr uint64_t kMergeMinBytes = uint64_t(16) << 20;
 template <typename CE>
 void merge_bands(std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>>& sub, const std::vector<std::vector<uint32_t>>& xsets) {
@@ -1785,7 +1806,9 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
     if (const char* e = std::getenv("GPC_V6_LEAF_LENS")) leaf_max = uint32_t(std::min<long>(kV6L1MaxLens, std::max<long>(0, std::atol(e))));
     l1_tab.assign(size_t(nt) * nreg * 4, 0u);
     std::vector<std::vector<uint32_t>> leaf_L(size_t(nt) * nreg);  // per entry: its search list (leaves)
-    size_t n_sub = 0, sub_bytes = 0;
+    size_t n_sub = 0, sub_bytes = 0, n_unsplit = 0;
+    size_t sub_budget = std::min(kV6SubMaxBudget, std::max(kV6SubMinBudget, kV6SubBytesPerPrefix * codes.nodes.size()));
+    if (const char* e = std::getenv("GPC_V6_SUB_BUDGET_KB")) sub_budget = size_t(std::max<long>(0, std::atol(e))) << 10;
     auto len_ix = [&](uint32_t len) { return uint32_t(std::lower_bound(lens.begin(), lens.end(), len) - lens.begin()); };
     std::function<void(size_t, uint32_t, uint32_t, uint32_t, std::vector<uint32_t>&)> fill =
         [&](size_t ei, uint32_t ll, uint32_t bc, uint32_t bl, std::vector<uint32_t>& ns) {
@@ -1793,7 +1816,10 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
           for (uint32_t n : ns) L.push_back(len_ix(uint32_t(codes.nodes[n].len)));
           std::sort(L.begin(), L.end());
           L.erase(std::unique(L.begin(), L.end()), L.end());
-          if (L.size() > leaf_max && ll < 128u) {
+          const bool over = L.size() > leaf_max && ll < 128u &&
+                            sub_bytes + 16ull * (1ull << v6_sub_bits(ll)) > sub_budget;
+          n_unsplit += over;
+          if (L.size() > leaf_max && ll < 128u && !over) {
             const uint32_t st = v6_sub_bits(ll), sl = ll + st, nsub = 1u << st;
             const size_t child = l1_tab.size() / 4;
             l1_tab.resize(l1_tab.size() + 4 * size_t(nsub), 0u);
@@ -1889,7 +1915,8 @@ int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc
       }
     }
     if (std::getenv("GPC_IMAGE_DEBUG"))
-      std::fprintf(stderr, "IPv6 sub-region tables: %zu (%.1f MB)\n", n_sub, double(sub_bytes) / 1e6);
+      std::fprintf(stderr, "IPv6 sub-region tables: %zu (%.1f MB of a %.1f MB budget; %zu blocks left unsplit)\n", n_sub,
+                   double(sub_bytes) / 1e6, double(sub_budget) / 1e6, n_unsplit);
     if (std::getenv("GPC_IMAGE_DEBUG"))
       std::fprintf(stderr, "IPv6 region tables: c = %u, %u tags\n", l1_c, nt);
   }
@@ -2236,7 +2263,8 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       now.reserve(r.clause[k].size());
       for (const Atom& a : r.clause[k]) now.push_back({atom_hash(a), &a});
       std::sort(now.begin(), now.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-      const std::vector<uint64_t>& was = br.atoms[k];
+      static const std::vector<uint64_t> kNone;
+      const std::vector<uint64_t>& was = br.atoms[k] ? *br.atoms[k] : kNone;
       size_t j = 0;
       for (size_t i = 0; i < now.size(); i++) {
         if (i && now[i].first == now[i - 1].first) continue;
@@ -2531,6 +2559,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
   auto& counted_deny = G.counted_deny;
   out->n_flows = G.n_flows;
   out->hdr.live = 0;
+  AtomSetInterner atom_sets;
   // ---- 2. per table: rank, emit records, driver indexes
   Blob B;
   B.w.reserve(1 << 20);
@@ -2705,7 +2734,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
           br.table = uint32_t(t);
           br.rec_off = base;
           br.sig = rule_sig(r, counted, slot);
-          for (int k = 0; k < r.n; k++) br.atoms[k] = clause_hashes(r.clause[k]);
+          for (int k = 0; k < r.n; k++) br.atoms[k] = atom_sets.intern(clause_hashes(r.clause[k]));
         }
       }
     }

@@ -22,7 +22,9 @@ class V6Codes;  // IPv6 prefix tree and codes (image.cpp)
 struct BaseRule {
   uint32_t table = 0, rec_off = 0;
   uint64_t sig = 0;
-  std::vector<uint64_t> atoms[kMaxClauses];
+  // sorted atom hashes per clause, interned per image: rules sharing a peer set (an AddressGroup
+  // referenced by many rules, C2g) share one vector (10 M hashes -> 160 k in C2g)
+  std::shared_ptr<const std::vector<uint64_t>> atoms[kMaxClauses];
 };
 
 struct HostImage {

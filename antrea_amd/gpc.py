@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import ipaddress
+import re
 import socket
 import os
 from typing import Dict, List, Optional
@@ -289,6 +290,10 @@ def _endpoints(eps):
 SVC_PROTOCOLS = {"TCP": 1, "UDP": 2, "SCTP": 3}
 
 
+_OCTET = r"(?:25[0-5]|2[0-4][0-9]|1[0-9][0-9]|[1-9]?[0-9])"
+_DOTTED_QUAD = re.compile(r"%s(?:\.%s){3}\Z" % (_OCTET, _OCTET))
+
+
 class RuleBuf:
     """Keeps the ctypes objects of one or more gpc_rule alive."""
 
@@ -303,9 +308,11 @@ class RuleBuf:
         if lst is None:
             return -1, None
         n = len(lst)
-        if n >= 64 and all(type(a) is str and a.count(".") == 3 and "/" not in a for a in lst):
+        if n >= 64 and all(type(a) is str and _DOTTED_QUAD.match(a) for a in lst):
             # large lists of IPv4 Pod addresses (AddressGroups): filled as one numpy record array
-            # in gpc_addr's layout, the dotted quads parsed by inet_aton (C) instead of ipaddress
+            # in gpc_addr's layout, the dotted quads parsed by inet_aton (C) instead of ipaddress;
+            # only plain decimal quads take this path (inet_aton also takes octal / hex / short
+            # forms that ipaddress rejects, and IPv4-embedded IPv6 text has colons)
             buf = np.zeros(n, dtype=_ADDR_NP)
             buf["kind"] = ADDR_KINDS["ip"]
             buf["family"] = 4

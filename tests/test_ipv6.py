@@ -158,3 +158,66 @@ def test_ipv6_code_overflow_keeps_ipv4():
             "proto": np.array([6], np.uint8), "out_port": np.array([3], np.uint32)}
     v = emu.classify(c, cols)
     assert v[0, 1]["action"] == 2  # allowed by rule 1 through the IPv4 image
+
+
+def _nested_blocks_rules(n_blocks):
+    """n_blocks /64s (spread so the region tag is short), each holding rules on a /64, a /96, a
+    /112 and a /128 of itself at rising priorities with alternating actions: every /64 region needs
+    sub-region tables down to /128."""
+    rules, fid = [], 1
+    for b in range(n_blocks):
+        net = ipaddress.IPv6Network((int(ipaddress.IPv6Address("fd00:1:2::")) | (b * 0x9E37 % 65536) << 64 | b << 60, 64),
+                                    strict=False)
+        base = int(net.network_address)
+        for k, (plen, action) in enumerate(((64, "Allow"), (96, "Drop"), (112, "Allow"), (128, "Drop"))):
+            host = base | (0xABCD << 32 if plen >= 96 else 0) | (0x1234 << 16 if plen >= 112 else 0) | (7 if plen == 128 else 0)
+            pfx = ipaddress.IPv6Network((host, plen), strict=False)
+            rules.append({"flow_id": fid, "direction": "In", "action": action, "table": "AntreaPolicyIngressRule",
+                          "priority": 1000 + 4 * b + k, "tier_priority": 50, "policy_type": "AntreaClusterNetworkPolicy",
+                          "policy_name": "p%d" % b, "policy_namespace": "", "policy_uid": "u%d" % b, "name": "r%d" % fid,
+                          "from": [{"ipnet": str(pfx)}], "to": [{"ofport": 5}],
+                          "service": [{"protocol": "TCP", "port": 80}]})
+            fid += 1
+    return rules
+
+
+def _nested_blocks_packets(rules, n_blocks, seed):
+    rng = np.random.default_rng(seed)
+    srcs = []
+    for b in range(n_blocks):
+        r = rules[4 * b]
+        base = int(ipaddress.IPv6Network(r["from"][0]["ipnet"]).network_address)
+        for host in (base | 0xABCD << 32 | 0x1234 << 16 | 7, base | 0xABCD << 32 | 0x1234 << 16 | 9,
+                     base | 0xABCD << 32 | 0x77 << 16, base | 0x11 << 32, base ^ 1 << 70):
+            srcs.append(host)
+    srcs = [srcs[i] for i in rng.permutation(len(srcs))]
+    n = len(srcs)
+    src6 = np.array([list(s.to_bytes(16, "big")) for s in srcs], dtype=np.uint8)
+    dst6 = np.tile(np.frombuffer(ipaddress.IPv6Address("fd00:9::1").packed, np.uint8), (n, 1))
+    return {"src6": src6, "dst6": dst6, "sport": np.full(n, 4000, np.uint16), "dport": np.full(n, 80, np.uint16),
+            "proto": np.full(n, 6, np.uint8), "out_port": np.full(n, 5, np.uint32)}
+
+
+def test_ipv6_sub_region_budget_bounds_image(monkeypatch):
+    """sub-region tables are capped by a byte budget (image.cpp
+    kV6SubMinBudget / GPC_V6_SUB_BUDGET_KB). Blocks past the budget keep their length list or the
+    global search: the image stays bounded and the verdicts stay exact (== the Python oracle)."""
+    nb = 96
+    rules = _nested_blocks_rules(nb)
+    cols6 = _nested_blocks_packets(rules, nb, seed=3)
+    n = len(cols6["proto"])
+    want = _oracle6(rules, cols6, n, ipv4=False)
+    sizes = {}
+    for budget in (None, "64", "0"):
+        if budget is None:
+            monkeypatch.delenv("GPC_V6_SUB_BUDGET_KB", raising=False)
+        else:
+            monkeypatch.setenv("GPC_V6_SUB_BUDGET_KB", budget)
+        c = _classifier(rules, ipv4=False)
+        sizes[budget] = c.debug_image6()[1] * 4
+        got = emu.classify6(c, cols6)
+        _cmp(got, want, cols6)
+    # every block splits down to /128 without a limit: 6 levels of 4 KB tables per /64 region
+    assert sizes[None] - sizes["0"] >= nb * 4 * 4096
+    assert sizes["64"] <= sizes["0"] + 64 * 1024 + 4096
+    assert set(np.unique(want["action"]).tolist()) >= {2, 3}

@@ -42,3 +42,24 @@ def test_verdicts_independent_of_sharing():
     a, b = emu.classify(shared, cols), emu.classify(private, cols)
     assert np.array_equal(a, b)
     assert (a["action"] != 0).any()
+
+
+def test_large_address_list_fast_path_is_strict():
+    """the numpy / inet_aton fill of large IPv4 peer lists takes plain decimal quads
+    only. IPv4-embedded IPv6 text goes through the ipaddress path (no OSError), and forms
+    inet_aton would accept but ipaddress rejects ('010.0.0.1' = octal) are rejected as before."""
+    import pytest
+    from antrea_amd import gpc
+    base = ["10.1.%d.%d" % (i // 250, i % 250 + 1) for i in range(80)]
+    mixed = base + ["::ffff:10.9.9.9"]
+    buf = gpc.RuleBuf([{"flow_id": 1, "direction": "In", "table": "IngressRule", "from": mixed, "to": None,
+                        "service": None}])
+    assert buf.arr[0].n_from == len(mixed)
+    fast = gpc.RuleBuf([{"flow_id": 1, "direction": "In", "table": "IngressRule", "from": base, "to": None,
+                         "service": None}])
+    slow = [gpc._addr(a) for a in base]
+    assert all(bytes(fast.arr[0].from_[i].ip) == bytes(slow[i].ip) and fast.arr[0].from_[i].kind == slow[i].kind
+               for i in range(len(base)))
+    with pytest.raises(ValueError):
+        gpc.RuleBuf([{"flow_id": 1, "direction": "In", "table": "IngressRule", "from": base + ["010.0.0.1"],
+                      "to": None, "service": None}])
