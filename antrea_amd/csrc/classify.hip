@@ -311,17 +311,18 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   // Ingress launch: only the egress action of the egress half is read here; nothing of it is held
   // over the walk (the result is stored as a half).
   uint32_t ea = 0;
-  if (kStage == 2) ea = (orig ? mid[i].y : reinterpret_cast<const uint2*>(out)[2 * i].y) & 0xffu;
+  if (kStage == 2) ea = (mid ? mid[i].y : reinterpret_cast<const uint2*>(out)[2 * i].y) & 0xffu;
   // caller index of this packet (loaded where a result is stored: no register held over the walk)
   auto at = [&](uint64_t k) -> uint64_t { return orig ? uint64_t(orig[k]) : k; };
   // the ingress launch's result: its half of the verdict pair in grouped order into gout
   // (unpermute_kernel joins it with the egress half in mid and stores the pair in caller order with
-  // whole-line stores); ungrouped, the ingress half of the pair the egress launch stored; grouped
-  // without the un-permute, the pair at the caller index with the egress half re-read from mid
+  // whole-line stores); grouped without the un-permute, or ungrouped with the egress halves in mid
+  // (the split store), the pair at the caller index with the egress half re-read from mid; else
+  // the ingress half of the pair the egress launch stored
   auto store2 = [&](uint64_t k, uint32_t conj, uint32_t packed) {
     if (gout) {
       gout[k] = make_uint2(conj, packed);
-    } else if (orig) {
+    } else if (mid) {
       const uint2 e = mid[k];
       out[at(k)] = make_uint4(e.x, e.y, conj, packed);
     } else {
@@ -355,7 +356,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
       if (kStage == 0 && gout) {
         mid[i] = make_uint2(0u, rj);
         gout[i] = make_uint2(0u, 0u);
-      } else if (kStage == 1 && orig) {
+      } else if (kStage == 1 && mid) {
         mid[i] = make_uint2(0u, rj);
       } else if (kStage == 1) {
         out[i] = make_uint4(0u, rj, 0u, 0u);
@@ -369,7 +370,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   }
   if (kStage == 2) {  // only packets the egress stage let through reach the ingress tables
     if (ea == RV_DROP || ea == RV_REJECT || ea == RV_ISO_DROP) {
-      if (orig) store2(i, 0u, 0u);  // ingress NONE
+      if (mid) store2(i, 0u, 0u);  // ingress NONE
       return;
     }
     if (kSvc) {  // the fields the egress launch's Service stage rewrote
@@ -448,7 +449,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
   count_one(s, il);
   const VerdictOut e = s.v, g = s.v;
   if (kStage == 2) store2(il, g.conj, g.packed);
-  else if (kStage == 1 && orig) mid[il] = make_uint2(e.conj, e.packed);
+  else if (kStage == 1 && mid) mid[il] = make_uint2(e.conj, e.packed);
   else out[il] = make_uint4(e.conj, e.packed, 0u, 0u);  // ingress NONE until the second launch
 }
 
@@ -591,6 +592,19 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
   if (kSvc) {
     launch_mark(marks, kLaunchBoth, stream);
     hipLaunchKernelGGL((classify_kernel<kDelta, true, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
+                       lb_out, counters, count, orig, mid, xo, gout, nullptr);
+    return;
+  }
+  // One launch for both stages unless a stage regroups its lanes by scan length (the sort is per
+  // stage). Round 2 measured the split 8 % faster on C3 (lanes leave the egress stage at different
+  // times); on the zero-scratch kernels one launch is faster (C3 4.70 -> 4.54 ms per 64 M packets,
+  // profiles/r06b_*): no egress verdict round trip through HBM and one read of the packet columns.
+  // GPC_FUSED=0 / 1 forces the split / the single launch (A/B experiments).
+  static const int fused_env = std::getenv("GPC_FUSED") ? std::atoi(std::getenv("GPC_FUSED")) : -1;
+  const bool fused = fused_env == 1 || (fused_env < 0 && !ep.sort_table[0] && !ep.sort_table[1]);
+  if (fused) {
+    launch_mark(marks, kLaunchBoth, stream);
+    hipLaunchKernelGGL((classify_kernel<kDelta, false, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,
                        lb_out, counters, count, orig, mid, xo, gout, nullptr);
     return;
   }

@@ -2231,7 +2231,10 @@ template <typename Add>
 GPC_HD void count_stage(const VerdictOut& v, uint32_t slot, uint32_t len, uint32_t ct_state, Add add) {
   const uint32_t base = kCounterWords * slot;
   add(base, 1ull);
-  add(base + 1, (unsigned long long)len);
+  // each add is one scattered device-scope atomic executed at the memory side (~40 B of fabric
+  // traffic; C3 with counters: 4.70 vs 4.26 ms without): adds of 0 are skipped (batches without
+  // the len column, sessions of established connections)
+  if (len) add(base + 1, (unsigned long long)len);
   if (count_session(v, ct_state)) add(base + 2, 1ull);
 }
 

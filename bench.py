@@ -77,26 +77,208 @@ def _lbar(wl, clf, n=20000, family=4):
 
 
 class _ChurnOps:
-    """The C5 address-op stream: alternating add / delete of /32 src peers on random rules, drawn
-    from one seeded generator. Every rank uses the same seed, so all ranks apply one op stream
-    (they replicate one policy); only how the ops are batched into commits is rank-local."""
+    """The C5 op stream, drawn from one seeded generator. Every rank uses the same seed and the same
+    candidate list, so all ranks apply one op stream (they replicate one policy); only how the ops
+    are batched into commits is rank-local. `log` records every op in the order applied, as dicts
+    the oracle replays (oracle/parity.py replay_churn).
 
-    def __init__(self, clf, wl, seed):
+    mix "uniform" (round 5): alternating add / delete of uniformly random /32 source peers on random
+    rules -- packets almost never hit them. mix "mixed" (default): the reference's churn entry points
+    at rates that move traffic (`MIX`, per op):
+      * AddPolicyRuleAddress of a /32 the timed batch sends (`cands`: for a sampled packet, a rule
+        whose other clauses it matches, so the rule completes for it: ingress rules get the source
+        in From, egress rules the destination in To) and DeletePolicyRuleAddress of earlier adds
+        (network_policy.go:1661-1710; point extensions of the base records);
+      * DeletePolicyRuleAddress of a rule's own ipBlock peer (the base record is tombstoned and the
+        rule journaled) and the later re-add of such a peer;
+      * UninstallPolicyRuleFlows (:1570) of whole rules and InstallPolicyRuleFlows (:1160) of some
+        of them again;
+      * ReassignFlowPriorities (:1873) of one rule to a free priority of its table."""
+
+    MIX = (("add_hit", 0.45), ("del_add", 0.35), ("del_base", 0.09), ("readd_base", 0.10), ("uninstall", 0.0012),
+           ("reinstall", 0.0008), ("reassign", 0.0010))
+    # (the del_base / readd_base share is scaled by `base_frac` / 0.19: --churn-base-frac)
+
+    def __init__(self, clf, wl, seed, mix="mixed", cands=None, base_frac=0.04, weights=None):
         import numpy as np
         self.clf = clf
         self.rng = np.random.default_rng(seed)
+        self.mix = mix
         self.rules = [r for r in wl.rules if r.get("from")]
         self.added = []
         self.issued = 0
-        self.log = []  # (1 add / 0 delete, rule id, IPv4 value, priority or -1): the oracle replays it
+        self.log = []
+        self.fast = getattr(clf, "rule_addr_ip4", None)  # the library's per-op cost, not string marshalling
+        if mix == "uniform":
+            return
+        import copy
+        self.by_fid = {r["flow_id"]: r for r in wl.rules}
+        self.fids = sorted(self.by_fid)
+        self.live = set(self.fids)
+        self.prio = {f: r.get("priority") for f, r in self.by_fid.items()}
+        self.cur = {f: {"src": copy.copy(r.get("from") or []), "dst": copy.copy(r.get("to") or [])}
+                    for f, r in self.by_fid.items()}
+        self.used = {}
+        for r in wl.rules:
+            if r.get("priority") is not None:
+                self.used.setdefault(r["table"], set()).add(r["priority"])
+        self.cands = cands if cands is not None else []
+        self.added_set = set()
+        self.base_gone = []  # (fid, side, addr) deleted base peers, re-addable
+        self.uninstalled = []
+        w = dict(self.MIX)
+        sc = base_frac / (w["del_base"] + w["readd_base"])
+        w["del_base"] *= sc
+        w["readd_base"] *= sc
+        w.update(weights or {})
+        self.kinds = list(w)
+        self.cum = np.cumsum([w[k] for k in self.kinds])
+        self.cum /= self.cum[-1]
+        self.counts = {k: 0 for k in self.kinds}
+
+    # --- ops (each records itself; returns False when not applicable now)
+    def _addr(self, add, fid, side, v):
+        a = _ip4(v)
+        if self.fast:
+            self.fast(add, fid, side, v, self.prio[fid])
+        elif add:
+            self.clf.add_policy_rule_address(fid, side, [a], self.prio[fid])
+        else:
+            self.clf.delete_policy_rule_address(fid, side, [a], self.prio[fid])
+        self.log.append({"op": "add" if add else "del", "fid": fid, "side": side, "addrs": [a],
+                         "priority": self.prio[fid]})
+
+    def _add_hit(self):
+        rng = self.rng
+        for _ in range(8):
+            if not len(self.cands):
+                return False
+            side, fid, v = self.cands[int(rng.integers(len(self.cands)))]
+            key = (fid, side, v)
+            if fid not in self.live or key in self.added_set:
+                continue
+            self._addr(True, fid, side, v)
+            self.added_set.add(key)
+            self.added.append(key)
+            self.cur[fid][side].append(_ip4(v))
+            return True
+        return False
+
+    def _del_add(self):
+        rng = self.rng
+        for _ in range(8):
+            if not self.added:
+                return False
+            j = int(rng.integers(len(self.added)))
+            fid, side, v = self.added[j]
+            if fid not in self.live:
+                continue
+            self.added[j] = self.added[-1]
+            self.added.pop()
+            self.added_set.discard((fid, side, v))
+            self._addr(False, fid, side, v)
+            self.cur[fid][side].remove(_ip4(v))
+            return True
+        return False
+
+    def _del_base(self):
+        rng = self.rng
+        for _ in range(8):
+            fid = self.fids[int(rng.integers(len(self.fids)))]
+            if fid not in self.live:
+                continue
+            r = self.by_fid[fid]
+            side = "src" if r["direction"] == "In" else "dst"  # the ipBlock side
+            base = [a for a in self.cur[fid][side] if isinstance(a, dict)]
+            if not base:
+                continue
+            a = base[int(rng.integers(len(base)))]
+            self.clf.delete_policy_rule_address(fid, side, [a], self.prio[fid])
+            self.log.append({"op": "del", "fid": fid, "side": side, "addrs": [a], "priority": self.prio[fid]})
+            self.cur[fid][side].remove(a)
+            self.base_gone.append((fid, side, a))
+            return True
+        return False
+
+    def _readd_base(self):
+        rng = self.rng
+        for _ in range(8):
+            if not self.base_gone:
+                return False
+            j = int(rng.integers(len(self.base_gone)))
+            fid, side, a = self.base_gone[j]
+            if fid not in self.live:
+                continue
+            self.base_gone[j] = self.base_gone[-1]
+            self.base_gone.pop()
+            self.clf.add_policy_rule_address(fid, side, [a], self.prio[fid])
+            self.log.append({"op": "add", "fid": fid, "side": side, "addrs": [a], "priority": self.prio[fid]})
+            self.cur[fid][side].append(a)
+            return True
+        return False
+
+    def _uninstall(self):
+        fid = self.fids[int(self.rng.integers(len(self.fids)))]
+        if fid not in self.live:
+            return False
+        self.clf.uninstall_policy_rule_flows(fid)
+        self.log.append({"op": "uninstall", "fid": fid})
+        self.live.discard(fid)
+        self.uninstalled.append(fid)
+        return True
+
+    def _reinstall(self):
+        import copy
+        if not self.uninstalled:
+            return False
+        fid = self.uninstalled.pop(int(self.rng.integers(len(self.uninstalled))))
+        r = dict(self.by_fid[fid])
+        r["from"], r["to"] = copy.copy(self.cur[fid]["src"]), copy.copy(self.cur[fid]["dst"])
+        if self.prio[fid] is not None:
+            r["priority"] = self.prio[fid]
+        self.clf.install_policy_rule_flows(r)
+        self.log.append({"op": "install", "rule": r})
+        self.live.add(fid)
+        return True
+
+    def _reassign(self):
+        rng = self.rng
+        fid = self.fids[int(rng.integers(len(self.fids)))]
+        if fid not in self.live or self.prio[fid] is None:
+            return False
+        t = self.by_fid[fid]["table"]
+        while True:
+            p = int(rng.integers(100, 65001))
+            if p not in self.used[t]:
+                break
+        self.clf.reassign_flow_priorities({self.prio[fid]: p}, t)
+        self.log.append({"op": "reassign", "table": t, "from": self.prio[fid], "to": p})
+        self.used[t].discard(self.prio[fid])
+        self.used[t].add(p)
+        self.prio[fid] = p
+        return True
 
     def apply(self, k):
-        rng, clf = self.rng, self.clf
-        fast = getattr(clf, "rule_addr_ip4", None)  # the library's per-op cost, not string marshalling
+        if self.mix == "uniform":
+            return self._apply_uniform(k)
+        import numpy as np
+        rng = self.rng
+        for _ in range(k):
+            kind = self.kinds[int(np.searchsorted(self.cum, rng.random(), side="right"))]
+            if not getattr(self, "_" + kind)():
+                kind = "add_hit"
+                if not self._add_hit():
+                    kind = "del_add"
+                    self._del_add()
+            self.counts[kind] += 1
+        self.issued += k
+
+    def _apply_uniform(self, k):
+        rng, clf, fast = self.rng, self.clf, self.fast
         for _ in range(k):
             if self.added and rng.random() < 0.5:
                 rid, v, prio = self.added.pop(int(rng.integers(len(self.added))))
-                self.log.append((0, rid, v, -1 if prio is None else prio))
+                self.log.append({"op": "del", "fid": rid, "side": "src", "addrs": [_ip4(v)], "priority": prio})
                 if fast:
                     fast(False, rid, "src", v, prio)
                 else:
@@ -109,8 +291,67 @@ class _ChurnOps:
                 else:
                     clf.add_policy_rule_address(r["flow_id"], "src", [_ip4(v)], r.get("priority"))
                 self.added.append((r["flow_id"], v, r.get("priority")))
-                self.log.append((1, r["flow_id"], v, -1 if r.get("priority") is None else r.get("priority")))
+                self.log.append({"op": "add", "fid": r["flow_id"], "side": "src", "addrs": [_ip4(v)],
+                                 "priority": r.get("priority")})
         self.issued += k
+
+
+VERDICT_NAMES = ("NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "BYPASS")
+
+
+def _verdict_mix(v):
+    """Share of each action per stage: v = (n, 2, 8) verdict bytes (byte 4 = action)."""
+    import numpy as np
+    mix = {}
+    for j, stage in enumerate(("egress", "ingress")):
+        a, c = np.unique(v[:, j, 4], return_counts=True)
+        mix[stage] = {VERDICT_NAMES[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
+    return mix
+
+
+def churn_candidates(wl, cols, max_per_packet=1, seed=77):
+    """Address adds that change verdicts of the timed batch (C5 "mixed"): for every sampled packet
+    (host columns), the rules whose clauses other than the peer clause it matches -- service
+    (protocol, destination port in the rule's range) and AppliedTo (ingress: its out_port among the
+    rule's ofports; egress: its source among the rule's Pod IPs) -- give (side, flow id, address):
+    ingress rules the packet's source as a From peer, egress rules its destination as a To peer.
+    Host numpy over the rule set, before the timed region."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    m = wl.meta
+    n_local = len(wl.local_ips)
+    port_ix = {int(p): i for i, p in enumerate(wl.local_ports)}
+    ip_ix = {int(a): i for i, a in enumerate(wl.local_ips)}
+    nr = len(wl.rules)
+    app = np.zeros((nr, n_local), bool)  # AppliedTo of each rule over the local Pods
+    for j, r in enumerate(wl.rules):
+        if r["direction"] == "In":
+            for a in r.get("to") or []:
+                if isinstance(a, dict) and "ofport" in a and int(a["ofport"]) in port_ix:
+                    app[j, port_ix[int(a["ofport"])]] = True
+        else:
+            for a in r.get("from") or []:
+                if isinstance(a, str) and "/" not in a:
+                    v = int.from_bytes(bytes(int(x) for x in a.split(".")), "big")
+                    if v in ip_ix:
+                        app[j, ip_ix[v]] = True
+    d, proto, plo, phi = m["dir"], m["proto"], m["plo"], m["phi"]
+    fids = np.array([r["flow_id"] for r in wl.rules])
+    out = []
+    for i in range(len(cols["src"])):
+        p, dp = int(cols["proto"][i]), int(cols["dport"][i])
+        svc = (proto == p) & (plo <= dp) & (phi >= dp)
+        o = port_ix.get(int(cols["out_port"][i]))
+        if o is not None:
+            hit = np.nonzero(svc & (d == 0) & app[:, o])[0]
+            for j in rng.permutation(hit)[:max_per_packet]:
+                out.append(("src", int(fids[j]), int(cols["src"][i])))
+        q = ip_ix.get(int(cols["src"][i]))
+        if q is not None:
+            hit = np.nonzero(svc & (d == 1) & app[:, q])[0]
+            for j in rng.permutation(hit)[:max_per_packet]:
+                out.append(("dst", int(fids[j]), int(cols["dst"][i])))
+    return out
 
 
 def _ip4(v):
@@ -573,6 +814,12 @@ def main(argv=None):
     ap.add_argument("--keep-pmc", default="", help="directory that keeps the PMC passes' counter CSVs")
     ap.add_argument("--churn-rate", type=float, default=10000.0, help="C5: address ops per second")
     ap.add_argument("--max-batch", type=int, default=2000, help="C5: most address ops per gpc_commit")
+    ap.add_argument("--churn-mix", default="mixed", choices=("mixed", "uniform"),
+                    help="C5 op stream: mixed = adds of peers the batch sends + base-peer deletes / re-adds + "
+                         "uninstall / reinstall + priority reassignment (_ChurnOps.MIX); uniform = round 5's "
+                         "random /32 source adds / deletes")
+    ap.add_argument("--churn-base-frac", type=float, default=0.04,
+                    help="C5 mixed: share of ops that delete / re-add a rule's own ipBlock peers (journaled)")
     ap.add_argument("--commit-interval-ms", type=float, default=10.0,
                     help="C5: at most one gpc_commit per this many ms (ops due meanwhile share it)")
     ap.add_argument("--group", type=int, default=0,
@@ -678,9 +925,25 @@ def main(argv=None):
     lat, th = [], None
     if churn:
         import threading
+        import numpy as np
+        # the C3 verdicts of the batch prefix (warmup ran on the base epoch): the mix shift baseline
+        n_pre = min(n, 1 << 20)
+        v_before = out.view(torch.uint8).reshape(n, 2, 8)[:n_pre].cpu().numpy().copy()
+        cands = None
+        if args.churn_mix == "mixed":
+            # adds that hit the timed batch: candidates from rank 0's batch prefix (every rank derives
+            # the same list, so every rank applies the same op stream)
+            k_c = min(n_pre, 8192)
+            idx_c = (torch.arange(k_c, dtype=torch.int64) * n_pre) // k_c
+            c0 = cols4 if rank == 0 else workload.gen_packets_torch(wl, n, seed=workload.PKT_SEED, device=dev)
+            cands = churn_candidates(wl, _host_sample(c0, idx_c.to(dev)))
+            del c0
+            _log("C5 mixed: %d candidate adds from %d sampled packets" % (len(cands), k_c))
+        st0 = clf.image_stats()
         sys.setswitchinterval(2e-4)  # the control thread must not wait 5 ms for the GIL behind launches
         stop = threading.Event()
-        churn_ops = _ChurnOps(clf, wl, seed=1234)  # the same op stream on every rank
+        churn_ops = _ChurnOps(clf, wl, seed=1234, mix=args.churn_mix, cands=cands,
+                              base_frac=args.churn_base_frac)  # the same op stream on every rank
         th = threading.Thread(target=_churn_loop, args=(churn_ops, args.churn_rate, args.max_batch, stop, lat,
                                                         args.commit_interval_ms / 1e3), daemon=True)
         th.start()
@@ -720,8 +983,14 @@ def main(argv=None):
                                     "max": round(float(op_ms.max()), 3) if len(op_ms) else None},
                   "commit_ms": {"p50": pct(commit_ms, 50), "p99": pct(commit_ms, 99)},
                   "overlay_rules_end": st["n_overlay_rules"], "tombstones_end": st["n_tombstones"],
-                  "full_builds": st["n_full_builds"], "delta_builds": st["n_delta_builds"],
-                  "background_builds": st["n_background_builds"]}
+                  "ext_rules_end": st["n_ext_rules"], "ext_values_end": st["n_ext_values"],
+                  "full_builds": st["n_full_builds"] - st0["n_full_builds"],
+                  "delta_builds": st["n_delta_builds"] - st0["n_delta_builds"],
+                  "background_builds": st["n_background_builds"] - st0["n_background_builds"],
+                  "mix": args.churn_mix}
+        if args.churn_mix == "mixed":
+            update["op_counts"] = dict(churn_ops.counts)
+            update["candidate_adds"] = len(cands)
         if world > 1:
             update["ranks"] = _churn_converge(churn_ops, wl, dev, world)
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
@@ -735,8 +1004,16 @@ def main(argv=None):
         # before the control thread stopped), and the final epoch classifies the batch once more
         _log("oracle replay of %d ops" % len(churn_ops.log))
         update["oracle_replay"] = worker.churn(churn_ops.log)
+    if churn:  # the final epoch classifies the batch once more (parity sample, verdict shift)
         dp.classify(soa, n, out, False, stream)
         dp.sync()
+        v_after = out.view(torch.uint8).reshape(n, 2, 8)[:n_pre].cpu().numpy()
+        changed = (v_before.reshape(n_pre, 16) != v_after.reshape(n_pre, 16)).any(axis=1)
+        update["verdict_shift"] = {
+            "packets": n_pre, "changed_frac": round(float(changed.mean()), 6),
+            "mix_before": _verdict_mix(v_before), "mix_after": _verdict_mix(v_after),
+            "basis": "verdicts of the first %d packets on the base (C3) epoch, before the churn, vs on the final "
+                     "epoch" % n_pre}
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     counters_reduced = None
     if world > 1:
@@ -762,12 +1039,7 @@ def main(argv=None):
     import numpy as np
     from antrea_amd.gpc import VERDICT_DTYPE
     v8 = out.view(torch.uint8).reshape(n, 2, 8)
-    v = v8[: min(n, 1 << 20)].cpu().numpy()
-    mix = {}
-    names = ["NONE", "NO_MATCH", "ALLOW", "DROP", "REJECT", "ISOLATION_DROP", "BYPASS"]
-    for j, stage in enumerate(("egress", "ingress")):
-        a, c = np.unique(v[:, j, 4], return_counts=True)
-        mix[stage] = {names[int(x)]: round(float(y) / len(v), 4) for x, y in zip(a, c)}
+    mix = _verdict_mix(v8[: min(n, 1 << 20)].cpu().numpy())
 
     parity = None
     if worker is not None and not args.no_parity:  # rank 0 (its own shard at N > 1)

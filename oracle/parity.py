@@ -8,9 +8,11 @@
                              (parsed exactly as network_policy.go:1917-1980, 2034 parse the dump).
 * `service_flows(wl)`     -- for a workload with Services (C4): the ServiceLB / EndpointDNAT flow
                              text, the select groups and the Pod map the C oracle's AntreaProxy stage
-                             runs on, as the product's host compiler realizes them (that text is
-                             pinned by the reference's client_test.go goldens, tests/test_service.py;
-                             the policy flows always come from the oracle compiler).
+                             runs on, from the oracle's own restatement of the Service flows
+                             (oracle/service.py, pinned by the reference's client_test.go goldens;
+                             equal to the product's dumps, tests/test_service.py).
+Nothing here loads the product library or its compiler; `antrea_amd.workload` (the synthetic
+input generator shared with bench.py) is the only import from the product package.
 * `non_service_mask`      -- packets of a workload with Services that do not hit a ServiceLB flow.
 * `OracleWorker`          -- the same in a separate CPU process (spawned, never touches a GPU):
                              bench.py starts it before its GPU work, then asks it to check a sample
@@ -71,19 +73,16 @@ def oracle_flows(wl):
 
 
 def service_flows(wl):
-    """(ServiceLB / EndpointDNAT flow lines, group lines, Pod map) of wl's Services, or None. Host
-    compiler only: nothing here touches a GPU."""
+    """(ServiceLB / EndpointDNAT flow lines, group lines, Pod map) of wl's Services, or None: the
+    oracle's own restatement of the AntreaProxy flows (oracle/service.py, pinned by the
+    client_test.go goldens), not the product's compiler."""
     if getattr(wl, "services", None) is None:
         return None
-    from antrea_amd import gpc, workload
-    c = gpc.Classifier(compact_after=-1)
-    try:
-        c.initialize()
-        workload.install_services(c, wl)
-        lines = [f for f in c.dump_flows() if "table=ServiceLB" in f or "table=EndpointDNAT" in f]
-        return lines, c.dump_groups(), dict(wl.pods)
-    finally:
-        del c
+    from . import service as osvc
+    s = osvc.FeatureService()
+    osvc.install_services(s, wl)
+    lines = [f for f in s.dump_flows() if "table=ServiceLB" in f or "table=EndpointDNAT" in f]
+    return lines, s.dump_groups(), dict(wl.pods)
 
 
 def oracle_pipeline(wl, procs: Optional[int] = None, flows=None):
@@ -100,15 +99,32 @@ def _ip4(v: int) -> str:
 
 
 def replay_churn(fnp, ops) -> int:
-    """Apply bench.py's C5 op log to the oracle compiler: (kind, rule id, IPv4 value, priority) with
-    kind 1 = AddPolicyRuleAddress, 0 = DeletePolicyRuleAddress of one /32 source peer
-    (network_policy.go:1661-1710), in the order the product applied them."""
-    for kind, rid, v, prio in ops:
-        prio = None if prio is None or prio < 0 else int(prio)
-        if kind:
-            fnp.add_policy_rule_address(int(rid), "src", [_ip4(int(v))], prio)
+    """Apply bench.py's C5 op log to the oracle compiler, in the order the product applied it. Ops
+    are dicts (bench._ChurnOps): {"op": "add" | "del", "fid", "side", "addrs", "priority"}
+    (AddPolicyRuleAddress / DeletePolicyRuleAddress, network_policy.go:1661-1710), {"op":
+    "uninstall", "fid"} (UninstallPolicyRuleFlows :1570), {"op": "install", "rule"}
+    (InstallPolicyRuleFlows :1160), {"op": "reassign", "table", "from", "to"}
+    (ReassignFlowPriorities :1873). Round 5's tuples (kind 1 = add / 0 = delete, rule id, IPv4
+    value, priority or -1) of one /32 source peer are still accepted."""
+    for o in ops:
+        if not isinstance(o, dict):
+            kind, rid, v, prio = o
+            prio = None if prio is None or prio < 0 else int(prio)
+            o = {"op": "add" if kind else "del", "fid": int(rid), "side": "src", "addrs": [_ip4(int(v))],
+                 "priority": prio}
+        k = o["op"]
+        if k == "add":
+            fnp.add_policy_rule_address(o["fid"], o["side"], copy.deepcopy(o["addrs"]), o["priority"])
+        elif k == "del":
+            fnp.delete_policy_rule_address(o["fid"], o["side"], copy.deepcopy(o["addrs"]), o["priority"])
+        elif k == "uninstall":
+            fnp.uninstall_policy_rule_flows(o["fid"])
+        elif k == "install":
+            fnp.install_policy_rule_flows(copy.deepcopy(o["rule"]))
+        elif k == "reassign":
+            fnp.reassign_flow_priorities({o["from"]: o["to"]}, o["table"])
         else:
-            fnp.delete_policy_rule_address(int(rid), "src", [_ip4(int(v))], prio)
+            raise ValueError("unknown churn op %r" % (k,))
     return len(ops)
 
 

@@ -2,6 +2,9 @@
 import threading
 import time
 
+import numpy as np
+import pytest
+
 import bench
 from antrea_amd import workload
 
@@ -17,6 +20,15 @@ class _Stub:
     def delete_policy_rule_address(self, *a):
         self.ops += 1
 
+    def uninstall_policy_rule_flows(self, *a):
+        self.ops += 1
+
+    def install_policy_rule_flows(self, *a):
+        self.ops += 1
+
+    def reassign_flow_priorities(self, *a):
+        self.ops += 1
+
     def commit(self):
         self.commits += 1
         time.sleep(0.002)
@@ -25,7 +37,7 @@ class _Stub:
 def test_churn_loop_paces_ops_and_records_latency():
     wl = workload.config1()
     stub, rec, stop = _Stub(), [], threading.Event()
-    ops = bench._ChurnOps(stub, wl, seed=1)
+    ops = bench._ChurnOps(stub, wl, seed=1, mix="uniform")
     th = threading.Thread(target=bench._churn_loop, args=(ops, 5000.0, 2000, stop, rec))
     th.start()
     time.sleep(0.5)
@@ -38,9 +50,11 @@ def test_churn_loop_paces_ops_and_records_latency():
     assert all(len(r[2]) == r[0] and (r[2] >= 0).all() for r in rec)
 
 
-def test_churn_ops_same_seed_same_stream():
+@pytest.mark.parametrize("mix", ["mixed", "uniform"])
+def test_churn_ops_same_seed_same_stream(mix):
     """C5 at N>1: every rank draws the same op sequence, whatever its batching."""
-    wl = workload.config1()
+    wl = workload.config3(seed=5, n_policies_per_dir=6, rules_per_policy=10) if mix == "mixed" else workload.config1()
+    cands = bench.churn_candidates(wl, workload.gen_packets(wl, 2000, seed=3)) if mix == "mixed" else None
 
     class Rec(_Stub):
         def __init__(self):
@@ -53,8 +67,19 @@ def test_churn_ops_same_seed_same_stream():
         def delete_policy_rule_address(self, *a):
             self.seq.append(("del",) + tuple(map(str, a)))
 
+        def uninstall_policy_rule_flows(self, *a):
+            self.seq.append(("uninstall",) + tuple(map(str, a)))
+
+        def install_policy_rule_flows(self, r):
+            self.seq.append(("install", r["flow_id"], str(r["from"]), str(r["to"]), r.get("priority")))
+
+        def reassign_flow_priorities(self, *a):
+            self.seq.append(("reassign",) + tuple(map(str, a)))
+
     a, b = Rec(), Rec()
-    oa, ob = bench._ChurnOps(a, wl, seed=1234), bench._ChurnOps(b, wl, seed=1234)
+    w = {"uninstall": 0.03, "reinstall": 0.02, "reassign": 0.03}
+    oa = bench._ChurnOps(a, wl, seed=1234, mix=mix, cands=cands, weights=w)
+    ob = bench._ChurnOps(b, wl, seed=1234, mix=mix, cands=cands, weights=w)
     for _ in range(50):
         oa.apply(7)
     for _ in range(7):
@@ -110,9 +135,12 @@ def test_rank_launch_times_world2(tmp_path):
                        {"group_tiles": 0.7, "classify_egress": 4.0, "classify_ingress": 5.5}]
 
 
-def test_churn_op_log_replays_on_the_oracle():
-    """C5 parity: the op log bench._ChurnOps records, replayed on the oracle
-    compiler, gives the flows the product compiler realized applying the same ops."""
+@pytest.mark.parametrize("mix", ["mixed", "uniform"])
+def test_churn_op_log_replays_on_the_oracle(mix):
+    """C5 parity: the op log bench._ChurnOps records, replayed on the
+    oracle compiler, gives the flows the product compiler realized applying the same ops -- for the
+    mixed stream every kind of op (adds of peers the batch sends, deletes of adds and of base
+    ipBlock peers, re-adds, uninstall / reinstall, priority reassignment) occurs."""
     import copy
 
     from antrea_amd import gpc
@@ -122,15 +150,49 @@ def test_churn_op_log_replays_on_the_oracle():
     clf = gpc.Classifier(compact_after=-1)
     clf.initialize()
     clf.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
-    ops = bench._ChurnOps(clf, wl, seed=99)
+    cands = bench.churn_candidates(wl, workload.gen_packets(wl, 4000, seed=3)) if mix == "mixed" else None
+    w = {"uninstall": 0.03, "reinstall": 0.02, "reassign": 0.03} if mix == "mixed" else None
+    ops = bench._ChurnOps(clf, wl, seed=99, mix=mix, cands=cands, base_frac=0.2, weights=w)
     for _ in range(40):
         ops.apply(5)
-    assert len(ops.log) == 200 and {k for k, *_ in ops.log} == {0, 1}
+    assert len(ops.log) == 200
+    if mix == "mixed":
+        assert len(cands) > 20
+        assert all(ops.counts[k] > 0 for k in ops.kinds), ops.counts
+        assert {o["op"] for o in ops.log} == {"add", "del", "uninstall", "install", "reassign"}
+    else:
+        assert {o["op"] for o in ops.log} == {"add", "del"}
     fnp = oc.FeatureNetworkPolicy()
     fnp.initialize()
     fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
     assert replay_churn(fnp, ops.log) == 200
     assert sorted(fnp.dump_flows()) == sorted(clf.dump_flows())
+
+
+def test_churn_candidates_complete_rules():
+    """Every candidate add of the mixed C5 stream makes its rule complete for the packet it came
+    from: after adding it, the emulated verdict of that packet is decided by that rule or by a rule
+    ranked above it (never NO_MATCH in the rule's stage)."""
+    import copy
+
+    from antrea_amd import gpc
+    from tests import emu
+    wl = workload.config3(seed=5, n_policies_per_dir=6, rules_per_policy=10)
+    cols = workload.gen_packets(wl, 3000, seed=3)
+    cands = bench.churn_candidates(wl, cols)
+    assert cands
+    side, fid, v = cands[0]
+    clf = gpc.Classifier(compact_after=-1)
+    clf.initialize()
+    clf.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+    rule = next(r for r in wl.rules if r["flow_id"] == fid)
+    clf.rule_addr_ip4(True, fid, side, v, rule.get("priority"))
+    emu.commit_host(clf)
+    key = "src" if side == "src" else "dst"
+    i = int(np.nonzero(cols[key] == np.uint32(v))[0][0])
+    one = {k: a[i:i + 1] for k, a in cols.items()}
+    got = emu.classify(clf, one)[0, 0 if side == "dst" else 1]
+    assert got["action"] != 1 and got["conj_id"] != 0
 
 
 def _run_bench(args, env_extra, timeout=600):

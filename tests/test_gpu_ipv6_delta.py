@@ -53,10 +53,25 @@ def test_gpu_ipv6_delta_epochs_dual_stack(size):
     st = c.image_stats()
     assert st["v6_delta_builds"] >= 5 and st["v6_overlay_rules"] > 0, st
     got = c.classify6_host(cols6)
-    if size == "small":  # the Python oracle over C3-10k's flows would take minutes; the emulation stands in
+    if size == "small":
         n = 300
         sub = {k: v[:n] for k, v in cols6.items()}
         _cmp(got[:n], _oracle_after(workload.to_ipv6(wl, dual=True).rules, log6, sub, n, True), sub)
+    else:
+        # at the C3-10k size the device's IPv6 verdicts of the last delta epoch
+        # against the C oracle, every packet: the oracle compiler replays the IPv4 log over the IPv4
+        # rules and the C classifier runs the IPv4 packets (the fd00:10::/96 embedding preserves every
+        # match); the dual-stack context's IPv4 verdicts must equal them too
+        from oracle import compiler as oc
+        from oracle import parity
+        fnp = oc.FeatureNetworkPolicy()
+        fnp.initialize()
+        fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
+        mcf.apply(fnp, log4)
+        want = parity.oracle_pipeline(wl, flows=fnp.dump_flows()).classify(cols)
+        for fam, v in (("IPv6", got), ("IPv4", c.classify_host(cols))):
+            res = parity.compare(v, want)
+            assert res["mismatches"] == 0, (fam, res)
     c.compact()
     assert c.image_stats()["v6_overlay_rules"] == 0
     _cmp(c.classify6_host(cols6), got, cols)

@@ -149,3 +149,72 @@ def test_reference_golden_service_in_oracle():
     assert p["dst"] in (int(ipaddress.ip_address("10.10.0.100")), int(ipaddress.ip_address("10.10.0.101")))
     assert p["dport"] == 80 and p["ct_dst"] == pkt["dst"]
     assert (p["dest"] == ovs_cls.DEST_TUNNEL) == (p["dst"] == int(ipaddress.ip_address("10.10.0.100")))
+
+
+# ---- the oracle's own restatement of the Service flows (oracle/service.py), pinned by the same goldens
+from oracle import service as osvc  # noqa: E402
+
+
+@pytest.mark.parametrize("case", GOLD["groups"], ids=[c["name"] for c in GOLD["groups"]])
+def test_oracle_group_text_golden(case):
+    s = osvc.FeatureService()
+    s.install_service_group(case["group_id"], case["endpoints"], case["with_session_affinity"])
+    assert s.dump_groups() == [case["expected"]]
+    s.uninstall_service_group(case["group_id"])
+    assert s.dump_groups() == []
+
+
+@pytest.mark.parametrize("case", GOLD["endpoint_flows"], ids=[c["name"] for c in GOLD["endpoint_flows"]])
+def test_oracle_endpoint_flows_golden(case):
+    s = osvc.FeatureService()
+    s.install_endpoint_flows(case["protocol"], case["endpoints"])
+    assert sorted(s.dump_flows()) == sorted(case["expected"])
+    s.uninstall_endpoint_flows(case["protocol"], case["endpoints"])
+    assert s.dump_flows() == []
+
+
+@pytest.mark.parametrize("case", GOLD["service_flows"], ids=[c["name"] for c in GOLD["service_flows"]])
+def test_oracle_service_flows_golden(case):
+    s = osvc.FeatureService()
+    s.install_service_flows(case["config"])
+    assert s.dump_flows() == case["expected"]
+    cfg = case["config"]
+    s.uninstall_service_flows(cfg["ip"], cfg["port"], cfg["protocol"])
+    assert s.dump_flows() == []
+
+
+@pytest.mark.parametrize("extra", [{"affinity_timeout": 100}, {"is_nodeport": True, "is_external": True},
+                                   {"is_dsr": True, "is_external": True}, {"is_nested": True},
+                                   {"is_external": True, "traffic_policy_local": True}])
+def test_oracle_unsupported_service_configs(extra):
+    with pytest.raises(ValueError):
+        osvc.FeatureService().install_service_flows(dict(GOLD["service_flows"][0]["config"], **extra))
+
+
+@pytest.mark.parametrize("name,seed", [("C1", 61), ("C3s", 62)])
+def test_oracle_service_compiler_equals_product(name, seed):
+    """The oracle's Service flows and groups for a whole Service workload (remote, local, Local-policy
+    and Endpoint-less Services, shared Endpoints, an external Service) equal the product's dumps --
+    and after uninstalling a third of the Services and shrinking a group."""
+    wl = _svc_workload(name, seed)
+    ext = dict(wl.services[0], is_external=True, traffic_policy_local=False)
+    wl.services[0] = ext
+    c = gpc.Classifier(compact_after=-1)
+    c.initialize()
+    workload.install_services(c, wl)
+    s = osvc.FeatureService()
+    osvc.install_services(s, wl)
+    prod = sorted(f for f in c.dump_flows() if any(t in f for t in ("table=ServiceLB", "table=EndpointDNAT",
+                                                                    "table=SNATMark")))
+    assert prod == s.dump_flows() and len(prod) > 10
+    assert c.dump_groups() == s.dump_groups()
+    for cfg in wl.services[::3]:
+        c.uninstall_service_flows(cfg["ip"], cfg["port"], cfg["protocol"])
+        s.uninstall_service_flows(cfg["ip"], cfg["port"], cfg["protocol"])
+    gid, eps = next((g, e) for g, e in wl.groups.items() if len(e) >= 2)
+    c.install_service_group(gid, eps[:1])
+    s.install_service_group(gid, eps[:1])
+    prod = sorted(f for f in c.dump_flows() if any(t in f for t in ("table=ServiceLB", "table=EndpointDNAT",
+                                                                    "table=SNATMark")))
+    assert prod == s.dump_flows()
+    assert c.dump_groups() == s.dump_groups()
