@@ -518,6 +518,7 @@ GPC_HD uint32_t v6_bucket_words(uint32_t kw) { return kw == 1u ? 16u : 2u * v6_s
 // Wide slot of the delta epochs' overflow table (journal): masked address (4 words), len | kV6Valid,
 // code, 2 pad; 2 slots per 64-B bucket, two choices.
 constexpr uint32_t kV6SlotWords = 8, kV6BucketSlots = 2, kV6Valid = 0x100u;
+constexpr uint32_t kV6MaxNewLens = 3;  // prefix lengths a delta epoch may add (JournalHdr.v6_ovf_log2)
 GPC_HD void v6_mask(const uint32_t* a, uint32_t len, uint32_t* m) {
   for (int w = 0; w < 4; w++) {
     const int bits = int(len) - 32 * w;
@@ -646,12 +647,16 @@ GPC_HD void v6_load_bucket(const uint32_t* p, uint32_t words, uint32_t* w) {
 // descriptors (the kernel's LDS copy; null: those of the image). kOvf (IPv6 delta epochs): the
 // journal's overflow table `ovf` (2^ovf_log2 wide buckets, the LPM entries of prefixes interned since
 // the base) is probed in the same step, its loads issued with the base's: no extra dependent round.
+// ovf_log2: JournalHdr.v6_ovf_log2 (log2 in the low byte, new prefix lengths above it): a prefix of a
+// new length is a leaf interned since the base with an exact code and nothing below it, so when the
+// address is in one it is the address's deepest match: after the search, one probe per new length
+// (at most kV6MaxNewLens; wave-uniform, only in epochs that have them) replaces the code on a hit.
 template <int K, bool kOvf = false>
 GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)[4], uint32_t* code,
                      const uint32_t* ovf = nullptr, uint32_t ovf_log2 = 0, const V6Len* desc = nullptr) {
   const V6Lpm* L = reinterpret_cast<const V6Lpm*>(blob + lpm_off);
   const V6Len* D = desc ? desc : L->d;
-  const uint32_t omask = (1u << ovf_log2) - 1u;
+  const uint32_t omask = (1u << (ovf_log2 & 0xffu)) - 1u;
   int lo[K], hi[K];
   uint32_t rl[K][2];  // regional search: the length indexes (8 bits each); all-ones: global
 #pragma unroll
@@ -771,6 +776,26 @@ GPC_HD void v6_codes(const uint32_t* blob, uint32_t lpm_off, const uint32_t (*a)
       else hi[k] = mid - 1;
     }
   }
+  if constexpr (kOvf) {
+    for (uint32_t nl = ovf_log2 >> 8; nl; nl >>= 8) {
+      const uint32_t len = nl & 0xffu;
+      if (!len) continue;
+      uint32_t m[K][4], ow[K][2][kV6BucketWords];
+#pragma unroll
+      for (int k = 0; k < K; k++) {  // both choices of every address loaded before any compare
+        v6_mask(a[k], len, m[k]);
+        const uint64_t ok = v6_hkey(m[k], len);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+          v6_load_bucket(ovf + size_t(c ? hash_b2(ok, omask) : hash_b1(ok, omask)) * (kV6SlotWords * kV6BucketSlots),
+                         kV6BucketWords, ow[k][c]);
+      }
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        if (!v6_wide_find(ow[k][0], m[k], len, &code[k])) (void)v6_wide_find(ow[k][1], m[k], len, &code[k]);
+      }
+    }
+  }
 }
 GPC_HD uint32_t v6_code(const uint32_t* blob, uint32_t lpm_off, const uint32_t* a, const uint32_t* ovf = nullptr,
                         uint32_t ovf_log2 = 0) {
@@ -857,7 +882,9 @@ struct JournalHdr {
   uint32_t odead_off;      // journal tombstones: page table (0: none)
   uint32_t bloom_axes;     // as ImageHdr.bloom_axes, over every journal entry so far
   // IPv6 journals: LPM entries of the prefixes interned since the base (image.cpp extend_image6),
-  // a hash laid out like V6Lpm's (2^v6_ovf_log2 buckets) probed next to the base's; 0: none
+  // a hash laid out like V6Lpm's (2^(v6_ovf_log2 & 0xff) buckets) probed next to the base's; 0:
+  // none. Bytes 1..3 of v6_ovf_log2: prefix lengths the base does not search (0: none), whose
+  // leaves are probed in that hash after the binary search (v6_codes)
   uint32_t v6_ovf_off, v6_ovf_log2;
   uint32_t ext_off;        // ExtHdr of this epoch's point extensions (0: none)
   uint32_t jflags;         // kJUsed: the journal holds records, tombstones or hard rules (else only extensions)

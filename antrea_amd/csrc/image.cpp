@@ -161,6 +161,9 @@ class V6Codes {
   std::vector<Node> nodes;  // nodes[0] = ::/0
   int max_clen = 0;
   std::set<int> lens;       // distinct node lengths (root excluded)
+  // lengths first seen in delta epochs (add_leaf), at most kV6MaxNewLens: their leaves are probed
+  // in the journal's overflow table after the binary search (core.hpp v6_codes), not searched
+  std::set<int> new_lens;
 
   int build(const FeatureNP& np, std::string* err) {
     std::vector<std::pair<u128, int>> pf;
@@ -181,6 +184,8 @@ class V6Codes {
     pf.erase(std::unique(pf.begin(), pf.end()), pf.end());
     nodes.assign(1, Node{0, 0});
     index_.clear();
+    lens.clear();
+    new_lens.clear();
     std::vector<int> st{0};
     for (auto& p : pf) {
       while (st.size() > 1) {
@@ -244,24 +249,30 @@ class V6Codes {
   // Interns a prefix that appeared after the build (a delta commit) without changing any existing
   // code: it must be a leaf (no interned prefix below it) and gets an exact code from the free
   // space of its deepest containing node. Every rule term of that node (a code prefix) and of its
-  // ancestors still covers it, so no other rule changes. Returns the node id, or -1 when the tree
-  // has to be rebuilt (not a leaf, no free code, or a prefix length the LPM does not search).
+  // ancestors still covers it, so no other rule changes. A length the base LPM does not search is
+  // taken as one of at most kV6MaxNewLens new lengths (probed directly: a leaf is the deepest match
+  // of every address in it). Returns the node id, or -1 when the tree has to be rebuilt (not a
+  // leaf, below a leaf added since the build, no free code, or too many new lengths).
   int add_leaf(u128 v, int len) {
-    if (len <= 0 || !lens.count(len)) return -1;
+    if (len <= 0) return -1;
+    const bool fresh = !lens.count(len) && !new_lens.count(len);
+    if (fresh && new_lens.size() >= kV6MaxNewLens) return -1;
     v &= v6_prefix_mask(len);
     auto hit = index_.find({v, len});
     if (hit != index_.end()) return hit->second;
     const u128 last = len >= 128 ? v : v | ~v6_prefix_mask(len);
     auto it = index_.upper_bound({v, len});
     if (it != index_.end() && it->first.first <= last) return -1;  // an interned prefix lies below it
-    int P = 0;
-    for (auto l = lens.rbegin(); l != lens.rend() && !P; ++l) {
-      if (*l >= len) continue;
-      auto a = index_.find({v & v6_prefix_mask(*l), *l});
-      if (a != index_.end()) P = a->second;
-    }
+    int P = 0, plen = 0;  // deepest containing node, over the searched and the new lengths
+    for (const std::set<int>* ls : {&lens, &new_lens})
+      for (int l : *ls) {
+        if (l >= len || l <= plen) continue;
+        auto a = index_.find({v & v6_prefix_mask(l), l});
+        if (a != index_.end()) P = a->second, plen = l;
+      }
     Node& p = nodes[size_t(P)];
     if (p.none_clen < 0 || p.none_clen >= 32 || p.next_free >= (uint64_t(1) << (32 - p.none_clen))) return -1;
+    if (fresh) new_lens.insert(len);
     Node k{v, len};
     k.parent = P;
     k.code = p.code + uint32_t(p.next_free++);
@@ -275,7 +286,7 @@ class V6Codes {
   }
   uint32_t n_added = 0;  // prefixes interned by add_leaf since the build
   const char* why_not(u128 v, int len) const {  // the reason add_leaf refused (debug output)
-    if (!lens.count(len)) return "new prefix length";
+    if (!lens.count(len) && !new_lens.count(len) && new_lens.size() >= kV6MaxNewLens) return "too many new prefix lengths";
     const u128 last = len >= 128 ? v : v | ~v6_prefix_mask(len);
     auto it = index_.upper_bound({v, len});
     if (it != index_.end() && it->first.first <= last) return "an interned prefix lies below it";
@@ -2006,10 +2017,12 @@ int extend_image6(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t h
     }
     const V6Codes::Node& N = codes.nodes[size_t(id)];
     // the prefix itself, then a marker at every shorter length its binary search passes through
-    // (build_image6), carrying the code of its deepest ancestor no longer than that length
+    // (build_image6), carrying the code of its deepest ancestor no longer than that length; a new
+    // length is probed directly after the search (no markers)
     const int t = int(std::lower_bound(lens.begin(), lens.end(), uint32_t(len)) - lens.begin());
-    if (t >= int(lens.size()) || lens[size_t(t)] != uint32_t(len)) return -GPC_EINVAL;
     put(v, uint32_t(len), N.code);
+    if (codes.new_lens.count(len)) return GPC_OK;
+    if (t >= int(lens.size()) || lens[size_t(t)] != uint32_t(len)) return -GPC_EINVAL;
     int lo = 0, hi = int(lens.size()) - 1;
     while (lo <= hi) {
       const int mid = (lo + hi) / 2;
@@ -2051,7 +2064,9 @@ int extend_image6(const FeatureNP& np, const std::set<uint32_t>& conj, uint8_t h
     std::vector<uint32_t> tab;
     uint32_t lg = 0;
     if (!v6_hash_build(sl, 0.5, &tab, &lg)) return -GPC_ENOMEM;
-    j6->set_v6_overflow(std::move(tab), lg);
+    uint32_t packed = 0, k = 0;  // JournalHdr.v6_ovf_log2: the new lengths above the log2 byte
+    for (int l : codes.new_lens) packed |= uint32_t(l) << (8 * ++k);
+    j6->set_v6_overflow(std::move(tab), lg | packed);
   }
   return GPC_OK;
 }

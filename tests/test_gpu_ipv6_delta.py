@@ -103,3 +103,32 @@ def test_gpu_upload_failure_then_delta_resyncs():
     assert c.image_stats()["v6_overlay_rules"] > 0
     _cmp(c.classify6_host(cols6), emu.classify6(c, cols6), cols)
     _cmp(c.classify_host(cols), emu.classify(c, cols), cols)
+
+
+def test_gpu_new_prefix_lengths_incremental():
+    """New IPv6 prefix lengths in a delta epoch (core.hpp v6_codes: probes of the new lengths after
+    the binary search) on the device: no IPv6 rebuild, device == emulation == Python oracle."""
+    from tests.test_ipv6_delta import _hit_packets, _oracle_after
+    wl = workload.config3(seed=11, n_policies_per_dir=6, rules_per_policy=8)
+    rules6 = workload.to_ipv6(wl).rules
+    c = gpc.Classifier(ipv4=False, ipv6=True, compact_after=-1)
+    c.initialize()
+    c.batch_install_policy_rule_flows(copy.deepcopy(rules6))
+    c.commit()
+    r = next(r for r in rules6 if r["direction"] == "In" and r.get("from") and r["action"] == "Allow")
+    log = [{"op": "add", "fid": r["flow_id"], "side": "src", "addrs": [{"ipnet": net}], "priority": r.get("priority")}
+           for net in ("2001:db8:1234::/47", "2001:db8:5678::/61", "2001:db9::/77")]
+    full0 = c.image_stats()["v6_full_builds"]
+    for o in log:
+        mcf.apply(c, [o])
+        c.commit()
+    assert c.image_stats()["v6_full_builds"] == full0
+    srcs = ["2001:db8:1234::1", "2001:db8:1235::1", "2001:db8:5678::9", "2001:db8:5679::9", "2001:db9::42",
+            "2001:db9:0:1::1", "2001:db7::1", "fd00:10::a00:1"] * 40
+    cols6 = _hit_packets(r, srcs)
+    got = c.classify6_host(cols6)
+    _cmp(got, emu.classify6(c, cols6), cols6)
+    n = 8
+    sub = {k: v[:n] for k, v in cols6.items()}
+    _cmp(got[:n], _oracle_after(rules6, log, sub, n, False), sub)
+    assert (got[:, 1]["conj_id"] == r["flow_id"]).sum() >= 3 * 40

@@ -138,16 +138,61 @@ def _oracle_after(rules, log, cols6, n, dual):
     return out
 
 
-def test_new_prefix_length_falls_back_to_full_build():
-    """A prefix length the LPM does not search yet cannot be interned in place: that commit
-    rebuilds the IPv6 image (and the verdicts stay right)."""
+def _hit_packets(r, srcs):
+    """IPv6 packets from `srcs` that match every clause of ingress rule r but its From."""
+    import ipaddress
+    n = len(srcs)
+    svc = r["service"][0]
+    proto = {"TCP": 6, "UDP": 17}[svc["protocol"]]
+    return {"src6": np.array([list(ipaddress.ip_address(a).packed) for a in srcs], np.uint8),
+            "dst6": np.tile(np.frombuffer(ipaddress.ip_address("fd00:10::a00:5").packed, np.uint8), (n, 1)),
+            "sport": np.full(n, 40000, np.uint16), "dport": np.full(n, svc["port"], np.uint16),
+            "proto": np.full(n, proto, np.uint8), "out_port": np.full(n, r["to"][0]["ofport"], np.uint32)}
+
+
+def test_new_prefix_lengths_are_incremental():
+    """a delta epoch that brings prefix lengths the base LPM does not search
+    interns them in place (up to kV6MaxNewLens = 3 new lengths, leaves probed in the journal's
+    overflow hash after the binary search): no IPv6 rebuild, verdicts == the Python oracle for
+    addresses inside and next to the new prefixes. A fourth new length, or a prefix below a leaf
+    added since the base, rebuilds the IPv6 image (and the verdicts stay right)."""
     wl = _wl()
-    c6 = _ctx(workload.to_ipv6(wl).rules, False, True)
-    r = next(r for r in wl.rules if r.get("from"))
-    c6.add_policy_rule_address(r["flow_id"], "src", [{"ipnet": "2001:db8:1234::/47"}], r.get("priority"))
-    emu.commit_host(c6)
-    st = c6.image_stats()
-    assert st["v6_full_builds"] == 2 and st["v6_delta_builds"] == 0
-    c6.add_policy_rule_address(r["flow_id"], "src", ["2001:db8:1234::7"], r.get("priority"))
-    emu.commit_host(c6)
-    assert c6.image_stats()["v6_delta_builds"] == 1
+    rules6 = workload.to_ipv6(wl).rules
+    c6 = _ctx(rules6, False, True)
+    r = next(r for r in rules6 if r["direction"] == "In" and r.get("from") and r["action"] == "Allow")
+    log = []
+
+    def add(addr):
+        o = {"op": "add", "fid": r["flow_id"], "side": "src", "addrs": [addr], "priority": r.get("priority")}
+        mcf.apply(c6, [o])
+        log.append(o)
+        emu.commit_host(c6)
+        return c6.image_stats()
+
+    full0 = c6.image_stats()["v6_full_builds"]
+    lens = {int(a["ipnet"].split("/")[1]) for rr in rules6 for side in ("from", "to") for a in rr.get(side) or []
+            if isinstance(a, dict) and "ipnet" in a}
+    new = [L for L in (47, 61, 77, 93) if L not in lens]
+    assert len(new) == 4
+    nets = ["2001:db8:1234::/%d" % new[0], "2001:db8:5678::/%d" % new[1], "2001:db9::/%d" % new[2]]
+    for k, net in enumerate(nets):
+        st = add({"ipnet": net})
+        assert st["v6_full_builds"] == full0 and st["v6_delta_builds"] == k + 1, (net, st)
+    srcs = ["2001:db8:1234::1", "2001:db8:1235::1", "2001:db8:5678::9", "2001:db8:5679::9", "2001:db9::42",
+            "2001:db9:0:1::1", "2001:db7::1", "fd00:10::a00:1"]
+    cols6 = _hit_packets(r, srcs)
+    want = _oracle_after(rules6, log, cols6, len(srcs), False)
+    got = emu.classify6(c6, cols6)
+    _cmp(got, want, cols6)
+    assert (got[:, 1]["conj_id"] == r["flow_id"]).sum() >= 3
+    # a fourth new length: full rebuild
+    st = add({"ipnet": "2001:dba::/%d" % new[3]})
+    assert st["v6_full_builds"] == full0 + 1
+    # below a leaf interned since the (new) base: full rebuild again
+    st = add({"ipnet": "2001:dbb::/%d" % new[0]})
+    assert st["v6_full_builds"] == full0 + 1
+    st = add({"ipnet": "2001:dbb::/%d" % (new[0] + 16)})
+    assert st["v6_full_builds"] == full0 + 2
+    srcs += ["2001:dba::5", "2001:dbb::1", "2001:dbb:1::1"]
+    cols6 = _hit_packets(r, srcs)
+    _cmp(emu.classify6(c6, cols6), _oracle_after(rules6, log, cols6, len(srcs), False), cols6)
