@@ -601,7 +601,8 @@ static void launch(const EpochArgs& ep, const gpc_pkt_soa& pk, uint64_t n, gpc_v
   // profiles/r06b_*): no egress verdict round trip through HBM and one read of the packet columns.
   // GPC_FUSED=0 / 1 forces the split / the single launch (A/B experiments).
   static const int fused_env = std::getenv("GPC_FUSED") ? std::atoi(std::getenv("GPC_FUSED")) : -1;
-  const bool fused = fused_env == 1 || (fused_env < 0 && !ep.sort_table[0] && !ep.sort_table[1]);
+  // (journal epochs keep the split: their fused kernel would spill at 5 waves)
+  const bool fused = fused_env == 1 || (fused_env < 0 && kDelta != kModeJournal && !ep.sort_table[0] && !ep.sort_table[1]);
   if (fused) {
     launch_mark(marks, kLaunchBoth, stream);
     hipLaunchKernelGGL((classify_kernel<kDelta, false, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, stream, ep, pk, n, o,

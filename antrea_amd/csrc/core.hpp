@@ -355,6 +355,7 @@ constexpr uint32_t kHashSlots = 2;  // 16-B buckets, two choices: one 16-B load 
 GPC_HD uint32_t hash_b1(uint64_t k, uint32_t mask) { return uint32_t(mix64(k)) & mask; }
 GPC_HD uint32_t hash_b2(uint64_t k, uint32_t mask) { return uint32_t(mix64(k) >> 32) & mask; }
 
+
 // Entry filter bits. IP axes: band 1/2/3/4 = prefix length 8-15 / 16-23 / 24-31 / 32 keyed by the
 // top 8 / 16 / 24 / 32 address bits; exact axes (in_port, reg1, reg7, tun_id): band 4 keyed by the value.
 constexpr uint32_t kFiltIpBits = 20, kFiltL4Shift = 20, kFiltL4Bits = 12;
@@ -403,6 +404,32 @@ GPC_HD void dir_list(const uint32_t* blob, const SubIdx& si, uint32_t b, uint32_
                          4u * uint32_t(__builtin_popcount(q.z & m));
   *lo = si.ent / 4u + start;
   *hi = *lo + c;
+}
+// Host-set combinations (round 6, image.cpp build_composite): a composite sub-index with band
+// kBandCombo is keyed by the packet's combination id -- from the membership hash at word SubIdx.pres
+// (combo_of) -- instead of by its address; its entries are exact-value entries whose Bloom axis
+// field is kFiltCombo and whose lo / hi carry the combination id in their top bytes.
+constexpr uint32_t kBandCombo = 5, kFiltCombo = 14u;
+GPC_HD uint64_t combo_key64(uint32_t v) { return (uint64_t(0xC0B0u) << 32) | v; }
+// Combination id of host value v (0: in no set of the sub-index): both 16-B buckets loaded together.
+GPC_HD uint32_t combo_of(const uint32_t* blob, uint32_t off, uint32_t v) {
+  const uint32_t* t = blob + off;
+  const uint32_t mask = (1u << t[0]) - 1u;
+  const uint64_t k = combo_key64(v);
+  const uint32_t* b1 = t + 4 + 4 * size_t(hash_b1(k, mask));
+  const uint32_t* b2 = t + 4 + 4 * size_t(hash_b2(k, mask));
+  GPC_TOUCH(b1, 16);
+  GPC_TOUCH(b2, 16);
+#if defined(__HIPCC__)
+  const uint4 q1 = *reinterpret_cast<const uint4*>(b1), q2 = *reinterpret_cast<const uint4*>(b2);
+#else
+  const struct { uint32_t x, y, z, w; } q1 = {b1[0], b1[1], b1[2], b1[3]}, q2 = {b2[0], b2[1], b2[2], b2[3]};
+#endif
+  return (q1.x == v ? q1.y : 0u) | (q1.z == v ? q1.w : 0u) | (q2.x == v ? q2.y : 0u) | (q2.z == v ? q2.w : 0u);
+}
+// Bucket key of a composite sub-index for the packet: its band key, or its combination id.
+GPC_HD uint32_t ckey_of(const uint32_t* blob, const SubIdx& si, uint32_t v) {
+  return si.band == kBandCombo ? combo_of(blob, si.pres, v) : v;
 }
 // Entries listed under bucket b of a sub-index (either format; host statistics).
 GPC_HD uint32_t sub_bucket_len(const uint32_t* blob, const SubIdx& si, uint32_t b) {
@@ -1203,16 +1230,21 @@ GPC_HD bool hard_fast_match(const Img& im, const HardFast& hf, const Pkt& p) {
 // xv: the packet's value of the table's composite axis (exact-value entries; any value elsewhere).
 // kSetProbes (base images): a probe entry's low 20 bits are its point set's id, not Bloom bits --
 // the probe itself is the test (a set large enough for the point hash saturates 20 Bloom bits).
+// cp: the packet's combination id (kBandCombo lists; 16 bits).
 template <bool kSetProbes = true>
-GPC_HD bool entry_pass(const Pkt& p, const Ent& e, uint32_t xv) {  // branch-free
+GPC_HD bool entry_pass(const Pkt& p, const Ent& e, uint32_t xv, uint32_t cp = 0u) {  // branch-free
   const uint32_t bax = e.x & 15u, iax = (e.x >> 4) & 15u;
+  const bool exact = (e.x & kEntExactX) != 0u;
   const bool l4 = (e.y & p.l4m) != 0u;
   // Bloom axis < 8: IP / exact-axis bits; 8..14 (probe entry): set id (base) or the probed clause's
-  // Bloom bits (journal); 15: none
+  // Bloom bits (journal); 15: none. Exact-value entries: 15, or kFiltCombo (a combination list)
   const bool bl = (bax == kFiltNoAxis) | (kSetProbes & (bax >= 8u)) | ((e.y & p.fm[bax & 7u]) != 0u);
+  const bool cmb = exact & (bax == kFiltCombo);
+  const uint32_t lo = cmb ? e.lo & 0xffffffu : e.lo, hi = cmb ? e.hi & 0xffffffu : e.hi;
+  const bool cok = !cmb | (((e.lo >> 24) | ((e.hi >> 24) << 8)) == cp);
   const uint32_t v = p.ax[iax < AX_N ? iax : 0];
-  const bool iv = (iax == kFiltNoAxis) | ((e.lo <= v) & (v <= e.hi));
-  return ((e.x & kEntExactX) ? e.y == xv : l4 & bl) & iv;
+  const bool iv = (iax == kFiltNoAxis) | ((lo <= v) & (v <= hi));
+  return (exact ? (e.y == xv) & cok : l4 & bl) & iv;
 }
 
 // Scan length of one table for the packet (the driver clause's candidate count, as eval_part picks
@@ -1225,7 +1257,9 @@ GPC_HD uint32_t scan_estimate(const Img& im, uint32_t table, const Pkt& p) {
     uint32_t c = th.always_n[th.cband];
     for (uint32_t i = 0; i < th.n_cidx && i < uint32_t(kIdxPerClause); i++) {
       const SubIdx& si = th.cidx[i];
-      const uint32_t bk = cbucket_of(si.band, si.bits, p.ax[si.axis], p.ax[th.cx]);
+      const uint32_t key = ckey_of(im.blob, si, p.ax[si.axis]);
+      if (si.band == kBandCombo && key == 0u) continue;
+      const uint32_t bk = cbucket_of(si.band, si.bits, key, p.ax[th.cx]);
       c += sub_bucket_len(im.blob, si, bk);
     }
     return c;
@@ -1260,7 +1294,7 @@ constexpr int kScanUnroll = GPC_SCAN_UNROLL;  // entry loads in flight per lane 
 // entry with one compare instead of kLists - 1.
 template <int kL>
 GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const uint32_t* upto, uint32_t total,
-                       uint32_t after, uint32_t rH, uint32_t xv, uint32_t& c0, uint32_t& c1, bool& more) {
+                       uint32_t after, uint32_t rH, uint32_t xv, uint32_t cp, uint32_t& c0, uint32_t& c1, bool& more) {
   const Ent* E = reinterpret_cast<const Ent*>(im.blob);
   c0 = c1 = 0xffffffffu;
   more = false;
@@ -1286,8 +1320,8 @@ GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const ui
 #pragma unroll
     for (int u = 0; u < kScanUnroll; u++) {
       const uint32_t off = ent_off(ev[u].x);
-      ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u], xv);
-      probe |= ps[u] & ((ev[u].x & 15u) - 8u < 7u);
+      ps[u] = (off > after) & (off < rH) & entry_pass(p, ev[u], xv, cp);
+      probe |= ps[u] & ((ev[u].x & 15u) - 8u < 7u) & !(ev[u].x & kEntExactX);
     }
     // Probe entries that passed: exact membership of the packet in the non-driver point-set
     // clause (point hash, both choices loaded before the compare), one entry slot at a time
@@ -1296,7 +1330,7 @@ GPC_HD void scan_lists(const Img& im, const Pkt& p, const uint32_t* dl, const ui
 #pragma unroll
       for (int u = 0; u < kScanUnroll; u++) {
         const uint32_t pax = (ev[u].x & 15u) - 8u;
-        const bool need = ps[u] & (pax < 7u);
+        const bool need = ps[u] & (pax < 7u) & !(ev[u].x & kEntExactX);
         if (GPC_WAVE_ANY(need)) {
           if (need) ps[u] = hash_contains(im, set_key(set_key_hi(ev[u].y & (kPointSetMax - 1u), pax), p.ax[pax]));
         }
@@ -1439,6 +1473,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
   bool d1 = false;
   uint32_t d = 0;
   uint32_t always_n = 0;  // entries of the driver's always list to scan
+  uint32_t cp = 0;        // the packet's combination id (kBandCombo sub-index)
   if (nc) {
     d = th.cband;
     const uint32_t xv = p.ax[th.cx];
@@ -1447,6 +1482,18 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     const bool xin = (im.blob[th.xmap_off + (xb >> 5)] >> (xb & 31u)) & 1u;  // else no soft rule can match
     always_n = xin ? th.always_n[d] : 0u;
     uint32_t cnt = always_n;
+    // bucket keys: the band keys, or for a combination sub-index (table-uniform) the packet's
+    // combination id, looked up in the value-map word's round; 0 (in no set): an empty list
+    uint32_t key[kIdxPerClause];
+#pragma unroll
+    for (int i = 0; i < kIdxPerClause; i++) {
+      key[i] = 0u;
+      if (uint32_t(i) < nc) {
+        const SubIdx& si = th.cidx[i];
+        key[i] = si.band == kBandCombo ? combo_of(im.blob, si.pres, p.ax[si.axis]) : p.ax[si.axis];
+        if (si.band == kBandCombo) cp = key[i];
+      }
+    }
     if (th.cidx[0].fmt) {
       // bucket directories: one 16-B block per sub-index (and a pointer entry where a bucket
       // overflowed), read in the value-map word's round (fmt 1) or, where the map filters most
@@ -1458,16 +1505,16 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       if (th.cidx[0].fmt == 1) {
 #pragma unroll
         for (int i = 0; i < kIdxPerClause; i++)
-          if (uint32_t(i) < nc) {
+          if ((uint32_t(i) < nc) && (th.cidx[i].band != kBandCombo || key[i] != 0u)) {
             const SubIdx& si = th.cidx[i];
-            dir_list(im.blob, si, cbucket_of(si.band, si.bits, p.ax[si.axis], xv), &lo0[i], &hi0[i]);
+            dir_list(im.blob, si, cbucket_of(si.band, si.bits, key[i], xv), &lo0[i], &hi0[i]);
           }
       } else {
 #pragma unroll
         for (int i = 0; i < kIdxPerClause; i++)
-          if ((uint32_t(i) < nc) & xin) {
+          if ((uint32_t(i) < nc) & xin && (th.cidx[i].band != kBandCombo || key[i] != 0u)) {
             const SubIdx& si = th.cidx[i];
-            dir_list(im.blob, si, cbucket_of(si.band, si.bits, p.ax[si.axis], xv), &lo0[i], &hi0[i]);
+            dir_list(im.blob, si, cbucket_of(si.band, si.bits, key[i], xv), &lo0[i], &hi0[i]);
           }
       }
 #pragma unroll
@@ -1498,7 +1545,7 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
       bk[i] = pw[i] = 0;
       if (uint32_t(i) < nc) {
         const SubIdx& si = th.cidx[i];
-        bk[i] = cbucket_of(si.band, si.bits, p.ax[si.axis], xv);
+        bk[i] = cbucket_of(si.band, si.bits, key[i], xv);
         if (si.pres) {
           GPC_TOUCH(im.blob + si.pres + (bk[i] >> 5), 4);
           pw[i] = im.blob[si.pres + (bk[i] >> 5)];
@@ -1586,8 +1633,8 @@ GPC_HD TablePart eval_part(const Img& im, uint32_t table, const Pkt& p) {
     bool more;
     GPC_MARK(ST_SCAN);
     GPC_STAT(8, 1);
-    if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, xv, c0, c1, more);
-    else scan_lists<kLists>(im, p, dl, upto, total, after, rH, xv, c0, c1, more);
+    if (one_idx) scan_lists<2>(im, p, dl, upto, total, after, rH, xv, cp, c0, c1, more);
+    else scan_lists<kLists>(im, p, dl, upto, total, after, rH, xv, cp, c0, c1, more);
     GPC_MARK(ST_VER);
 #pragma unroll
     for (int q = 0; q < 2; q++) {

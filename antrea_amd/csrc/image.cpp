@@ -1079,7 +1079,13 @@ void build_bits(const std::vector<RuleB*>& rs, const std::vector<uint32_t>& rec_
 // MI355X (64M packets, profiles/r03h_*): C1 8.73 -> 8.51 ms, C2 14.00 -> 10.25, C3 10.66 -> 10.12,
 // C4 12.18 -> 11.38.
 constexpr size_t kCompositeMaxValues = 16;
+// Entries of a composite index at most (GPC_COMPOSITE_MAX_ENTRIES overrides, experiments)
 constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 24;  // 256 MB of entries at most
+uint64_t composite_max_entries() {
+  static const uint64_t v = std::getenv("GPC_COMPOSITE_MAX_ENTRIES")
+                                ? std::strtoull(std::getenv("GPC_COMPOSITE_MAX_ENTRIES"), nullptr, 0) : kCompositeMaxEntries;
+  return v;
+}
 // Band merging (round 5). Every sub-index is a probe -- a dependent bucket-offset load and an entry
 // load, lines of 25-30 MB arrays that miss L2 -- so a packet pays per band, not per entry. Per IP
 // axis of the band clause, the atoms of bands m.. are keyed at band m's granularity (one sub-index)
@@ -1101,6 +1107,48 @@ constexpr uint32_t kV6DefaultTags = 4;
 // the unsplit round-5 layout: exact, only slower for the addresses under it.
 constexpr size_t kV6SubBytesPerPrefix = 1024, kV6SubMinBudget = size_t(128) << 20, kV6SubMaxBudget = size_t(1) << 30;
 constexpr uint64_t kMergeMinBytes = uint64_t(16) << 20;
+// Host-set combinations (build_composite, core.hpp kBandCombo): applied to a host-address band
+// of at least kComboMinEntries (member, value) entries that at least halves them, with at most
+// kComboMax combinations (ids fit the entries' 16 spare bits).
+constexpr uint64_t kComboMinEntries = 1u << 16;
+constexpr size_t kComboMax = 65535;
+// Membership hash of a combination sub-index (core.hpp combo_of): {lg, 0, 0, 0}, then 2^lg buckets
+// of two {host value, combination id} slots, two choices, load <= 1/2 (combination 0: empty slot).
+uint32_t put_combo_members(const std::vector<std::pair<uint32_t, uint32_t>>& members, Blob& B, HostImage* out) {
+  uint32_t lg = 4;
+  while ((1ull << lg) < members.size()) lg++;
+  std::mt19937 rng(0xC0B0u);
+  for (;; lg++) {
+    const uint32_t mask = (1u << lg) - 1u;
+    std::vector<uint32_t> tab(4 + (size_t(4) << lg), 0u);
+    tab[0] = lg;
+    bool ok = true;
+    for (auto m : members) {
+      uint32_t v = m.first, c = m.second;
+      for (int kick = 0; kick < 500 && c; kick++) {
+        const uint64_t k = combo_key64(v);
+        const uint32_t b[2] = {hash_b1(k, mask), hash_b2(k, mask)};
+        for (int j = 0; j < 2 && c; j++)
+          for (int sl = 0; sl < 2 && c; sl++) {
+            uint32_t* q = &tab[4 + 4 * size_t(b[j]) + 2 * sl];
+            if (q[1] == 0) q[0] = v, q[1] = c, c = 0;
+          }
+        if (!c) break;
+        uint32_t* q = &tab[4 + 4 * size_t(b[rng() & 1u]) + 2 * (rng() & 1u)];  // evict, retry the victim
+        std::swap(q[0], v);
+        std::swap(q[1], c);
+      }
+      if (c) {
+        ok = false;
+        break;
+      }
+    }
+    if (!ok) continue;
+    out->bytes_hash += 4ull * tab.size();
+    return B.put(tab.data(), tab.size(), 16);
+  }
+}
+
 template <typename CE>
 void merge_bands(std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>>& sub, const std::vector<std::vector<uint32_t>>& xsets) {
   std::set<uint8_t> axes;
@@ -1120,7 +1168,7 @@ void merge_bands(std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>>& sub, co
         for (auto& e : kv.second) {
           for (uint64_t k = e.key.lo >> sh; k <= (e.key.hi >> sh) && !big; k++)
             for (uint32_t x : xsets[e.xi]) combos.push_back((k << 32) | x);
-          big = combos.size() > kCompositeMaxEntries;
+          big = combos.size() > composite_max_entries();
         }
       }
       if (big || combos.empty()) continue;
@@ -1181,6 +1229,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     std::vector<std::vector<uint32_t>> xsets;
     std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>> sub;
     std::vector<std::pair<uint32_t, uint32_t>> xpatch;  // (record word 5 offset, skip bits) of exact-value rules
+    std::vector<uint32_t> xi_rank;                      // rule of each value list (rank in rs)
     const bool exact_ok = !std::getenv("GPC_NO_EXACT_X");  // (experiments)
     for (size_t rank = 0; rank < rs.size() && ok; rank++) {
       const RuleB& r = *rs[rank];
@@ -1229,14 +1278,117 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
         sub[{key.axis, key.band}].push_back({key, uint32_t(xsets.size()), ent});
       }
       xsets.push_back(std::move(xs));
+      xi_rank.push_back(uint32_t(rank));
     }
     if (!ok || nsoft == 0 || X < 0) continue;
     if (!mb) merge_bands(sub, xsets);
     if (sub.size() > size_t(kIdxPerClause)) continue;
+    // Host-set combinations (round 6, core.hpp kBandCombo): the host-address band of an IP axis
+    // whose atoms are large shared sets (AddressGroups of Pod IPs) is keyed by the packet's
+    // combination -- the interned set of those host sets that contain its address (a membership
+    // hash, value -> combination id) -- instead of by the address. Each rule is listed once per
+    // (combination holding its set, value of its other clause), not once per (member, value): C2g
+    // (16 groups of 10 000 Pod IPs) 24 M entries -> far fewer, each list the few rules whose group
+    // holds the packet's source AND whose AppliedTo holds its value. The entries are exact-value
+    // entries that also carry the combination id (16 bits in the top bytes of lo / hi), so the
+    // band clause is decided by the entry too (record word 5 skips it for rules keyed only here).
+    std::pair<uint8_t, uint8_t> combo_key{0xff, 0xff};
+    std::vector<std::pair<uint64_t, std::array<uint32_t, 4>>> combo_ents;  // (combo << 32 | x, entry)
+    std::vector<std::pair<uint32_t, uint32_t>> combo_members;               // (host value, combo id)
+    std::map<uint32_t, uint32_t> combo_rules;  // rules keyed only by combinations: (record word 5, skip bits)
+    if (!std::getenv("GPC_NO_COMBO")) {  // (experiments)
+      for (auto& kv : sub) {
+        if (kv.first.second != 4 || kv.first.first > AX_CTDST || combo_key.first != 0xff) continue;
+        std::map<uint32_t, std::vector<uint32_t>> hosts;  // rule (xi) -> its host values in this band
+        std::map<uint32_t, std::array<uint32_t, 4>> tmpl;  // rule (xi) -> its combination entry
+        std::map<uint32_t, uint32_t> skips;                // rule (xi) -> clauses its entry decides
+        bool elig = true;
+        uint64_t old_n = 0;
+        for (auto& e : kv.second) {
+          elig = elig && e.key.lo == e.key.hi && rec_off[xi_rank[e.xi]] < (1u << 27);
+          if (!elig) break;
+          hosts[e.xi].push_back(e.key.lo);
+          old_n += xsets[e.xi].size();
+          if (tmpl.count(e.xi)) continue;
+          // the entry decides the value clause (y) and the band clause (combination id); the rule's
+          // third clause, if any, must be on a port axis: its hull is the entry's interval, decided
+          // when it is one interval, else verified from the record
+          const RuleB& r = *rs[xi_rank[e.xi]];
+          uint32_t sax = kFiltNoAxis, slo = 0, shi = 0, skip = (1u << ce) | (1u << cb);
+          if (r.n == 3) {
+            const int sc = 3 - cb - ce;
+            const auto& cl = r.clause[sc];
+            const uint32_t a0 = cl.empty() || cl[0].t.size() != 1 ? uint32_t(AX_N) : cl[0].t[0].axis;
+            elig = (a0 == AX_L4D || a0 == AX_L4S) && clause_hull(cl, a0, &slo, &shi) && shi <= 0xffffffu;
+            if (!elig) break;
+            sax = a0;
+            if (clause_is_interval(cl, a0, slo, shi)) skip |= 1u << sc;
+          } else if (r.n != 2) {
+            elig = false;
+            break;
+          }
+          tmpl[e.xi] = {((rec_off[xi_rank[e.xi]] >> 4) << 8) | (sax << 4) | kFiltCombo | kEntExactX, 0u, slo, shi};
+          skips[e.xi] = skip;
+        }
+        if (!elig || old_n < kComboMinEntries) continue;
+        std::map<std::vector<uint32_t>, uint32_t> set_ids;
+        std::vector<std::vector<uint32_t>> set_rules;  // set id -> rules (xi)
+        for (auto& h : hosts) {
+          std::sort(h.second.begin(), h.second.end());
+          h.second.erase(std::unique(h.second.begin(), h.second.end()), h.second.end());
+          auto ins = set_ids.emplace(h.second, uint32_t(set_ids.size()));
+          if (ins.second) set_rules.emplace_back();
+          set_rules[ins.first->second].push_back(h.first);
+        }
+        std::unordered_map<uint32_t, std::vector<uint32_t>> pat;  // host value -> set ids (ascending)
+        for (auto& si : set_ids)
+          for (uint32_t v : si.first) pat[v].push_back(si.second);
+        std::map<std::vector<uint32_t>, uint32_t> combos;
+        std::vector<std::pair<uint32_t, uint32_t>> members;
+        members.reserve(pat.size());
+        for (auto& pv : pat) {
+          auto ins = combos.emplace(pv.second, uint32_t(combos.size() + 1));
+          members.push_back({pv.first, ins.first->second});
+        }
+        if (combos.size() > kComboMax) continue;
+        uint64_t new_n = 0;
+        for (auto& c : combos)
+          for (uint32_t sid : c.first)
+            for (uint32_t xi : set_rules[sid]) new_n += xsets[xi].size();
+        if (new_n * 2 > old_n) continue;  // not worth a dependent membership load
+        std::vector<std::pair<uint64_t, std::array<uint32_t, 4>>> ents;
+        ents.reserve(new_n);
+        for (auto& c : combos)
+          for (uint32_t sid : c.first)
+            for (uint32_t xi : set_rules[sid])
+              for (uint32_t x : xsets[xi]) {
+                std::array<uint32_t, 4> en = tmpl[xi];
+                en[1] = x;
+                en[2] = (en[2] & 0xffffffu) | ((c.second & 0xffu) << 24);
+                en[3] = (en[3] & 0xffffffu) | (((c.second >> 8) & 0xffu) << 24);
+                ents.push_back({(uint64_t(c.second) << 32) | x, en});
+              }
+        // rules whose every band-clause entry is in this band: the combination decides the clause
+        std::map<uint32_t, size_t> n_all, n_here;
+        for (auto& kv2 : sub)
+          for (auto& e : kv2.second) (kv2.first == kv.first ? n_here : n_all)[e.xi]++;
+        for (auto& h : tmpl)
+          if (!n_all.count(h.first)) combo_rules[rec_off[xi_rank[h.first]] + 5] = skips[h.first] << (3 * cb);
+        if (std::getenv("GPC_IMAGE_DEBUG"))
+          std::fprintf(stderr, "table %d composite axis %u: %zu host sets, %zu combinations over %zu hosts: %llu -> %llu entries\n",
+                       t, kv.first.first, set_ids.size(), combos.size(), members.size(), (unsigned long long)old_n,
+                       (unsigned long long)new_n);
+        combo_key = kv.first;
+        combo_ents.swap(ents);
+        combo_members.swap(members);
+      }
+    }
     uint64_t total = 0;
     for (auto& kv : sub)
-      for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size();
-    if (total > kCompositeMaxEntries) continue;
+      if (kv.first == combo_key) total += combo_ents.size();
+      else
+        for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size();
+    if (total > composite_max_entries()) continue;
     std::vector<std::pair<uint32_t, std::array<uint32_t, 4>>> be;
     // 2^extra buckets per entry: fewer hash collisions per probe. Round 4 (offset pairs, C3 / C2):
     // extra 0 -> 10.48 / 10.98 ms, 1 -> 10.12 / 10.25 ms, 2 -> 10.10 / 10.05 ms with 40 % more image.
@@ -1251,22 +1403,30 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     const char* de = std::getenv("GPC_COMPOSITE_DIR");
     const int dir_fmt = de ? std::min(2, std::max(0, std::atoi(de))) : (X > AX_CTDST ? 1 : 2);
     for (auto& kv : sub) {
-      const uint8_t axis = kv.first.first, band = kv.first.second;
+      const bool combo = kv.first == combo_key;
+      const uint8_t axis = kv.first.first, band = combo ? uint8_t(kBandCombo) : kv.first.second;
       uint64_t n = 0;
-      for (auto& e : kv.second) n += atom_span(e.key) * xsets[e.xi].size();
+      if (combo) n = combo_ents.size();
+      else
+        for (auto& e : kv.second) n += atom_span(e.key) * xsets[e.xi].size();
       uint32_t bits = 10;
-      while (bits < 22 && (1ull << bits) < n) bits++;
-      bits = std::min(24u, bits + extra);
+      while (bits < 24 && (1ull << bits) < n) bits++;
+      bits = std::min(26u, bits + extra);
       const uint32_t sh = ip_band_shift(band);
       be.clear();
-      for (auto& e : kv.second)
-        for (uint64_t k = e.key.lo >> sh; k <= (e.key.hi >> sh); k++)
-          for (uint32_t x : xsets[e.xi]) {
-            std::array<uint32_t, 4> en = e.ent;
-            if (en[0] & kEntExactX) en[1] = x;
-            else out->hdr.bloom_axes |= bloom_axis_bit(en[0]) | kBloomL4;
-            be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), en});
-          }
+      if (combo) {
+        for (auto& ce : combo_ents)
+          be.push_back({cbucket_of(band, bits, uint32_t(ce.first >> 32), uint32_t(ce.first)), ce.second});
+      } else {
+        for (auto& e : kv.second)
+          for (uint64_t k = e.key.lo >> sh; k <= (e.key.hi >> sh); k++)
+            for (uint32_t x : xsets[e.xi]) {
+              std::array<uint32_t, 4> en = e.ent;
+              if (en[0] & kEntExactX) en[1] = x;
+              else out->hdr.bloom_axes |= bloom_axis_bit(en[0]) | kBloomL4;
+              be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), en});
+            }
+      }
       std::sort(be.begin(), be.end());
       be.erase(std::unique(be.begin(), be.end()), be.end());
       const uint32_t nb = 1u << bits;
@@ -1278,7 +1438,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       si.axis = axis;
       si.band = band;
       si.bits = uint8_t(bits);
-      si.pres = 0;
+      si.pres = combo ? put_combo_members(combo_members, B, out) : 0u;
       si.fmt = uint8_t(dir_fmt);
       if (dir_fmt) {
         // core.hpp dir_list: a 16-B block per 32 buckets; lists of kDirCountMax or more entries
@@ -1344,6 +1504,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     th.cband = uint8_t(cb);
     th.cx = uint8_t(X);
     for (auto& pt : xpatch) B.w[pt.first] |= pt.second;
+    for (auto& pt : combo_rules) B.w[pt.first] |= pt.second;
     return;
   }
 }
