@@ -282,6 +282,8 @@ static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : -GPC_EDEV; }
 // 8.5 ms without). The array is therefore striped over `copies` replicas (block b updates copy
 // b mod copies), sized so the replicas together span >= 64 K slots, and folded into copy 0 before
 // anything reads it (gpc_counters, gpc_metrics). Large rule sets (C3: 89 k slots) keep one copy.
+// The allocation holds copies + 1 arrays: the kernels' accumulators, then the published array
+// that gpc_counters returns ({packets, bytes, sessions}; core.hpp count_stage).
 static uint32_t counter_copies_for(size_t cap) {
   if (const char* e = std::getenv("GPC_COUNTER_COPIES")) {  // experiments: fixed power of two <= 64
     uint32_t r = 1;
@@ -292,8 +294,11 @@ static uint32_t counter_copies_for(size_t cap) {
   while (r < 64 && cap * r < 65536) r <<= 1;
   return r;
 }
+static unsigned long long* published_counters(const DevState& D) {
+  return D.d_counters ? D.d_counters + size_t(D.counter_copies) * D.counter_cap * kCounterWords : nullptr;
+}
 static int fold_counters(DevState& D) {  // caller holds ctl; device synchronized on return
-  if (!D.d_counters || D.counter_copies <= 1) return GPC_OK;
+  if (!D.d_counters) return GPC_OK;
   if (hip_ok(hipSetDevice(D.device)) || hip_ok(hipDeviceSynchronize())) return -GPC_EDEV;
   int rc = launch_fold_counters(D.d_counters, uint64_t(D.counter_cap) * kCounterWords, D.counter_copies, nullptr);
   if (!rc) rc = hip_ok(hipDeviceSynchronize());
@@ -1076,8 +1081,8 @@ int gpc_replay(gpc_ctx* ctx) {
       }
     }
     if (!rc && !ctx->svc_blob.empty()) rc = upload_words(ctx->svc_blob, D.device, us, &ne[k].svc);
-    if (!rc && (hip_ok(hipMalloc(&nc[k], cap * kCounterBytes * copies)) ||
-                hip_ok(hipMemset(nc[k], 0, cap * kCounterBytes * copies))))
+    if (!rc && (hip_ok(hipMalloc(&nc[k], cap * kCounterBytes * (copies + 1))) ||
+                hip_ok(hipMemset(nc[k], 0, cap * kCounterBytes * (copies + 1)))))
       rc = -GPC_EDEV;
     if (!rc) rc = hip_ok(hipStreamSynchronize(us));
   }
@@ -1450,8 +1455,8 @@ int gpc_counters_on(gpc_ctx* ctx, uint32_t slot, uint64_t** dev, const uint32_t*
   if (!ctx || slot >= ctx->dev.size()) return -GPC_EINVAL;
   std::lock_guard<std::mutex> g(ctx->ctl);
   DevState& D = ctx->dev[slot];
-  if (int rc = fold_counters(D)) return rc;  // the caller sees one array (copy 0)
-  if (dev) *dev = reinterpret_cast<uint64_t*>(D.d_counters);
+  if (int rc = fold_counters(D)) return rc;  // the caller sees one array (the published one)
+  if (dev) *dev = reinterpret_cast<uint64_t*>(published_counters(D));
   if (slot_conj) *slot_conj = ctx->slot_conj.data();
   if (n_slots) *n_slots = ctx->slot_conj.size();
   return GPC_OK;
@@ -1463,7 +1468,7 @@ int gpc_reset_counters(gpc_ctx* ctx) {
   for (DevState& D : ctx->dev) {
     if (!D.d_counters) continue;
     if (hip_ok(hipSetDevice(D.device))) return -GPC_EDEV;
-    if (hip_ok(hipDeviceSynchronize()) || hip_ok(hipMemset(D.d_counters, 0, D.counter_cap * kCounterBytes * D.counter_copies)))
+    if (hip_ok(hipDeviceSynchronize()) || hip_ok(hipMemset(D.d_counters, 0, D.counter_cap * kCounterBytes * (D.counter_copies + 1))))
       return -GPC_EDEV;
   }
   return GPC_OK;
@@ -1479,7 +1484,7 @@ int gpc_metrics(gpc_ctx* ctx, gpc_rule_metric* out, size_t cap, size_t* n) {
     if (int rc = fold_counters(D)) return rc;
     if (!D.d_counters || h.empty()) continue;
     if (hip_ok(hipSetDevice(D.device)) || hip_ok(hipDeviceSynchronize()) ||
-        hip_ok(hipMemcpy(part.data(), D.d_counters, part.size() * 8, hipMemcpyDeviceToHost)))
+        hip_ok(hipMemcpy(part.data(), published_counters(D), part.size() * 8, hipMemcpyDeviceToHost)))
       return -GPC_EDEV;
     for (size_t i = 0; i < h.size(); i++) h[i] += part[i];
   }
@@ -1976,7 +1981,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     if (need > D.counter_cap) {
       new_cap[k] = std::max(need, D.counter_cap * 2);
       new_copies[k] = counter_copies_for(new_cap[k]);
-      const size_t bytes = new_cap[k] * kCounterBytes * new_copies[k];
+      const size_t bytes = new_cap[k] * kCounterBytes * (new_copies[k] + 1);
       nc[k] = nullptr;
       if (hip_ok(hipMalloc(&nc[k], bytes)) || hip_ok(hipMemset(nc[k], 0, bytes))) return fail(-GPC_EDEV);
     }
@@ -2022,14 +2027,15 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       // device has drained them, all its replicas are merged into the new copy 0 (atomically: new
       // launches may already be adding to it), so no count is lost however the growth interleaves.
       (void)hipDeviceSynchronize();
-      (void)launch_merge_counters(D.d_counters, old_counters[k], uint64_t(old_cap[k]) * kCounterWords, old_copies[k],
-                                  uint64_t(old_cap[k]) * kCounterWords, nullptr);
+      const uint64_t ow = uint64_t(old_cap[k]) * kCounterWords;
+      (void)launch_merge_counters(D.d_counters, old_counters[k], ow, old_copies[k], ow, nullptr);
+      (void)launch_merge_counters(published_counters(D), old_counters[k] + old_copies[k] * ow, ow, 1, ow, nullptr);
       (void)hipDeviceSynchronize();
       (void)hipFree(old_counters[k]);
     }
     for (uint32_t s : ctx->released_slots)
       if (s < D.counter_cap)
-        for (uint32_t r = 0; r < D.counter_copies; r++)
+        for (uint32_t r = 0; r <= D.counter_copies; r++)  // (the published array too)
           (void)hipMemsetAsync(D.d_counters + kCounterWords * (size_t(r) * D.counter_cap + s), 0, kCounterBytes,
                                D.ustream);
   }

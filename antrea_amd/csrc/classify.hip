@@ -670,18 +670,29 @@ int launch_trace(const EpochArgs& ep, const gpc_pkt_soa& pk, uint4* out, uint4* 
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 
+// One thread per counter slot: the accumulator copies {packets, bytes, non-session packets} are
+// drained (atomic exchange: a classification running concurrently on another stream loses no
+// update, it lands in the next fold) and added to the published copy as {packets, bytes, sessions}.
 __global__ void fold_counters_kernel(unsigned long long* __restrict__ c, uint64_t stride, uint32_t copies) {
-  const uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (w >= stride) return;
-  // atomics: a classification running concurrently on another stream loses no update
-  unsigned long long sum = 0;
-  for (uint32_t r = 1; r < copies; r++) sum += atomicExch(&c[r * stride + w], 0ull);
-  if (sum) atomicAdd(&c[w], sum);
+  const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (kCounterWords * s >= stride) return;
+  unsigned long long p = 0, b = 0, ns = 0;
+  for (uint32_t r = 0; r < copies; r++) {
+    unsigned long long* a = c + r * stride + kCounterWords * s;
+    p += atomicExch(&a[0], 0ull);
+    b += atomicExch(&a[1], 0ull);
+    ns += atomicExch(&a[2], 0ull);
+  }
+  unsigned long long* o = c + uint64_t(copies) * stride + kCounterWords * s;
+  if (p) atomicAdd(&o[0], p);
+  if (b) atomicAdd(&o[1], b);
+  if (p != ns) atomicAdd(&o[2], p - ns);  // (mod 2^64: a fold between a packet's two adds evens out next time)
 }
 
 int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t copies, hipStream_t stream) {
-  if (!counters || copies <= 1 || stride == 0) return 0;
-  hipLaunchKernelGGL(fold_counters_kernel, dim3(uint32_t((stride + 255) / 256)), dim3(256), 0, stream, counters, stride, copies);
+  if (!counters || copies == 0 || stride == 0) return 0;
+  const uint64_t slots = stride / kCounterWords;
+  hipLaunchKernelGGL(fold_counters_kernel, dim3(uint32_t((slots + 255) / 256)), dim3(256), 0, stream, counters, stride, copies);
   return hipGetLastError() == hipSuccess ? 0 : -GPC_EDEV;
 }
 

@@ -23,7 +23,8 @@ struct EpochArgs {
 // One packet (index 0 of the device columns) through the table walk with a per-table trace.
 int launch_trace(const EpochArgs& ep, const gpc_pkt_soa& pk, uint4* out, uint4* lb_out, TraceStep* steps, uint32_t* n_steps,
                  hipStream_t stream);
-// Sums counter copies 1..copies-1 into copy 0 and zeroes them (stride words per copy).
+// Drains the accumulator copies 0..copies-1 ({packets, bytes, non-session packets} per slot, stride
+// words per copy) into the published copy `copies` ({packets, bytes, sessions}): core.hpp count_stage.
 int launch_fold_counters(unsigned long long* counters, uint64_t stride, uint32_t copies, hipStream_t stream);
 // dst[w] += sum over r < copies of src[r * src_stride + w], w < n_words (device-scope atomics: launches
 // on other streams may be adding to dst concurrently). Used when the counter array grows.

@@ -40,18 +40,42 @@ def load():
     return _lib
 
 
+class _Counters:
+    """The kernels accumulate {packets, bytes, non-session packets} per slot (core.hpp count_stage);
+    the library publishes {packets, bytes, sessions} (api.cpp fold_counters). The emulation runs the
+    same count_stage into a raw array, added to the caller's array in the published format."""
+
+    def __init__(self, counters):
+        self.out = counters
+        self.raw = None
+        if counters is not None:
+            assert counters.dtype == np.uint64 and counters.flags.c_contiguous
+            self.raw = np.zeros_like(counters)
+
+    @property
+    def ptr(self):
+        return None if self.raw is None else self.raw.ctypes.data
+
+    def publish(self):
+        if self.raw is None:
+            return
+        r = self.raw.reshape(-1, 3)
+        o = self.out.reshape(-1, 3)
+        o[:, 0] += r[:, 0]
+        o[:, 1] += r[:, 1]
+        o[:, 2] += r[:, 0] - r[:, 2]
+
+
 def classify6(clf: "gpc.Classifier", cols, counters=None):
     """Emulated IPv6 verdicts (n, 2) of the IPv6 image last committed by `clf`."""
     blob, nw, hdr = clf.debug_image6()
     assert blob, "no IPv6 image (ipv6 disabled, or the IPv6 rule set was rejected)"
     soa, keep, n = gpc.pkt_soa_host(cols)
     out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
-    cptr = None
-    if counters is not None:
-        assert counters.dtype == np.uint64 and counters.flags.c_contiguous
-        cptr = counters.ctypes.data
+    cnt = _Counters(counters)
     pool, _, jhdr = clf.debug_epoch6()
-    load().emu_classify6(blob, hdr, pool, jhdr, C.byref(soa), n, out.ctypes.data, cptr)
+    load().emu_classify6(blob, hdr, pool, jhdr, C.byref(soa), n, out.ctypes.data, cnt.ptr)
+    cnt.publish()
     return out.reshape(n, 2)
 
 
@@ -64,16 +88,14 @@ def classify(clf: "gpc.Classifier", cols, counters=None, lb=None):
     pool, _, jhdr = clf.debug_epoch()
     soa, keep, n = gpc.pkt_soa_host(cols)
     out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
-    cptr = None
-    if counters is not None:
-        assert counters.dtype == np.uint64 and counters.flags.c_contiguous
-        cptr = counters.ctypes.data
+    cnt = _Counters(counters)
     svc = clf.debug_service_image()
     lptr = None
     if lb is not None:
         assert lb.dtype == gpc.LB_DTYPE and len(lb) >= n
         lptr = lb.ctypes.data
-    load().emu_classify(blob, hdr, pool, jhdr, svc, C.byref(soa), n, out.ctypes.data, lptr, cptr)
+    load().emu_classify(blob, hdr, pool, jhdr, svc, C.byref(soa), n, out.ctypes.data, lptr, cnt.ptr)
+    cnt.publish()
     return out.reshape(n, 2)
 
 
@@ -121,13 +143,11 @@ def classify_snapshot(snap, cols, counters=None):
     """Emulated verdicts (n, 2) of a snapshot() epoch."""
     soa, keep, n = gpc.pkt_soa_host(cols)
     out = np.zeros(2 * n, dtype=gpc.VERDICT_DTYPE)
-    cptr = None
-    if counters is not None:
-        assert counters.dtype == np.uint64 and counters.flags.c_contiguous
-        cptr = counters.ctypes.data
+    cnt = _Counters(counters)
     pool = snap["pool"].ctypes.data if snap["pool"] is not None else None
     load().emu_classify(snap["blob"].ctypes.data, snap["hdr"].ctypes.data, pool, snap["jhdr"], None, C.byref(soa), n,
-                        out.ctypes.data, None, cptr)
+                        out.ctypes.data, None, cnt.ptr)
+    cnt.publish()
     return out.reshape(n, 2)
 
 
