@@ -369,8 +369,16 @@ def _churn_loop(ops, rate, max_batch, stop, rec, interval=0.0):
     t0 = time.perf_counter()
     base = ops.issued
     last = t0 - interval
+    next_log = t0 + 5.0
     while not stop.is_set():
         now = time.perf_counter()
+        if now >= next_log and hasattr(ops.clf, "image_stats"):  # progress (a long C5 run must not look hung)
+            next_log = now + 5.0
+            st = ops.clf.image_stats()
+            _log("C5 %.0f s: %d ops, %d commits (last %.1f ms); journal rules %d, tombstones %d, extended rules %d, "
+                 "compactions %d, full builds %d" % (now - t0, ops.issued - base, len(rec), rec[-1][1] * 1e3 if rec else 0,
+                                                   st["n_overlay_rules"], st["n_tombstones"], st["n_ext_rules"],
+                                                   st["n_background_builds"], st["n_full_builds"]))
         due = int((now - t0) * rate) - (ops.issued - base)
         if due <= 0 or now - last < interval:
             time.sleep(0.0002)
@@ -960,6 +968,8 @@ def main(argv=None):
         starts[i].record(stream)
         dp.classify(soa, n, out, count, stream)
         ends[i].record(stream)
+        if churn and i % 1000 == 999:  # progress of a long C5 run (launches are paced: ~the device's rate)
+            _log("C5: %d steps launched" % (i + 1))
     dp.sync()
     if world > 1:
         dist.barrier()
