@@ -841,6 +841,27 @@ bool clause_is_interval(const std::vector<Atom>& atoms, uint8_t axis, uint32_t l
   return reach == hi;
 }
 
+// The clause's match set on `axis` as sorted disjoint intervals (single-term prefix atoms, merged
+// where they touch); false if some atom is not such a term.
+bool clause_intervals(const std::vector<Atom>& atoms, uint8_t axis, std::vector<std::pair<uint32_t, uint32_t>>* out) {
+  std::vector<std::pair<uint32_t, uint32_t>> iv;
+  for (auto& a : atoms) {
+    if (a.t.size() != 1 || a.t[0].axis != axis || !is_prefix(a.t[0].mask)) return false;
+    const uint32_t l = a.t[0].val & a.t[0].mask;
+    iv.push_back({l, l | ~a.t[0].mask});
+  }
+  if (iv.empty()) return false;
+  std::sort(iv.begin(), iv.end());
+  out->clear();
+  for (auto& x : iv) {
+    if (!out->empty() && uint64_t(x.first) <= uint64_t(out->back().second) + 1)
+      out->back().second = std::max(out->back().second, x.second);
+    else
+      out->push_back(x);
+  }
+  return true;
+}
+
 struct IvalChoice {
   int clause = -1;
   uint32_t axis = kFiltNoAxis, lo = 0, hi = 0;
@@ -1079,6 +1100,9 @@ void build_bits(const std::vector<RuleB*>& rs, const std::vector<uint32_t>& rec_
 // MI355X (64M packets, profiles/r03h_*): C1 8.73 -> 8.51 ms, C2 14.00 -> 10.25, C3 10.66 -> 10.12,
 // C4 12.18 -> 11.38.
 constexpr size_t kCompositeMaxValues = 16;
+// An exact-value entry decides a third clause of up to this many intervals (one entry per interval;
+// C2 / C2g services: 1-3 single ports), so candidates need no record read to verify it.
+constexpr size_t kExactMaxIntervals = 4;
 // Entries of a composite index at most (GPC_COMPOSITE_MAX_ENTRIES overrides, experiments)
 constexpr uint64_t kCompositeMaxEntries = uint64_t(1) << 24;  // 256 MB of entries at most
 uint64_t composite_max_entries() {
@@ -1230,7 +1254,10 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
     std::map<std::pair<uint8_t, uint8_t>, std::vector<CE>> sub;
     std::vector<std::pair<uint32_t, uint32_t>> xpatch;  // (record word 5 offset, skip bits) of exact-value rules
     std::vector<uint32_t> xi_rank;                      // rule of each value list (rank in rs)
+    // exact-value rules whose third clause is 2..kExactMaxIntervals intervals: one entry per interval
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> xivs;
     const bool exact_ok = !std::getenv("GPC_NO_EXACT_X");  // (experiments)
+    const bool multi_ok = !std::getenv("GPC_NO_EXACT_MULTI");  // (experiments)
     for (size_t rank = 0; rank < rs.size() && ok; rank++) {
       const RuleB& r = *rs[rank];
       if (r.hard) continue;
@@ -1257,13 +1284,19 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       int sc = -1;
       uint32_t sax = kFiltNoAxis, slo = 0, shi = 0;
       bool exact = exact_ok && r.n <= 3 && rec_off[rank] < (1u << 27);
+      std::vector<std::pair<uint32_t, uint32_t>> ivs;
       if (exact && r.n == 3) {
         sc = 3 - cb - ce;
         const auto& cl = r.clause[sc];
         exact = !cl.empty() && cl[0].t.size() == 1 && cl[0].t[0].axis < AX_N &&
-                clause_hull(cl, cl[0].t[0].axis, &slo, &shi) && clause_is_interval(cl, cl[0].t[0].axis, slo, shi);
-        if (exact) sax = cl[0].t[0].axis;
+                clause_intervals(cl, cl[0].t[0].axis, &ivs) && (ivs.size() == 1 || (multi_ok && ivs.size() <= kExactMaxIntervals));
+        if (exact) {
+          sax = cl[0].t[0].axis;
+          slo = ivs[0].first;
+          shi = ivs[0].second;
+        }
       }
+      if (ivs.size() < 2) ivs.clear();
       if (exact) {
         ent = {((rec_off[rank] >> 4) << 8) | (sax << 4) | kFiltNoAxis | kEntExactX, 0u, slo, shi};
         xpatch.push_back({rec_off[rank] + 5, ((1u << ce) | (sc >= 0 ? 1u << sc : 0u)) << (3 * cb)});
@@ -1279,6 +1312,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       }
       xsets.push_back(std::move(xs));
       xi_rank.push_back(uint32_t(rank));
+      xivs.push_back(exact ? std::move(ivs) : std::vector<std::pair<uint32_t, uint32_t>>());
     }
     if (!ok || nsoft == 0 || X < 0) continue;
     if (!mb) merge_bands(sub, xsets);
@@ -1300,7 +1334,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       for (auto& kv : sub) {
         if (kv.first.second != 4 || kv.first.first > AX_CTDST || combo_key.first != 0xff) continue;
         std::map<uint32_t, std::vector<uint32_t>> hosts;  // rule (xi) -> its host values in this band
-        std::map<uint32_t, std::array<uint32_t, 4>> tmpl;  // rule (xi) -> its combination entry
+        std::map<uint32_t, std::vector<std::array<uint32_t, 4>>> tmpl;  // rule (xi) -> its combination entries
         std::map<uint32_t, uint32_t> skips;                // rule (xi) -> clauses its entry decides
         bool elig = true;
         uint64_t old_n = 0;
@@ -1308,13 +1342,14 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
           elig = elig && e.key.lo == e.key.hi && rec_off[xi_rank[e.xi]] < (1u << 27);
           if (!elig) break;
           hosts[e.xi].push_back(e.key.lo);
-          old_n += xsets[e.xi].size();
+          old_n += xsets[e.xi].size() * std::max<size_t>(1, xivs[e.xi].size());
           if (tmpl.count(e.xi)) continue;
           // the entry decides the value clause (y) and the band clause (combination id); the rule's
           // third clause, if any, must be on a port axis: its hull is the entry's interval, decided
           // when it is one interval, else verified from the record
           const RuleB& r = *rs[xi_rank[e.xi]];
           uint32_t sax = kFiltNoAxis, slo = 0, shi = 0, skip = (1u << ce) | (1u << cb);
+          std::vector<std::pair<uint32_t, uint32_t>> ivs{{0u, 0u}};
           if (r.n == 3) {
             const int sc = 3 - cb - ce;
             const auto& cl = r.clause[sc];
@@ -1322,12 +1357,20 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
             elig = (a0 == AX_L4D || a0 == AX_L4S) && clause_hull(cl, a0, &slo, &shi) && shi <= 0xffffffu;
             if (!elig) break;
             sax = a0;
-            if (clause_is_interval(cl, a0, slo, shi)) skip |= 1u << sc;
+            std::vector<std::pair<uint32_t, uint32_t>> exact_ivs;
+            if (clause_intervals(cl, a0, &exact_ivs) && exact_ivs.size() <= (multi_ok ? kExactMaxIntervals : 1u)) {
+              skip |= 1u << sc;  // decided by the entry: one entry per interval
+              ivs = exact_ivs;
+            } else {
+              ivs = {{slo, shi}};  // the hull, verified from the record
+            }
           } else if (r.n != 2) {
             elig = false;
             break;
           }
-          tmpl[e.xi] = {((rec_off[xi_rank[e.xi]] >> 4) << 8) | (sax << 4) | kFiltCombo | kEntExactX, 0u, slo, shi};
+          for (auto& iv : ivs)
+            tmpl[e.xi].push_back({((rec_off[xi_rank[e.xi]] >> 4) << 8) | (sax << 4) | kFiltCombo | kEntExactX, 0u,
+                                  iv.first, iv.second});
           skips[e.xi] = skip;
         }
         if (!elig || old_n < kComboMinEntries) continue;
@@ -1354,26 +1397,28 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
         uint64_t new_n = 0;
         for (auto& c : combos)
           for (uint32_t sid : c.first)
-            for (uint32_t xi : set_rules[sid]) new_n += xsets[xi].size();
+            for (uint32_t xi : set_rules[sid]) new_n += xsets[xi].size() * tmpl[xi].size();
         if (new_n * 2 > old_n) continue;  // not worth a dependent membership load
         std::vector<std::pair<uint64_t, std::array<uint32_t, 4>>> ents;
         ents.reserve(new_n);
         for (auto& c : combos)
           for (uint32_t sid : c.first)
             for (uint32_t xi : set_rules[sid])
-              for (uint32_t x : xsets[xi]) {
-                std::array<uint32_t, 4> en = tmpl[xi];
-                en[1] = x;
-                en[2] = (en[2] & 0xffffffu) | ((c.second & 0xffu) << 24);
-                en[3] = (en[3] & 0xffffffu) | (((c.second >> 8) & 0xffu) << 24);
-                ents.push_back({(uint64_t(c.second) << 32) | x, en});
-              }
+              for (uint32_t x : xsets[xi])
+                for (const auto& t0 : tmpl[xi]) {
+                  std::array<uint32_t, 4> en = t0;
+                  en[1] = x;
+                  en[2] = (en[2] & 0xffffffu) | ((c.second & 0xffu) << 24);
+                  en[3] = (en[3] & 0xffffffu) | (((c.second >> 8) & 0xffu) << 24);
+                  ents.push_back({(uint64_t(c.second) << 32) | x, en});
+                }
         // rules whose every band-clause entry is in this band: the combination decides the clause
         std::map<uint32_t, size_t> n_all, n_here;
         for (auto& kv2 : sub)
           for (auto& e : kv2.second) (kv2.first == kv.first ? n_here : n_all)[e.xi]++;
         for (auto& h : tmpl)
           if (!n_all.count(h.first)) combo_rules[rec_off[xi_rank[h.first]] + 5] = skips[h.first] << (3 * cb);
+        (void)n_here;
         if (std::getenv("GPC_IMAGE_DEBUG"))
           std::fprintf(stderr, "table %d composite axis %u: %zu host sets, %zu combinations over %zu hosts: %llu -> %llu entries\n",
                        t, kv.first.first, set_ids.size(), combos.size(), members.size(), (unsigned long long)old_n,
@@ -1383,11 +1428,12 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
         combo_members.swap(members);
       }
     }
+    auto n_ent = [&](uint32_t xi) -> uint64_t { return std::max<size_t>(1, xivs[xi].size()); };
     uint64_t total = 0;
     for (auto& kv : sub)
       if (kv.first == combo_key) total += combo_ents.size();
       else
-        for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size();
+        for (auto& e : kv.second) total += atom_span(e.key) * xsets[e.xi].size() * n_ent(e.xi);
     if (total > composite_max_entries()) continue;
     std::vector<std::pair<uint32_t, std::array<uint32_t, 4>>> be;
     // 2^extra buckets per entry: fewer hash collisions per probe. Round 4 (offset pairs, C3 / C2):
@@ -1408,7 +1454,7 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
       uint64_t n = 0;
       if (combo) n = combo_ents.size();
       else
-        for (auto& e : kv.second) n += atom_span(e.key) * xsets[e.xi].size();
+        for (auto& e : kv.second) n += atom_span(e.key) * xsets[e.xi].size() * n_ent(e.xi);
       uint32_t bits = 10;
       while (bits < 24 && (1ull << bits) < n) bits++;
       bits = std::min(26u, bits + extra);
@@ -1424,7 +1470,16 @@ void build_composite(const std::vector<RuleB*>& rs, const std::vector<uint32_t>&
               std::array<uint32_t, 4> en = e.ent;
               if (en[0] & kEntExactX) en[1] = x;
               else out->hdr.bloom_axes |= bloom_axis_bit(en[0]) | kBloomL4;
-              be.push_back({cbucket_of(band, bits, uint32_t(k << sh), x), en});
+              const uint32_t bk = cbucket_of(band, bits, uint32_t(k << sh), x);
+              if (xivs[e.xi].size() > 1) {  // one exact entry per interval of the third clause
+                for (auto& iv : xivs[e.xi]) {
+                  en[2] = iv.first;
+                  en[3] = iv.second;
+                  be.push_back({bk, en});
+                }
+              } else {
+                be.push_back({bk, en});
+              }
             }
       }
       std::sort(be.begin(), be.end());

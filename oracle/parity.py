@@ -267,8 +267,13 @@ class OracleWorker:
 
     def churn(self, ops) -> dict:
         """Replay an op log (replay_churn) in the worker; later checks classify against the result."""
+        import sys
+        import time
         self._ready()
         self.conn.send(("churn", ops))
+        t0 = time.time()
+        while not self.conn.poll(20):  # a progress line while the oracle replays (a long log takes minutes)
+            print("[oracle] replaying %d ops (%.0f s)" % (len(ops), time.time() - t0), file=sys.stderr, flush=True)
         return self.conn.recv()
 
     def baseline(self, seconds: float, chunk: int = 4096) -> dict:
