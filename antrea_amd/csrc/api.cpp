@@ -1894,10 +1894,13 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     tail_bytes = (jn.pool.size() - jn.uploaded) * 4;
     copy_bytes = std::min(std::max(tail_bytes, kMinUploadBytes), kPoolWords * 4 - jn.uploaded * 4);
     if (ctx->stage_bytes < copy_bytes) {
+      // grown geometrically: hipHostFree waits for the device to drain, so a staging buffer
+      // reallocated for every slightly larger tail stalled commits behind the classification queue
+      // (C5 mixed: 260-340 ms per commit with 6-7 MB tails)
       if (ctx->stage) (void)hipHostFree(ctx->stage);
       ctx->stage = nullptr;
       ctx->stage_bytes = 0;
-      const size_t cap = std::max(copy_bytes, size_t(4) << 20);
+      const size_t cap = std::max(2 * copy_bytes, size_t(16) << 20);
       if (hip_ok(hipHostMalloc(&ctx->stage, cap, hipHostMallocPortable))) return fail(-GPC_EDEV);
       ctx->stage_bytes = cap;
     }
@@ -1925,7 +1928,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
       if (ctx->stage6) (void)hipHostFree(ctx->stage6);
       ctx->stage6 = nullptr;
       ctx->stage6_bytes = 0;
-      const size_t cap = std::max(copy6_bytes, size_t(4) << 20);
+      const size_t cap = std::max(2 * copy6_bytes, size_t(16) << 20);
       if (hip_ok(hipHostMalloc(&ctx->stage6, cap, hipHostMallocPortable))) return fail(-GPC_EDEV);
       ctx->stage6_bytes = cap;
     }

@@ -99,7 +99,7 @@ class _ChurnOps:
            ("reinstall", 0.0008), ("reassign", 0.0010))
     # (the del_base / readd_base share is scaled by `base_frac` / 0.19: --churn-base-frac)
 
-    def __init__(self, clf, wl, seed, mix="mixed", cands=None, base_frac=0.04, weights=None):
+    def __init__(self, clf, wl, seed, mix="mixed", cands=None, base_frac=0.005, weights=None):
         import numpy as np
         self.clf = clf
         self.rng = np.random.default_rng(seed)
@@ -826,8 +826,9 @@ def main(argv=None):
                     help="C5 op stream: mixed = adds of peers the batch sends + base-peer deletes / re-adds + "
                          "uninstall / reinstall + priority reassignment (_ChurnOps.MIX); uniform = round 5's "
                          "random /32 source adds / deletes")
-    ap.add_argument("--churn-base-frac", type=float, default=0.04,
-                    help="C5 mixed: share of ops that delete / re-add a rule's own ipBlock peers (journaled)")
+    ap.add_argument("--churn-base-frac", type=float, default=0.005,
+                    help="C5 mixed: share of ops that delete / re-add a rule's own ipBlock peers (policy edits: "
+                         "journaled; 0.005 = 50 / s at 10 000 ops / s)")
     ap.add_argument("--commit-interval-ms", type=float, default=10.0,
                     help="C5: at most one gpc_commit per this many ms (ops due meanwhile share it)")
     ap.add_argument("--group", type=int, default=0,
