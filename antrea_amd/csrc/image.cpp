@@ -2693,7 +2693,14 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
         bloom_axes_ |= bloom_axis_bit(pf[0]) | kBloomL4;
         for (auto& a : r.clause[k]) {
           AtomKey key;
-          const bool keyed = (!bt.n_cidx || xok) && atom_key(a, &key) && journal_keys(key, &keys);
+          bool keyed = (!bt.n_cidx || xok) && atom_key(a, &key);
+          // a composite base that merged its IP bands (build_composite merge_bands: C3 / C4 key
+          // every prefix at band 0) keys the journal the same way: one chain per (band key, value)
+          // for the packet to walk instead of one per band
+          if (keyed && bt.n_cidx && key.axis <= AX_CTDST && !std::getenv("GPC_JOURNAL_NO_MERGE"))
+            for (uint32_t i = 0; i < bt.n_cidx && i < uint32_t(kIdxPerClause); i++)
+              if (bt.cidx[i].axis == key.axis && bt.cidx[i].band < key.band) key.band = bt.cidx[i].band;
+          keyed = keyed && journal_keys(key, &keys);
           if (!keyed) {
             const uint32_t e[kJEntWords] = {jt.always[k], 0u, (orid << kJOridShift), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
             const uint32_t eo = append(e, kJEntWords, kJEntWords);
