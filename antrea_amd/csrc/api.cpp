@@ -185,6 +185,10 @@ struct Compactor {
   std::vector<std::shared_ptr<DevImage>> dbase, dpool;  // per device slot (empty: not uploaded)
   size_t uploaded = 0;
   uint64_t at_commit = 0;
+  // point extensions live at the requested commit: the new base leaves them out and the fresh
+  // journal lists them as extensions again. Folding them into the base (round 5) made every later
+  // delete of such a value a journaled rule (C5 mixed: 4-6 k journal rules, 25-70 ms per step).
+  HeldExts hold;
 };
 
 struct gpc_ctx {
@@ -525,6 +529,7 @@ static void compactor_main(gpc_ctx* ctx) {
     return n;
   };
   std::vector<Op> ops;
+  HeldExts hold;
   while (grab(&ops, true)) {
     replay(ops);
     uint64_t want;
@@ -534,6 +539,8 @@ static void compactor_main(gpc_ctx* ctx) {
       if (want && at_marker && shadow_commit >= want) {
         C.want_commit = 0;
         C.busy = true;
+        hold.swap(C.hold);
+        C.hold.clear();
       } else {
         continue;
       }
@@ -550,7 +557,7 @@ static void compactor_main(gpc_ctx* ctx) {
     int rc = GPC_OK;
     try {
       (void)shadow.take_dirty();
-      rc = build_image(shadow, ctx->slots, base.get(), /*alloc=*/false);
+      rc = build_image(shadow, ctx->slots, base.get(), /*alloc=*/false, hold.empty() ? nullptr : &hold);
       t_build = ms_since(t0);
       jn->reset(base.get());
       for (int round = 0; rc == GPC_OK && round < 4; round++) {
@@ -568,6 +575,8 @@ static void compactor_main(gpc_ctx* ctx) {
           rc = -GPC_EINVAL;
           break;
         }
+        if (round == 0)  // the held extensions become extensions of the new base
+          for (auto& h : hold) d.conj.insert(h.first);
         std::string err;
         if ((!d.conj.empty() || d.hard_tables) && jn->apply(shadow, ctx->slots, d.conj, d.hard_tables, &err, false) != GPC_OK)
           rc = -GPC_EINVAL;
@@ -1768,13 +1777,17 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   const size_t soft = ca > 0 ? size_t(ca) : std::max<size_t>(2048, ctx->last.conj_rid.size() / 32);
   // (or once many point extensions are live, or the pool is a quarter full: epochs that only move
   // extensions append an index each, and the compactor folds them into a new base)
+  // Live point extensions are held across the compaction (Compactor::hold) unless they are many
+  // (kExtCompactValues), so they do not ask for one; their per-epoch index does, through the pool.
+  const bool hold_ext = !std::getenv("GPC_COMPACT_FOLD_EXT") && ctx->journal.n_ext_values() <= kExtCompactValues;
   if (!full && ca >= 0 && !ctx->comp_pending &&
-      (ctx->journal.n_live + ctx->journal.n_ext_rules() > soft || ctx->journal.n_ext_values() > kExtCompactValues ||
-       ctx->journal.pool.size() > kPoolWords / 4)) {
+      (ctx->journal.n_live + (hold_ext ? 0u : ctx->journal.n_ext_rules()) > soft ||
+       ctx->journal.n_ext_values() > kExtCompactValues || ctx->journal.pool.size() > kPoolWords / 4)) {
     {
       std::lock_guard<std::mutex> c(ctx->comp.mu);
       if (ctx->comp.enabled && !ctx->comp.busy && !ctx->comp.ready) {
         ctx->comp.want_commit = commit_no;
+        ctx->comp.hold = hold_ext ? ctx->journal.held_extensions() : HeldExts();
         ctx->comp_pending = true;
         ctx->dirty_hist.clear();
       }

@@ -1734,7 +1734,7 @@ int emit(Gather& G, const FeatureNP& np, SlotMap& slots, HostImage* out, bool al
 
 }  // namespace
 
-int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc) {
+int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc, const HeldExts* hold) {
   *out = HostImage();
   Gather G;
   for (auto& kv : np.installed()) {
@@ -1744,7 +1744,36 @@ int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc)
       return rc;
     }
   }
+  // Held point extensions: the base gets the rule without those exact values (never an emptied
+  // clause: such a rule keeps all its atoms, and Journal::apply then journals it as it would any).
+  if (hold)
+    for (auto& h : *hold) {
+      RuleB* r = nullptr;
+      for (int t = 1; t <= 6 && !r; t++) {
+        auto it = G.soft[t].find(h.first);
+        if (it != G.soft[t].end()) r = &it->second;
+      }
+      if (!r || h.second.clause >= uint32_t(r->n)) continue;
+      std::vector<Atom>& cl = r->clause[h.second.clause];
+      auto held = [&](const Atom& a) {
+        return a.t.size() == 1 && a.t[0].mask == 0xffffffffu &&
+               std::binary_search(h.second.values.begin(), h.second.values.end(),
+                                  std::make_pair(uint32_t(a.t[0].axis), a.t[0].val));
+      };
+      const size_t keep = size_t(std::count_if(cl.begin(), cl.end(), [&](const Atom& a) { return !held(a); }));
+      if (keep && keep < cl.size()) cl.erase(std::remove_if(cl.begin(), cl.end(), held), cl.end());
+    }
   return emit(G, np, slots, out, alloc);
+}
+
+HeldExts Journal::held_extensions() const {
+  HeldExts h;
+  for (auto& kv : ext_) {
+    HeldExt& e = h[kv.first];
+    e.clause = kv.second.clause;
+    e.values = kv.second.values;
+  }
+  return h;
 }
 
 // A 2-choice hash of V6Lpm slots (core.hpp v6_codes) at most `load` full: 2^lg buckets of

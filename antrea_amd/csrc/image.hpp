@@ -76,7 +76,14 @@ class SlotMap {
 };
 
 // alloc = false (background compactor): counter slots are looked up, never allocated.
-int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true);
+// Point extensions a compaction keeps as extensions (api.cpp compactor): per conj, the clause and
+// the (axis, value) atoms the new base leaves out (the fresh journal re-adds them as extensions).
+struct HeldExt {
+  uint32_t clause = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> values;  // (axis, value), sorted
+};
+using HeldExts = std::map<uint32_t, HeldExt>;
+int build_image(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true, const HeldExts* hold = nullptr);
 // The IPv6 image (core.hpp "IPv6 interning"): full build.
 int build_image6(const FeatureNP& np, SlotMap& slots, HostImage* out, bool alloc = true);
 class Journal;
@@ -109,6 +116,7 @@ class Journal {
   // What the current epoch needs of the kernel (core.hpp kModeBase / kModeExt / kModeJournal).
   int mode() const { return journaled_ ? kModeJournal : ext_off_ ? kModeExt : kModeBase; }
   uint32_t n_ext_rules() const { return uint32_t(ext_.size()); }
+  HeldExts held_extensions() const;  // the live point extensions, for a compaction that keeps them
   uint32_t n_ext_values() const { return ext_values_; }
   uint32_t n_tombstones() const;
   std::vector<uint32_t> pool;  // host mirror of the device pool

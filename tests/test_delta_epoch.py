@@ -187,6 +187,7 @@ def test_compaction_uninstall_releases_slot(monkeypatch):
     'identical on every rank' promise the RCCL all-reduce relies on)."""
     import time
     monkeypatch.setenv("GPC_TEST_COMPACT_DELAY_MS", "400")
+    monkeypatch.setenv("GPC_COMPACT_FOLD_EXT", "1")  # point extensions count toward compaction (not held)
     wl = workload.config3(seed=26, n_policies_per_dir=8, rules_per_policy=20)
     rules = copy.deepcopy(wl.rules)
     cols = workload.gen_packets(wl, N_PKTS, seed=26)
@@ -216,3 +217,58 @@ def test_compaction_uninstall_releases_slot(monkeypatch):
     _, slots_b = b.counters()
     assert victim not in slots_a and victim not in a.network_policy_metrics()
     assert slots_a == slots_b
+
+
+def test_compaction_holds_point_extensions(monkeypatch):
+    """A compaction started while point extensions are live keeps them as extensions: the new base
+    leaves their values out and the fresh journal re-adds them (api.cpp Compactor::hold). Deleting
+    such a value after the handover stays an extension update instead of a journaled rule (the
+    C5-mixed failure of round 5: thousands of journal rules after each compaction)."""
+    import time
+    monkeypatch.setenv("GPC_TEST_COMPACT_DELAY_MS", "0")
+    wl = workload.config3(seed=27, n_policies_per_dir=8, rules_per_policy=20)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=27)
+    rng = np.random.default_rng(27)
+    a, b = gpc.Classifier(compact_after=4), gpc.Classifier(compact_after=-1)
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    by_id = {r["flow_id"]: r for r in rules if r.get("from") and len(r["from"]) > 2}
+    ids = sorted(by_id)
+    ext_ids, del_ids = ids[:6], ids[6:12]
+    added = {}
+    for rid in ext_ids:
+        addrs = [_ip(int(cols["src"][i])) for i in rng.choice(N_PKTS, size=3, replace=False)]
+        addrs = [x for x in dict.fromkeys(addrs) if x not in by_id[rid]["from"]]
+        for c in (a, b):
+            c.add_policy_rule_address(rid, "src", addrs, by_id[rid].get("priority"))
+        added[rid] = addrs
+        _compare(a, b, cols, "add %d" % rid)
+    st = a.image_stats()
+    assert st["n_ext_rules"] == len(ext_ids) and st["n_overlay_rules"] == 0, st
+    for rid in del_ids:  # base-value deletes: journaled rules, past compact_after -> compaction
+        r = by_id[rid]
+        for c in (a, b):
+            c.delete_policy_rule_address(rid, "src", [r["from"][0]], r.get("priority"))
+        del r["from"][0]
+        _compare(a, b, cols, "del %d" % rid)
+    for _ in range(50):
+        time.sleep(0.1)
+        _compare(a, b, cols, "handover")
+        if a.image_stats()["n_background_builds"] >= 1:
+            break
+    st = a.image_stats()
+    # (the deletes committed after the compactor's snapshot stay journaled)
+    live = st["n_overlay_rules"]
+    assert st["n_background_builds"] >= 1 and live < len(del_ids) - 4, st
+    assert st["n_ext_rules"] == len(ext_ids), st  # held, not folded into the base
+    # one added value deleted: still an extension; all of them: back at the base version
+    r0, r1 = ext_ids[0], ext_ids[1]
+    for c in (a, b):
+        c.delete_policy_rule_address(r0, "src", added[r0][:1], by_id[r0].get("priority"))
+        c.delete_policy_rule_address(r1, "src", added[r1], by_id[r1].get("priority"))
+    _compare(a, b, cols, "delete added values")
+    st = a.image_stats()
+    assert st["n_overlay_rules"] == live and st["n_ext_rules"] == len(ext_ids) - 1, st
