@@ -1840,6 +1840,7 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
 #endif
       e = ew[0];
       if (!always && (ew[1] != key || (ew[2] & kJMetaMask) != meta)) continue;
+      GPC_STAT(15, 1u);  // (emulation: journal entries of the packet's keys)
       if (rule_dead(im, ew[2] >> kJOridShift)) continue;
       Ent f;
       f.x = ew[4];
@@ -1887,18 +1888,40 @@ GPC_HD TablePart eval_journal(const View& v, uint32_t table, const Pkt& p) {
 // its other clauses from the base record (the extended clause is decided by the probe). The index
 // is small (live added values) and emitted whole per epoch: a presence bitmap (one L2-resident
 // load settles almost every packet), bucket offsets, 16-B entries {value, table | axis << 3 |
-// clause << 7, record offset, priority}.
+// clause << 7 | composite << 9, record offset, priority}.
+// Composite keys: in a table with a composite base index (TableHdr n_cidx), a value added to the
+// band clause cband is keyed by (value, x) for every exact value x of the rule's clause 1 - cband
+// (on axis cx), like the base's composite driver. Without that, a Pod IP added to many rules (C5
+// mixed: ~70 rules per local Pod IP) made every packet from that Pod verify all of them (the
+// extension probe went from 0 to 13 ms per 64 M-packet launch as the adds accumulated). The
+// probe's hash then includes the packet's cx value; the record check still verifies clause
+// 1 - cband, so a hash collision costs a verification, never a wrong verdict.
+// Two levels (image.cpp emit_ext): the bulk level B, appended when rebuilt and shared by the
+// epochs after it, and the delta level D of the rules changed since, appended per epoch with a
+// bitmap over B's entries that tombstones the changed rules' B entries. Both levels are probed.
 struct ExtHdr {
-  uint32_t n;                   // entries
-  uint32_t pres_off, pres_log2;  // presence bitmap: 2^pres_log2 bits
-  uint32_t bkt_off, bkt_log2;    // 2^bkt_log2 + 1 bucket offsets (entry index)
-  uint32_t ent_off;              // entries, kExtEntWords words each, bucket-sorted
-  uint32_t axes[6];              // per table: bit a = some entry of the table is on axis a
+  uint32_t n;                   // D entries
+  uint32_t pres_off, pres_log2;  // presence bitmap of B and D entries: 2^pres_log2 bits
+  uint32_t bkt_off, bkt_log2;    // D: 2^bkt_log2 + 1 bucket offsets (entry index)
+  uint32_t ent_off;              // D: entries, kExtEntWords words each, bucket-sorted
+  // per table: bit a = some plain entry of the table is on axis a; bit 16 + a = a composite one
+  uint32_t axes[6];
+  uint32_t b_n, b_bkt_off, b_bkt_log2, b_ent_off;  // B (b_n 0: none)
+  uint32_t b_tomb_off;                              // bit i: B entry i is dead
 };
 constexpr uint32_t kExtEntWords = 4;
+constexpr uint32_t kExtComposite = 1u << 9;  // entry meta: keyed by (value, cx value)
 GPC_HD uint32_t ext_meta(uint32_t table, uint32_t axis, uint32_t clause) { return table | (axis << 3) | (clause << 7); }
 GPC_HD uint32_t ext_hash(uint32_t table, uint32_t axis, uint32_t v) {
   return mix32(v ^ mix32(((table << 4) | axis) * 0x9e3779b1u + 0x632be5abu));
+}
+GPC_HD uint32_t ext_hash_x(uint32_t table, uint32_t axis, uint32_t v, uint32_t x) {
+  return mix32(ext_hash(table, axis, v) ^ cx_hash(x));
+}
+// The probe hash of kind bit b (ExtHdr axes) for packet p.
+GPC_HD uint32_t ext_kind_hash(const View& v, uint32_t table, uint32_t b, const Pkt& p) {
+  const uint32_t a = b & 15u;
+  return b < 16u ? ext_hash(table, a, p.ax[a]) : ext_hash_x(table, a, p.ax[a], p.ax[v.base.hdr->t[table - 1].cx]);
 }
 
 // The presence words of a table's extended axes (at most two; more: scanned unconditionally),
@@ -1917,9 +1940,9 @@ GPC_HD ExtProbe ext_begin(const View& v, uint32_t table, const Pkt& p) {
   x.bits = 0xffffu;
   const uint32_t sh = 32u - eh->pres_log2;
   for (uint32_t i = 0; i < 2 && axes; i++) {
-    const uint32_t a = uint32_t(__builtin_ctz(axes));
+    const uint32_t b = uint32_t(__builtin_ctz(axes));
     axes &= axes - 1u;
-    const uint32_t pb = ext_hash(table, a, p.ax[a]) >> sh;
+    const uint32_t pb = ext_kind_hash(v, table, b, p) >> sh;
     GPC_TOUCH(pool + eh->pres_off + (pb >> 5), 4);
     const uint32_t w = pool[eh->pres_off + (pb >> 5)];
     if (i == 0) {
@@ -1954,29 +1977,34 @@ GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p, uint32_t 
   uint32_t axes = eh->axes[table - 1];
   uint32_t best = 0, best_prio = 0, best_conj = 0, at_best = 0;
   for (uint32_t i = 0; axes; i++) {
-    const uint32_t a = uint32_t(__builtin_ctz(axes));
+    const uint32_t b = uint32_t(__builtin_ctz(axes)), a = b & 15u;
     axes &= axes - 1u;
     if (!((hits >> i) & 1u)) continue;
-    const uint32_t val = p.ax[a], h = ext_hash(table, a, val);
+    const uint32_t val = p.ax[a], h = ext_kind_hash(v, table, b, p);
+    const uint32_t meta = table | (a << 3) | (b < 16u ? 0u : kExtComposite);
+    for (uint32_t lv = 0; lv < 2; lv++) {  // D, then B
+    if (!(lv ? eh->b_n : eh->n)) continue;
+    const uint32_t* bk = pool + (lv ? eh->b_bkt_off : eh->bkt_off) + (h & ((1u << (lv ? eh->b_bkt_log2 : eh->bkt_log2)) - 1u));
+    const uint32_t eo = lv ? eh->b_ent_off : eh->ent_off;
     uint32_t e, end;
-    GPC_TOUCH(pool + eh->bkt_off + (h & ((1u << eh->bkt_log2) - 1u)), 8);
-    load_pair(pool + eh->bkt_off + (h & ((1u << eh->bkt_log2) - 1u)), &e, &end);
-    const uint32_t meta = table | (a << 3);
+    GPC_TOUCH(bk, 8);
+    load_pair(bk, &e, &end);
     for (; e < end; e++) {
-      const uint32_t* en = pool + eh->ent_off + e * kExtEntWords;
+      const uint32_t* en = pool + eo + e * kExtEntWords;
       GPC_TOUCH(en, 16);
 #if defined(__HIPCC__)
       const uint4 q = *reinterpret_cast<const uint4*>(en);
 #else
       const struct { uint32_t x, y, z, w; } q = {en[0], en[1], en[2], en[3]};
 #endif
-      if (q.x != val || (q.y & 0x7fu) != meta) continue;
+      if (q.x != val || (q.y & (0x7fu | kExtComposite)) != meta) continue;
+      if (lv && ((pool[eh->b_tomb_off + (e >> 5)] >> (e & 31u)) & 1u)) continue;  // a changed rule's B entry
       const uint32_t prio = q.w;
       if (best && prio < best_prio) continue;  // cannot change the decision
       const uint32_t* rec = v.base.blob + q.z;
       GPC_TOUCH(rec, 4 * kRecLine);
       const uint32_t conj = rec[0];
-      if (!rule_match(v.base, rec, rec[2], rec + kRecFcd, 1u << (q.y >> 7), p)) continue;
+      if (!rule_match(v.base, rec, rec[2], rec + kRecFcd, 1u << ((q.y >> 7) & 3u), p)) continue;
       if (!best || prio > best_prio) {
         best = q.z;
         best_prio = prio;
@@ -1989,6 +2017,7 @@ GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p, uint32_t 
           best_conj = conj;
         }
       }
+    }
     }
   }
   if (best) {

@@ -2408,6 +2408,14 @@ void Journal::reset(const HostImage* base, uint32_t lg) {
   ovf_dirty_ = false;
   ext_.clear();
   ext_values_ = ext_off_ = 0;
+  ext_entries_ = 0;
+  ext_dirty_.clear();
+  extd_.clear();
+  extb_ = ExtHdr{};
+  extb_ents_.clear();
+  extb_tomb_.clear();
+  extb_pres_.clear();
+  extb_dead_ = 0;
   journaled_ = false;
   pt_off_ = bdead_pt_off_ = odead_pt_off_ = 0;
 }
@@ -2429,42 +2437,114 @@ uint32_t Journal::append(const uint32_t* w, size_t n, size_t align) {
 // Point extensions per rule (core.hpp ExtHdr): at most kExtMaxRuleValues added values per rule and
 // kExtMaxValues in all (past them a rule takes the journal; the compactor folds them into a base).
 constexpr size_t kExtMaxRuleValues = 256, kExtMaxValues = size_t(1) << 20;
+constexpr size_t kExtMaxXValues = 64, kExtPresBits = 8;  // composite keys up to this many x values per rule (else plain)
 
-// The index of every live point extension, appended to the pool (published whole per epoch: it is
-// small, and nothing published is rewritten). Returns its ExtHdr offset (0: no extensions).
+// The index of every live point extension, appended to the pool per epoch in two levels (nothing
+// published is rewritten). The bulk level B holds every extended rule's entries as of its last
+// rebuild and is appended only then; the delta level D holds the entries of the rules changed since
+// (re-appended every epoch, small), and a bitmap over B's entries tombstones those rules' B entries.
+// B is rebuilt once D passes max(kExtDeltaMin, B / kExtDeltaFrac) entries or half of B is dead.
+// Per epoch: the presence bitmap of B and D (one bitmap: a packet still settles with one load),
+// D, the tombstones and the header. C5 mixed (80 k entries with composite keys): ~0.3 MB per commit
+// instead of 1.3 MB re-emitting everything. Returns the ExtHdr offset (0: no extensions).
+constexpr size_t kExtDeltaMin = 4096, kExtDeltaFrac = 8;
 uint32_t Journal::emit_ext() {
-  if (ext_.empty()) return 0;
-  struct E {
-    uint32_t bkt, w[kExtEntWords];
-  };
-  std::vector<E> es;
-  es.reserve(ext_values_);
-  ExtHdr h{};
-  h.n = ext_values_;
-  h.pres_log2 = 12;
-  while (h.pres_log2 < 24 && (uint64_t(1) << h.pres_log2) < uint64_t(ext_values_) * 32) h.pres_log2++;
-  h.bkt_log2 = 6;
-  while (h.bkt_log2 < 22 && (uint64_t(1) << h.bkt_log2) < uint64_t(ext_values_)) h.bkt_log2++;
-  std::vector<uint32_t> pres(size_t(1) << (h.pres_log2 - 5), 0u), offs((size_t(1) << h.bkt_log2) + 1, 0u);
-  for (auto& kv : ext_) {
-    const ExtRule& e = kv.second;
-    for (auto& av : e.values) {
-      const uint32_t hs = ext_hash(e.table, av.first, av.second);
-      const uint32_t pb = hs >> (32u - h.pres_log2);
-      pres[pb >> 5] |= 1u << (pb & 31u);
-      es.push_back({hs & ((1u << h.bkt_log2) - 1u), {av.second, ext_meta(e.table, av.first, e.clause), e.rec_off, e.prio}});
-      h.axes[e.table - 1] |= 1u << av.first;
+  for (uint32_t c : ext_dirty_) {  // the changed rules leave B (their entries go to D, if any)
+    auto it = extb_ents_.find(c);
+    if (it != extb_ents_.end()) {
+      for (uint32_t i : it->second) extb_tomb_[i >> 5] |= 1u << (i & 31u);
+      extb_dead_ += uint32_t(it->second.size());
+      extb_ents_.erase(it);
     }
+    if (ext_.count(c)) extd_.insert(c);
+    else extd_.erase(c);
   }
-  std::stable_sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.bkt < b.bkt; });
-  for (const E& e : es) offs[e.bkt + 1]++;
-  for (size_t b = 0; b + 1 < offs.size(); b++) offs[b + 1] += offs[b];
-  std::vector<uint32_t> ents;
-  ents.reserve(es.size() * kExtEntWords);
-  for (const E& e : es) ents.insert(ents.end(), e.w, e.w + kExtEntWords);
+  ext_dirty_.clear();
+  if (ext_.empty()) {
+    extb_ = ExtHdr{};
+    extb_ents_.clear();
+    extb_tomb_.clear();
+    extb_pres_.clear();
+    extd_.clear();
+    extb_dead_ = 0;
+    return 0;
+  }
+  struct E {
+    uint32_t hs, w[kExtEntWords], conj;
+  };
+  auto entries_of = [](uint32_t c, const ExtRule& e, uint32_t* axes, std::vector<E>* out) {
+    for (auto& av : e.values) {
+      const uint32_t meta = ext_meta(e.table, av.first, e.clause);
+      if (e.xv.empty()) {
+        out->push_back({ext_hash(e.table, av.first, av.second), {av.second, meta, e.rec_off, e.prio}, c});
+        axes[e.table - 1] |= 1u << av.first;
+      } else {
+        for (uint32_t x : e.xv)
+          out->push_back({ext_hash_x(e.table, av.first, av.second, x), {av.second, meta | kExtComposite, e.rec_off, e.prio}, c});
+        axes[e.table - 1] |= 1u << (16 + av.first);
+      }
+    }
+  };
+  // one level: entries bucket-sorted (half a bucket per entry); returns offsets / entries in the pool
+  auto put_level = [&](std::vector<E>& es, uint32_t* bkt_off, uint32_t* bkt_log2, uint32_t* ent_off) {
+    uint32_t lg = 6;
+    while (lg < 22 && (uint64_t(2) << lg) < uint64_t(es.size())) lg++;
+    const uint32_t mask = (1u << lg) - 1u;
+    std::stable_sort(es.begin(), es.end(), [mask](const E& a, const E& b) { return (a.hs & mask) < (b.hs & mask); });
+    std::vector<uint32_t> offs((size_t(1) << lg) + 1, 0u), ents;
+    for (const E& e : es) offs[(e.hs & mask) + 1]++;
+    for (size_t b = 0; b + 1 < offs.size(); b++) offs[b + 1] += offs[b];
+    ents.reserve(es.size() * kExtEntWords);
+    for (const E& e : es) ents.insert(ents.end(), e.w, e.w + kExtEntWords);
+    *bkt_log2 = lg;
+    *bkt_off = append(offs.data(), offs.size(), 16);
+    *ent_off = ents.empty() ? *bkt_off : append(ents.data(), ents.size(), 16);
+  };
+  size_t dn = 0;
+  for (uint32_t c : extd_) {
+    const ExtRule& e = ext_.at(c);
+    dn += e.values.size() * std::max<size_t>(1, e.xv.size());
+  }
+  const char* dmin_env = std::getenv("GPC_EXT_DELTA_MIN");  // (tests: rebuild B often)
+  const size_t dmin = dmin_env ? size_t(std::strtoul(dmin_env, nullptr, 10)) : kExtDeltaMin;
+  const bool rebase = std::getenv("GPC_EXT_ONE_LEVEL") || !extb_.b_n ||
+                      dn > std::max(dmin, size_t(extb_.b_n) / kExtDeltaFrac) || extb_dead_ * 2 > extb_.b_n;
+  if (rebase) {  // B := every extended rule; D empty
+    std::vector<E> es;
+    es.reserve(ext_entries_);
+    ExtHdr b{};
+    for (auto& kv : ext_) entries_of(kv.first, kv.second, b.axes, &es);
+    // presence sized for B and the D it may grow before the next rebuild
+    b.pres_log2 = 12;
+    const uint64_t cap = es.size() + std::max(dmin, es.size() / kExtDeltaFrac);
+    while (b.pres_log2 < 24 && (uint64_t(1) << b.pres_log2) < cap * kExtPresBits) b.pres_log2++;
+    extb_pres_.assign(size_t(1) << (b.pres_log2 - 5), 0u);
+    for (const E& e : es) {
+      const uint32_t pb = e.hs >> (32u - b.pres_log2);
+      extb_pres_[pb >> 5] |= 1u << (pb & 31u);
+    }
+    put_level(es, &b.b_bkt_off, &b.b_bkt_log2, &b.b_ent_off);
+    b.b_n = uint32_t(es.size());
+    extb_ents_.clear();
+    for (uint32_t i = 0; i < uint32_t(es.size()); i++) extb_ents_[es[i].conj].push_back(i);
+    extb_tomb_.assign((es.size() + 31) / 32 + 1, 0u);
+    extb_dead_ = 0;
+    extd_.clear();
+    extb_ = b;
+  }
+  ExtHdr h = extb_;  // B's level, presence size and axes
+  std::vector<E> ds;
+  ds.reserve(dn);
+  for (uint32_t c : extd_) entries_of(c, ext_.at(c), h.axes, &ds);
+  std::vector<uint32_t> pres = extb_pres_;
+  for (const E& e : ds) {
+    const uint32_t pb = e.hs >> (32u - h.pres_log2);
+    pres[pb >> 5] |= 1u << (pb & 31u);
+  }
+  h.n = uint32_t(ds.size());
+  if (h.n) put_level(ds, &h.bkt_off, &h.bkt_log2, &h.ent_off);
   h.pres_off = append(pres.data(), pres.size(), 16);
-  h.bkt_off = append(offs.data(), offs.size(), 16);
-  h.ent_off = ents.empty() ? h.bkt_off : append(ents.data(), ents.size(), 16);
+  h.b_tomb_off = append(extb_tomb_.data(), extb_tomb_.size(), 16);
   return append(reinterpret_cast<const uint32_t*>(&h), sizeof h / 4, 16);
 }
 
@@ -2546,16 +2626,34 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     if (kx < 0) {  // the base version again
       if (old != ext_.end()) {
         ext_values_ -= uint32_t(had);
+        ext_entries_ -= had * std::max<size_t>(1, old->second.xv.size());
         ext_.erase(old);
+        ext_dirty_.insert(c);
         ext_changed = true;
       }
       return true;
     }
     e.clause = uint32_t(kx);
+    const TableHdr& th = base_->hdr.t[e.table - 1];
+    if (th.n_cidx && uint32_t(kx) == th.cband && !std::getenv("GPC_EXT_PLAIN")) {  // composite keys
+      for (const Atom& a : r.clause[1 - th.cband]) {
+        if (a.t.size() != 1 || a.t[0].axis != th.cx || a.t[0].mask != 0xffffffffu) {
+          e.xv.clear();
+          break;
+        }
+        e.xv.push_back(a.t[0].val);
+      }
+      std::sort(e.xv.begin(), e.xv.end());
+      e.xv.erase(std::unique(e.xv.begin(), e.xv.end()), e.xv.end());
+      if (e.xv.size() > kExtMaxXValues) e.xv.clear();
+    }
     if (e.values.size() > kExtMaxRuleValues || ext_values_ - had + e.values.size() > kExtMaxValues) return false;
     if (old != ext_.end() && old->second == e) return true;
     ext_values_ = uint32_t(ext_values_ - had + e.values.size());
+    if (old != ext_.end()) ext_entries_ -= old->second.values.size() * std::max<size_t>(1, old->second.xv.size());
+    ext_entries_ += e.values.size() * std::max<size_t>(1, e.xv.size());
     ext_[c] = std::move(e);
+    ext_dirty_.insert(c);
     ext_changed = true;
     return true;
   };
@@ -2565,7 +2663,9 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     auto old = ext_.find(c);
     if (old != ext_.end()) {
       ext_values_ -= uint32_t(old->second.values.size());
+      ext_entries_ -= old->second.values.size() * std::max<size_t>(1, old->second.xv.size());
       ext_.erase(old);
+      ext_dirty_.insert(c);
       ext_changed = true;
     }
   }

@@ -143,12 +143,24 @@ class Journal {
   struct ExtRule {
     uint32_t table = 0, rec_off = 0, clause = 0, prio = 0;
     std::vector<std::pair<uint32_t, uint32_t>> values;  // (axis, value), sorted
+    // composite keys (core.hpp ExtHdr): the exact values of clause 1 - cband when the values extend
+    // clause cband of a composite table; empty: plain (table, axis, value) keys
+    std::vector<uint32_t> xv;
     bool operator==(const ExtRule& o) const {
-      return table == o.table && rec_off == o.rec_off && clause == o.clause && prio == o.prio && values == o.values;
+      return table == o.table && rec_off == o.rec_off && clause == o.clause && prio == o.prio && values == o.values &&
+             xv == o.xv;
     }
   };
   std::map<uint32_t, ExtRule> ext_;
   uint32_t ext_values_ = 0, ext_off_ = 0;
+  size_t ext_entries_ = 0;  // index entries: a composite value has one per x
+  // two-level index (emit_ext): B's header fields (b_*, presence size, axes), its presence bits, its
+  // entries per rule, their tombstones; the rules in D; the rules changed since the last epoch
+  ExtHdr extb_{};
+  std::vector<uint32_t> extb_pres_, extb_tomb_;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> extb_ents_;
+  uint32_t extb_dead_ = 0;
+  std::set<uint32_t> extd_, ext_dirty_;
   bool journaled_ = false;  // records, tombstones or hard rules since reset (JournalHdr kJUsed)
   uint32_t pt_off_ = 0, bdead_pt_off_ = 0, odead_pt_off_ = 0;  // last published page tables (reused if unchanged)
   uint32_t emit_ext();

@@ -831,6 +831,9 @@ def main(argv=None):
                          "journaled; 0.005 = 50 / s at 10 000 ops / s)")
     ap.add_argument("--commit-interval-ms", type=float, default=10.0,
                     help="C5: at most one gpc_commit per this many ms (ops due meanwhile share it)")
+    ap.add_argument("--compact-after", type=int, default=0,
+                    help="gpc_config.compact_after: live journal rules that start a background compaction "
+                         "(0 = the library default, max(2048, base rules / 32))")
     ap.add_argument("--group", type=int, default=0,
                     help="gpc_config.group_packets: 0 = auto (batches >= 2^18 against images >= 4 MB), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),
@@ -906,7 +909,7 @@ def main(argv=None):
     t0 = time.time()
     wl = workload.CONFIGS["C3" if churn else args.config]()
     v6 = args.family == 6
-    clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6, group_packets=args.group)
+    clf = gpc.Classifier(device=local, ipv4=not v6, ipv6=v6, group_packets=args.group, compact_after=args.compact_after)
     dp.bind(clf, v6)
     clf.initialize()
     clf.batch_install_policy_rule_flows(workload.to_ipv6(wl, embed=args.v6_embed).rules if v6 else wl.rules)
@@ -1015,6 +1018,26 @@ def main(argv=None):
         # before the control thread stopped), and the final epoch classifies the batch once more
         _log("oracle replay of %d ops" % len(churn_ops.log))
         update["oracle_replay"] = worker.churn(churn_ops.log)
+    if churn:
+        # step times over the timed region (is the cost steady or in bursts?) and the final epoch
+        # timed alone, with the control thread stopped (epoch state vs concurrent commits)
+        import numpy as np
+        step_ms = np.array([s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)])
+        w = max(1, len(step_ms) // 16)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        for _ in range(10):
+            dp.classify(soa, n, out, count, stream)
+        ev[1].record(stream)
+        dp.sync()
+        st_end = clf.image_stats()
+        update["step_ms"] = {"p50": round(float(np.percentile(step_ms, 50)), 3),
+                             "p90": round(float(np.percentile(step_ms, 90)), 3),
+                             "max": round(float(step_ms.max()), 3),
+                             "windows": [round(float(step_ms[i:i + w].mean()), 2) for i in range(0, len(step_ms), w)],
+                             "final_epoch_alone": round(ev[0].elapsed_time(ev[1]) / 10, 3),
+                             "final_epoch_mode": {"journal_rules": st_end["n_overlay_rules"],
+                                                  "ext_rules": st_end["n_ext_rules"]}}
     if churn:  # the final epoch classifies the batch once more (parity sample, verdict shift)
         dp.classify(soa, n, out, False, stream)
         dp.sync()

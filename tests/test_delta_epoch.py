@@ -272,3 +272,45 @@ def test_compaction_holds_point_extensions(monkeypatch):
     _compare(a, b, cols, "delete added values")
     st = a.image_stats()
     assert st["n_overlay_rules"] == live and st["n_ext_rules"] == len(ext_ids) - 1, st
+
+
+@pytest.mark.parametrize("env", [{"GPC_EXT_DELTA_MIN": "3"}, {"GPC_EXT_ONE_LEVEL": "1"}, {"GPC_EXT_PLAIN": "1"}],
+                         ids=["two-level-rebuild-often", "one-level", "plain-keys"])
+def test_extension_index_variants(env, monkeypatch):
+    """The point-extension index (core.hpp ExtHdr): composite (value, AppliedTo value) keys in
+    composite tables, a bulk level rebuilt rarely plus a per-epoch delta level with tombstones over
+    the bulk entries. Address adds and deletes on C3-shaped rules, verdicts and counters equal to a
+    full rebuild after every commit, with the bulk level rebuilt every few changes, never (one
+    level: everything re-emitted per epoch) and with plain keys."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    wl = workload.config3(seed=28, n_policies_per_dir=8, rules_per_policy=20)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=28)
+    rng = np.random.default_rng(28)
+    a, b = gpc.Classifier(compact_after=-1), gpc.Classifier(compact_after=-1)
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    by_id = {r["flow_id"]: r for r in rules}
+    ids = sorted(by_id)
+    added = []
+    for step in range(40):
+        if added and step % 3 == 2:
+            rid, side, addr = added.pop(int(rng.integers(len(added))))
+            for c in (a, b):
+                c.delete_policy_rule_address(rid, side, [addr], by_id[rid].get("priority"))
+        else:
+            rid = int(rng.choice(ids))
+            side = "src" if by_id[rid]["direction"] == "In" else "dst"
+            i = int(rng.integers(N_PKTS))  # a packet's own address: the add moves verdicts
+            addr = _ip(int(cols[side][i]))
+            if any(x[0] == rid and x[2] == addr for x in added):
+                continue
+            for c in (a, b):
+                c.add_policy_rule_address(rid, side, [addr], by_id[rid].get("priority"))
+            added.append((rid, side, addr))
+        _compare(a, b, cols, "step %d" % step)
+    st = a.image_stats()
+    assert st["n_ext_rules"] > 0 and st["n_overlay_rules"] == 0, st
