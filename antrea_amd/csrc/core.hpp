@@ -1909,8 +1909,16 @@ struct ExtHdr {
   uint32_t b_n, b_bkt_off, b_bkt_log2, b_ent_off;  // B (b_n 0: none)
   uint32_t b_tomb_off;                              // bit i: B entry i is dead
 };
-constexpr uint32_t kExtEntWords = 4;
+// Entries (32 B): {value, meta, record offset, priority, x, lo, hi, conj id}. meta = table | axis
+// << 3 | clause << 7 | composite << 9 | exact << 10 | interval axis << 11. A composite entry holds
+// the cx value x it is listed under (hash collisions are rejected without the record); an exact one
+// also decides the rule's remaining clause (one interval [lo, hi] on the interval axis, or none: one
+// entry per interval, like the base's exact-value entries), so the probe completes the rule from the
+// entry alone -- no record read, no rule_match: C5 mixed packets that hit an added (Pod IP, ofport)
+// pair paid a dependent record line and a point-set probe per candidate.
+constexpr uint32_t kExtEntWords = 8;
 constexpr uint32_t kExtComposite = 1u << 9;  // entry meta: keyed by (value, cx value)
+constexpr uint32_t kExtExact = 1u << 10;     // entry meta: decides every clause (no record read)
 GPC_HD uint32_t ext_meta(uint32_t table, uint32_t axis, uint32_t clause) { return table | (axis << 3) | (clause << 7); }
 GPC_HD uint32_t ext_hash(uint32_t table, uint32_t axis, uint32_t v) {
   return mix32(v ^ mix32(((table << 4) | axis) * 0x9e3779b1u + 0x632be5abu));
@@ -1976,6 +1984,7 @@ GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p, uint32_t 
   const ExtHdr* eh = reinterpret_cast<const ExtHdr*>(pool + v.ext);
   uint32_t axes = eh->axes[table - 1];
   uint32_t best = 0, best_prio = 0, best_conj = 0, at_best = 0;
+  const uint32_t xv = p.ax[v.base.hdr->t[table - 1].cx];  // (composite entries)
   for (uint32_t i = 0; axes; i++) {
     const uint32_t b = uint32_t(__builtin_ctz(axes)), a = b & 15u;
     axes &= axes - 1u;
@@ -1991,20 +2000,28 @@ GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p, uint32_t 
     load_pair(bk, &e, &end);
     for (; e < end; e++) {
       const uint32_t* en = pool + eo + e * kExtEntWords;
-      GPC_TOUCH(en, 16);
+      GPC_TOUCH(en, 32);
 #if defined(__HIPCC__)
-      const uint4 q = *reinterpret_cast<const uint4*>(en);
+      const uint4 q = reinterpret_cast<const uint4*>(en)[0], r = reinterpret_cast<const uint4*>(en)[1];
 #else
-      const struct { uint32_t x, y, z, w; } q = {en[0], en[1], en[2], en[3]};
+      const struct { uint32_t x, y, z, w; } q = {en[0], en[1], en[2], en[3]}, r = {en[4], en[5], en[6], en[7]};
 #endif
       if (q.x != val || (q.y & (0x7fu | kExtComposite)) != meta) continue;
+      if ((q.y & kExtComposite) && r.x != xv) continue;  // another x (a bucket collision)
       if (lv && ((pool[eh->b_tomb_off + (e >> 5)] >> (e & 31u)) & 1u)) continue;  // a changed rule's B entry
       const uint32_t prio = q.w;
       if (best && prio < best_prio) continue;  // cannot change the decision
-      const uint32_t* rec = v.base.blob + q.z;
-      GPC_TOUCH(rec, 4 * kRecLine);
-      const uint32_t conj = rec[0];
-      if (!rule_match(v.base, rec, rec[2], rec + kRecFcd, 1u << ((q.y >> 7) & 3u), p)) continue;
+      const uint32_t conj = r.w;
+      if (q.y & kExtExact) {
+        const uint32_t iax = (q.y >> 11) & 15u, sv = p.ax[iax < AX_N ? iax : 0];
+        if (iax != kFiltNoAxis && (sv < r.y || sv > r.z)) continue;
+      } else {
+        const uint32_t* rec = v.base.blob + q.z;
+        GPC_TOUCH(rec, 4 * kRecLine);
+        // the extended clause is decided by the value; a composite entry's clause 1 - clause by x
+        const uint32_t k = (q.y >> 7) & 3u, skip = (1u << k) | ((q.y & kExtComposite) ? 1u << (1u - k) : 0u);
+        if (!rule_match(v.base, rec, rec[2], rec + kRecFcd, skip, p)) continue;
+      }
       if (!best || prio > best_prio) {
         best = q.z;
         best_prio = prio;

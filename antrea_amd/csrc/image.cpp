@@ -2409,6 +2409,8 @@ void Journal::reset(const HostImage* base, uint32_t lg) {
   ext_.clear();
   ext_values_ = ext_off_ = 0;
   ext_entries_ = 0;
+  touched_.clear();
+  touched_hard_ = 0;
   ext_dirty_.clear();
   extd_.clear();
   extb_ = ExtHdr{};
@@ -2418,6 +2420,23 @@ void Journal::reset(const HostImage* base, uint32_t lg) {
   extb_dead_ = 0;
   journaled_ = false;
   pt_off_ = bdead_pt_off_ = odead_pt_off_ = 0;
+}
+
+int Journal::rebuild(const FeatureNP& np, SlotMap& slots, std::string* err) {
+  Journal j;
+  j.fam_ = fam_;
+  j.reset(base_, lg_);
+  const std::set<uint32_t> conj = touched_;
+  const int rc = j.apply(np, slots, conj, touched_hard_, err);
+  if (rc) return rc;
+  *this = std::move(j);
+  return GPC_OK;
+}
+
+uint32_t Journal::n_dead_versions() const {
+  uint32_t n = 0;
+  for (uint32_t w : odead_) n += uint32_t(__builtin_popcount(w));
+  return n;
 }
 
 uint32_t Journal::n_tombstones() const {
@@ -2437,7 +2456,12 @@ uint32_t Journal::append(const uint32_t* w, size_t n, size_t align) {
 // Point extensions per rule (core.hpp ExtHdr): at most kExtMaxRuleValues added values per rule and
 // kExtMaxValues in all (past them a rule takes the journal; the compactor folds them into a base).
 constexpr size_t kExtMaxRuleValues = 256, kExtMaxValues = size_t(1) << 20;
-constexpr size_t kExtMaxXValues = 64, kExtPresBits = 8;  // composite keys up to this many x values per rule (else plain)
+constexpr size_t kExtMaxXValues = 64, kExtPresBits = 8, kExtMaxIntervals = 4;
+// index entries of one extended rule (emit_ext): per value, one per x (composite) and interval (exact)
+template <class R>
+static size_t ext_entries_of(const R& e) {
+  return e.values.size() * std::max<size_t>(1, e.xv.size()) * std::max<size_t>(1, e.ivs.size());
+}  // composite keys up to this many x values per rule (else plain)
 
 // The index of every live point extension, appended to the pool per epoch in two levels (nothing
 // published is rewritten). The bulk level B holds every extended rule's entries as of its last
@@ -2476,11 +2500,18 @@ uint32_t Journal::emit_ext() {
     for (auto& av : e.values) {
       const uint32_t meta = ext_meta(e.table, av.first, e.clause);
       if (e.xv.empty()) {
-        out->push_back({ext_hash(e.table, av.first, av.second), {av.second, meta, e.rec_off, e.prio}, c});
+        out->push_back({ext_hash(e.table, av.first, av.second), {av.second, meta, e.rec_off, e.prio, 0u, 0u, 0u, c}, c});
         axes[e.table - 1] |= 1u << av.first;
-      } else {
+      } else if (e.ivs.empty()) {  // composite, the record verifies the third clause
         for (uint32_t x : e.xv)
-          out->push_back({ext_hash_x(e.table, av.first, av.second, x), {av.second, meta | kExtComposite, e.rec_off, e.prio}, c});
+          out->push_back({ext_hash_x(e.table, av.first, av.second, x),
+                          {av.second, meta | kExtComposite, e.rec_off, e.prio, x, 0u, 0u, c}, c});
+        axes[e.table - 1] |= 1u << (16 + av.first);
+      } else {  // composite and exact: one entry per (x, interval)
+        const uint32_t m = meta | kExtComposite | kExtExact | (e.iax << 11);
+        for (uint32_t x : e.xv)
+          for (auto& iv : e.ivs)
+            out->push_back({ext_hash_x(e.table, av.first, av.second, x), {av.second, m, e.rec_off, e.prio, x, iv.first, iv.second, c}, c});
         axes[e.table - 1] |= 1u << (16 + av.first);
       }
     }
@@ -2502,8 +2533,7 @@ uint32_t Journal::emit_ext() {
   };
   size_t dn = 0;
   for (uint32_t c : extd_) {
-    const ExtRule& e = ext_.at(c);
-    dn += e.values.size() * std::max<size_t>(1, e.xv.size());
+    dn += ext_entries_of(ext_.at(c));
   }
   const char* dmin_env = std::getenv("GPC_EXT_DELTA_MIN");  // (tests: rebuild B often)
   const size_t dmin = dmin_env ? size_t(std::strtoul(dmin_env, nullptr, 10)) : kExtDeltaMin;
@@ -2558,6 +2588,8 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     *err = "IPv6 journal without a prefix tree";
     return -GPC_EINVAL;
   }
+  touched_.insert(conj.begin(), conj.end());
+  touched_hard_ |= hard_tables;
   int rc = gather_rules(np, conj, hard_tables, &G);
   if (rc) {
     *err = G.error;
@@ -2626,7 +2658,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     if (kx < 0) {  // the base version again
       if (old != ext_.end()) {
         ext_values_ -= uint32_t(had);
-        ext_entries_ -= had * std::max<size_t>(1, old->second.xv.size());
+        ext_entries_ -= ext_entries_of(old->second);
         ext_.erase(old);
         ext_dirty_.insert(c);
         ext_changed = true;
@@ -2646,12 +2678,26 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
       std::sort(e.xv.begin(), e.xv.end());
       e.xv.erase(std::unique(e.xv.begin(), e.xv.end()), e.xv.end());
       if (e.xv.size() > kExtMaxXValues) e.xv.clear();
+      // exact entries: nothing else to verify, or a third clause of at most kExtMaxIntervals
+      // intervals on one axis (one entry per interval)
+      e.conj = c;
+      if (!e.xv.empty() && r.n == 2) {
+        e.ivs = {{0u, 0u}};
+      } else if (!e.xv.empty() && r.n == 3 && !std::getenv("GPC_EXT_NO_EXACT")) {
+        const auto& cl = r.clause[2];
+        std::vector<std::pair<uint32_t, uint32_t>> ivs;
+        if (!cl.empty() && cl[0].t.size() == 1 && cl[0].t[0].axis < AX_N &&
+            clause_intervals(cl, cl[0].t[0].axis, &ivs) && ivs.size() <= kExtMaxIntervals) {
+          e.iax = cl[0].t[0].axis;
+          e.ivs = std::move(ivs);
+        }
+      }
     }
     if (e.values.size() > kExtMaxRuleValues || ext_values_ - had + e.values.size() > kExtMaxValues) return false;
     if (old != ext_.end() && old->second == e) return true;
     ext_values_ = uint32_t(ext_values_ - had + e.values.size());
-    if (old != ext_.end()) ext_entries_ -= old->second.values.size() * std::max<size_t>(1, old->second.xv.size());
-    ext_entries_ += e.values.size() * std::max<size_t>(1, e.xv.size());
+    if (old != ext_.end()) ext_entries_ -= ext_entries_of(old->second);
+    ext_entries_ += ext_entries_of(e);
     ext_[c] = std::move(e);
     ext_dirty_.insert(c);
     ext_changed = true;
@@ -2663,7 +2709,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     auto old = ext_.find(c);
     if (old != ext_.end()) {
       ext_values_ -= uint32_t(old->second.values.size());
-      ext_entries_ -= old->second.values.size() * std::max<size_t>(1, old->second.xv.size());
+      ext_entries_ -= ext_entries_of(old->second);
       ext_.erase(old);
       ext_dirty_.insert(c);
       ext_changed = true;
@@ -2825,8 +2871,10 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
           bool keyed = (!bt.n_cidx || xok) && atom_key(a, &key);
           // a composite base that merged its IP bands (build_composite merge_bands: C3 / C4 key
           // every prefix at band 0) keys the journal the same way: one chain per (band key, value)
-          // for the packet to walk instead of one per band
-          if (keyed && bt.n_cidx && key.axis <= AX_CTDST && !std::getenv("GPC_JOURNAL_NO_MERGE"))
+          // for the packet to walk instead of one per band. Single addresses (band kIpBands - 1:
+          // the Pod IPs AddPolicyRuleAddress adds) keep their own band: merged, every /32 of a Pod
+          // subnet shared one chain per value (C5 mixed: 6.9 matching entries per packet, 0.1 apart)
+          if (keyed && bt.n_cidx && key.axis <= AX_CTDST && key.band + 1u < kIpBands && !std::getenv("GPC_JOURNAL_NO_MERGE"))
             for (uint32_t i = 0; i < bt.n_cidx && i < uint32_t(kIdxPerClause); i++)
               if (bt.cidx[i].axis == key.axis && bt.cidx[i].band < key.band) key.band = bt.cidx[i].band;
           keyed = keyed && journal_keys(key, &keys);
@@ -2891,7 +2939,7 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
     return *last;
   };
   if (ext_changed) ext_off_ = emit_ext();
-  h.ext_off = ext_off_;
+  h.ext_off = std::getenv("GPC_DEBUG_HIDE_EXT") ? 0u : ext_off_;  // (timing experiments only: wrong verdicts)
   h.jflags = journaled_ ? kJUsed : 0u;
   h.bloom_axes = bloom_axes_;
   if (ovf_dirty_) {

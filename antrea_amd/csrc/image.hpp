@@ -119,6 +119,11 @@ class Journal {
   HeldExts held_extensions() const;  // the live point extensions, for a compaction that keeps them
   uint32_t n_ext_values() const { return ext_values_; }
   uint32_t n_tombstones() const;
+  uint32_t n_dead_versions() const;  // journal versions tombstoned by a later version
+  // Pool garbage collection (api.cpp): the same state over the same base in a fresh pool -- every
+  // rule this journal took since its reset applied once more (journaled rules once, extensions,
+  // tombstones) -- without the dead versions and superseded extension indexes of the old pool.
+  int rebuild(const FeatureNP& np, SlotMap& slots, std::string* err);
   std::vector<uint32_t> pool;  // host mirror of the device pool
   size_t uploaded = 0;         // words already on the device
   uint32_t hdr_off = 0;        // JournalHdr of the latest epoch (0: no journal yet)
@@ -146,9 +151,13 @@ class Journal {
     // composite keys (core.hpp ExtHdr): the exact values of clause 1 - cband when the values extend
     // clause cband of a composite table; empty: plain (table, axis, value) keys
     std::vector<uint32_t> xv;
+    // exact composite entries (core.hpp kExtExact): the rule's remaining clause as intervals on iax
+    // (iax 15: the rule has no other clause); empty: the record verifies it
+    uint32_t conj = 0, iax = 15;
+    std::vector<std::pair<uint32_t, uint32_t>> ivs;
     bool operator==(const ExtRule& o) const {
       return table == o.table && rec_off == o.rec_off && clause == o.clause && prio == o.prio && values == o.values &&
-             xv == o.xv;
+             xv == o.xv && conj == o.conj && iax == o.iax && ivs == o.ivs;
     }
   };
   std::map<uint32_t, ExtRule> ext_;
@@ -161,6 +170,8 @@ class Journal {
   std::unordered_map<uint32_t, std::vector<uint32_t>> extb_ents_;
   uint32_t extb_dead_ = 0;
   std::set<uint32_t> extd_, ext_dirty_;
+  std::set<uint32_t> touched_;  // every rule applied since the reset (rebuild)
+  uint8_t touched_hard_ = 0;
   bool journaled_ = false;  // records, tombstones or hard rules since reset (JournalHdr kJUsed)
   uint32_t pt_off_ = 0, bdead_pt_off_ = 0, odead_pt_off_ = 0;  // last published page tables (reused if unchanged)
   uint32_t emit_ext();

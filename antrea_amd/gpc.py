@@ -106,7 +106,7 @@ class gpc_image_stats(C.Structure):
                 ("n_delta_builds", C.c_uint64), ("n_background_builds", C.c_uint64), ("group_key", C.c_uint32),
                 ("lane_sort", C.c_uint32), ("v6_full_builds", C.c_uint64), ("v6_delta_builds", C.c_uint64),
                 ("v6_overlay_rules", C.c_uint32), ("v6_prefixes", C.c_uint32), ("n_ext_rules", C.c_uint32),
-                ("n_ext_values", C.c_uint32)]
+                ("n_ext_values", C.c_uint32), ("n_pool_collections", C.c_uint64)]
 
 
 class gpc_endpoint(C.Structure):
@@ -734,4 +734,5 @@ class Classifier:
                 "group_key": st.group_key, "lane_sort": [st.lane_sort & 0xff, st.lane_sort >> 8],
                 "v6_full_builds": st.v6_full_builds, "v6_delta_builds": st.v6_delta_builds,
                 "v6_overlay_rules": st.v6_overlay_rules, "v6_prefixes": st.v6_prefixes,
-                "n_ext_rules": st.n_ext_rules, "n_ext_values": st.n_ext_values}
+                "n_ext_rules": st.n_ext_rules, "n_ext_values": st.n_ext_values,
+                "n_pool_collections": st.n_pool_collections}

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GPC_ABI_VERSION 5
+#define GPC_ABI_VERSION 6
 /* device slots of one context (gpc_create_multi) */
 #define GPC_MAX_DEVICES 16
 
@@ -327,6 +327,9 @@ typedef struct gpc_image_stats { /* shape of the committed device image (for roo
    * are probed per packet instead of walking a journal copy of the rule */
   uint32_t n_ext_rules;          /* rules with point extensions                                  */
   uint32_t n_ext_values;         /* added values they hold                                       */
+  /* ABI 6: journal pool collections (the journal's state rewritten into a fresh pool, without
+   * superseded extension indexes and dead versions; no image build) */
+  uint64_t n_pool_collections;
 } gpc_image_stats;
 
 /* ---------------------------------------------------------------------------- lifecycle */

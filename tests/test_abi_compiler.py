@@ -28,7 +28,7 @@ def test_exports_every_header_symbol():
     exported = set(re.findall(r"\bT (gpc_\w+)", syms))
     assert declared <= exported, declared - exported
     lib = gpc.load()
-    assert lib.gpc_abi_version() == 5  # 5: point-extension stats (4: multi-device contexts; 3: ct_mark column, DNS trio, flow keys; 2: IPv6)
+    assert lib.gpc_abi_version() == 6  # 6: pool collections stat; 5: point-extension stats (4: multi-device contexts; 3: ct_mark column, DNS trio, flow keys; 2: IPv6)
 
 
 @pytest.mark.parametrize("case", GOLD["cases"], ids=[c["name"] for c in GOLD["cases"]])

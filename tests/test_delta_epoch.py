@@ -314,3 +314,44 @@ def test_extension_index_variants(env, monkeypatch):
         _compare(a, b, cols, "step %d" % step)
     st = a.image_stats()
     assert st["n_ext_rules"] > 0 and st["n_overlay_rules"] == 0, st
+
+
+def test_pool_collection(monkeypatch):
+    """Pool garbage collection (api.cpp, Journal::rebuild): once the pool holds many dead journal
+    versions (here: more than 4 -- GPC_GC_DEAD_MIN) the journal's state is rewritten into a fresh
+    pool without an image build. Rules re-journaled over and over (base-peer deletes and re-adds),
+    point extensions and uninstalls across several collections: verdicts and counters equal a full
+    rebuild after every commit."""
+    monkeypatch.setenv("GPC_GC_DEAD_MIN", "4")
+    wl = workload.config3(seed=29, n_policies_per_dir=8, rules_per_policy=20)
+    rules = copy.deepcopy(wl.rules)
+    cols = workload.gen_packets(wl, N_PKTS, seed=29)
+    rng = np.random.default_rng(29)
+    a, b = gpc.Classifier(compact_after=-1), gpc.Classifier(compact_after=-1)
+    for c in (a, b):
+        c.initialize()
+        c.batch_install_policy_rule_flows(copy.deepcopy(rules))
+    _compare(a, b, cols, "batch")
+    by_id = {r["flow_id"]: r for r in rules if r.get("from") and r["direction"] == "In"}
+    ids = sorted(by_id)[:3]
+    for step in range(36):
+        rid = ids[step % len(ids)]
+        r = by_id[rid]
+        if step % 3 == 0:  # a base peer out and back in: a new journal version each time
+            peer = r["from"][0]
+            for c in (a, b):
+                c.delete_policy_rule_address(rid, "src", [peer], r.get("priority"))
+            _compare(a, b, cols, "del %d" % step)
+            for c in (a, b):
+                c.add_policy_rule_address(rid, "src", [peer], r.get("priority"))
+        elif step % 3 == 1:
+            addr = _ip(int(cols["src"][int(rng.integers(N_PKTS))]))
+            for c in (a, b):
+                c.add_policy_rule_address(rid, "src", [addr], r.get("priority"))
+            r["from"].append(addr)
+        elif step == 35:
+            for c in (a, b):
+                c.uninstall_policy_rule_flows(rid)
+        _compare(a, b, cols, "step %d" % step)
+    st = a.image_stats()
+    assert st["n_pool_collections"] >= 2 and st["n_full_builds"] == 1, st
