@@ -1771,9 +1771,16 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
          ctx->journal.n_dead_versions() > std::max<size_t>(env_u32("GPC_GC_DEAD_MIN", kGcDeadMin, 1, 1u << 30),
                                                            2 * size_t(ctx->journal.n_live)))) {
       std::string err;
+      const size_t was = ctx->journal.pool.size();
+      const clk::time_point tg = clk::now();
       if (ctx->journal.rebuild(ctx->np, ctx->slots, &err) == GPC_OK) {
         pool_gc = true;
         ctx->n_pool_gc++;
+        if (std::getenv("GPC_COMPACT_DEBUG"))
+          std::fprintf(stderr, "commit %llu: pool collection %.1f -> %.1f MB in %.1f ms (%zu live rules, %u extended)\n",
+                       (unsigned long long)commit_no, was * 4e-6, ctx->journal.pool.size() * 4e-6,
+                       std::chrono::duration<double, std::milli>(clk::now() - tg).count(), ctx->journal.n_live,
+                       ctx->journal.n_ext_rules());
       } else {
         full = true;
       }
@@ -1796,7 +1803,9 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   }
   // ask the compactor for a new base once the journal is large; commits continue meanwhile
   const int32_t ca = ctx->cfg.compact_after;
-  const size_t soft = ca > 0 ? size_t(ca) : std::max<size_t>(2048, ctx->last.conj_rid.size() / 32);
+  // (default: max(512, base rules / 128) -- C3: 781; every live journal rule adds to the walk of the
+  // packets its keys reach, and the pool collections keep everything else small)
+  const size_t soft = ca > 0 ? size_t(ca) : std::max<size_t>(512, ctx->last.conj_rid.size() / 128);
   // (or once many point extensions are live, or the pool is a quarter full: epochs that only move
   // extensions append an index each, and the compactor folds them into a new base)
   // Live point extensions are held across the compaction (Compactor::hold) unless they are many

@@ -833,7 +833,7 @@ def main(argv=None):
                     help="C5: at most one gpc_commit per this many ms (ops due meanwhile share it)")
     ap.add_argument("--compact-after", type=int, default=0,
                     help="gpc_config.compact_after: live journal rules that start a background compaction "
-                         "(0 = the library default, max(2048, base rules / 32))")
+                         "(0 = the library default, max(512, base rules / 128))")
     ap.add_argument("--group", type=int, default=0,
                     help="gpc_config.group_packets: 0 = auto (batches >= 2^18 against images >= 4 MB), 1 = on, -1 = off")
     ap.add_argument("--family", type=int, default=4, choices=(4, 6),

@@ -127,7 +127,7 @@ typedef struct gpc_config {
   uint64_t cookie;               /* cookie printed in flow dumps (round<<48 | category<<40)     */
   int32_t device;                /* HIP device ordinal used by this context                    */
   int32_t compact_after;         /* live journal rules that start a background compaction
-                                    (0: max(2048, rules / 32); < 0: never in the background)   */
+                                    (0: max(512, rules / 128); < 0: never in the background)  */
   int32_t ovs_meters;            /* OVS meters supported: packet-in flows carry meter:256/258    */
   int32_t external_node;         /* config.ExternalNode: no IngressSecurityClassifier flows      */
   int32_t group_packets;         /* gpc_classify groups a batch by nw_src before the table walk:
