@@ -963,6 +963,14 @@ def main(argv=None):
             time.sleep(0.01)
         lat.clear()
     _log("timed region: %d steps of %d packets" % (args.steps, n))
+    # The harness's own heap (the workload's 100 k rule dicts, C5's op log growing by 10 k dicts a
+    # second) makes CPython's cyclic collector pause every thread for up to ~0.6 s while it holds
+    # the GIL: the launch loop stalled (C5 step max 564 ms, op p99 680 ms). Nothing of the library
+    # is collected; the harness freezes its heap and collects again after the timed region.
+    import gc
+    gc.collect()
+    gc.freeze()
+    gc.disable()
     # HIP events around each kernel of the timed calls (gpc_launch_times; the library keeps at most
     # 4096 calls: a longer run, e.g. C5 over 30 s, is timed per kernel over its first 4096 steps)
     dp.set_launch_timing(min(args.steps, 4096))
@@ -979,6 +987,7 @@ def main(argv=None):
         dist.barrier()
     dp.sync()
     elapsed = time.perf_counter() - t_start
+    gc.enable()
     update = None
     if churn:
         stop.set()
