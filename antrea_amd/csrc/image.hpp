@@ -120,9 +120,9 @@ class Journal {
   uint32_t n_ext_values() const { return ext_values_; }
   uint32_t n_tombstones() const;
   uint32_t n_dead_versions() const;  // journal versions tombstoned by a later version
-  // Pool garbage collection (api.cpp): the same state over the same base in a fresh pool -- every
-  // rule this journal took since its reset applied once more (journaled rules once, extensions,
-  // tombstones) -- without the dead versions and superseded extension indexes of the old pool.
+  // Pool garbage collection (api.cpp): the same state over the same base in a fresh pool -- the
+  // live journaled rules written once more, extensions and base tombstones carried over -- without
+  // the dead versions and superseded extension indexes of the old pool (IPv4 journal only).
   int rebuild(const FeatureNP& np, SlotMap& slots, std::string* err);
   std::vector<uint32_t> pool;  // host mirror of the device pool
   size_t uploaded = 0;         // words already on the device
@@ -172,6 +172,7 @@ class Journal {
   std::set<uint32_t> extd_, ext_dirty_;
   std::set<uint32_t> touched_;  // every rule applied since the reset (rebuild)
   uint8_t touched_hard_ = 0;
+  bool ext_force_ = false;  // rebuild: emit the carried-over extension index with the next epoch
   bool journaled_ = false;  // records, tombstones or hard rules since reset (JournalHdr kJUsed)
   uint32_t pt_off_ = 0, bdead_pt_off_ = 0, odead_pt_off_ = 0;  // last published page tables (reused if unchanged)
   uint32_t emit_ext();
