@@ -919,6 +919,15 @@ int gpc_uninstall_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family) {
   if (!ip) return -GPC_EINVAL;
   GPC_SVC_CALL(ctx->svc.uninstall_pod(ip, family));
 }
+int gpc_set_node_port_addresses(gpc_ctx* ctx, const uint8_t* ips, uint8_t family, size_t n) {
+  if ((!ips && n) || family != 4 || n > kSvcMaxNodePortAddrs - 1) return -GPC_EINVAL;
+  std::vector<uint32_t> v4(n);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* b = ips + 16 * i;
+    v4[i] = (uint32_t(b[0]) << 24) | (uint32_t(b[1]) << 16) | (uint32_t(b[2]) << 8) | b[3];
+  }
+  GPC_SVC_CALL(ctx->svc.set_node_port_addresses(v4.data(), n));
+}
 
 int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   if (!ctx) return -GPC_EINVAL;

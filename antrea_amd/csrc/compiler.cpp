@@ -28,7 +28,8 @@ static const char* kTableNames[TB_COUNT] = {"",
                                             "EndpointDNAT",
                                             "SNATMark",
                                             "SNAT",
-                                            "IngressSecurityClassifier"};
+                                            "IngressSecurityClassifier",
+                                            "NodePortMark"};
 
 const char* table_name(uint8_t t) { return t < TB_COUNT ? kTableNames[t] : "?"; }
 

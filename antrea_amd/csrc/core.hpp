@@ -2109,7 +2109,12 @@ struct SvcHdr {
   uint32_t hash_off, hash_log2, svc_off, n_svc, ep_off, n_ep;
   uint32_t map_off, map_log2;  // 2^map_log2-bit map of the keys (svc_map_bit): most packets that
                                // address no Service are settled by one load
+  // NodePort addresses (the NodePortMark flows' nw_dst, pipeline.go:2282-2314; 0 when no NodePort
+  // Service exists): a packet to one of them that misses the (protocol, address, port) key takes
+  // the NodePort key (protocol, 0, port) -- ServiceLB's ToNodePortAddressRegMark flows
+  uint32_t np_off, n_np;
 };
+constexpr uint32_t kSvcMaxNodePortAddrs = 64;
 // Service hash: 2-choice cuckoo, buckets of two 16-B slots {key low, key high, service index, 0}:
 // a lookup is one 128-bit load per slot (four per packet), not a 96-B scan of an 8-way bucket.
 constexpr uint32_t kSvcBucketWords = 8, kSvcSlots = 2, kSvcSlotWords = 4;
@@ -2164,9 +2169,14 @@ GPC_HD uint32_t lb_stage(const uint32_t* sv, uint32_t src, uint32_t& dst, uint32
                          uint32_t& svc_group, uint32_t& out_port, uint32_t& dest, uint32_t* o) {
   o[0] = o[1] = o[2] = o[3] = 0;
   if (proto != 6 && proto != 17 && proto != 132) return 0;
-  const uint32_t si = svc_lookup(sv, proto, dst, dport);
-  if (si == 0xffffffffu) return 0;
   const SvcHdr* h = reinterpret_cast<const SvcHdr*>(sv);
+  uint32_t si = svc_lookup(sv, proto, dst, dport);
+  if (si == 0xffffffffu && h->n_np) {  // NodePortMark, then the NodePort ServiceLB flows
+    bool np = false;
+    for (uint32_t i = 0; i < h->n_np; i++) np |= sv[h->np_off + i] == dst;
+    if (np) si = svc_lookup(sv, proto, 0u, dport);
+  }
+  if (si == 0xffffffffu) return 0;
   const uint32_t* s = sv + h->svc_off + 4 * si;
   GPC_TOUCH(s, 16);
   const uint32_t n = s[1] & 0xffffffu, lg = s[1] >> 24;

@@ -37,7 +37,8 @@ enum TableId : uint8_t {
   TB_SNAT_MARK = 14,
   TB_SNAT = 15,
   TB_INGRESS_CLASSIFIER = 16,  // IngressSecurityClassifier (pipeline.go:2144-2182)
-  TB_COUNT = 17
+  TB_NODEPORT_MARK = 17,       // NodePortMark (pipeline.go:2280-2314, proxyAll)
+  TB_COUNT = 18
 };
 const char* table_name(uint8_t t);
 // Logging-and-resubmit group IDs as initGroups allocates them (network_policy.go:2271-2300, Multicast

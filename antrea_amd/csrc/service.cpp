@@ -18,7 +18,9 @@ constexpr uint32_t kSvcNoEp = 1u << 14;            // reg0[14]  SvcNoEpRegMark
 constexpr uint32_t kEpStateMask = 0x7u << 16;      // reg4[16..18] ServiceEPStateField
 constexpr uint32_t kEpToSelect = 0x1u << 16;
 constexpr uint32_t kEpSelected = 0x2u << 16;
+constexpr uint32_t kToNodePort = 1u << 19;         // reg4[19]  ToNodePortAddressRegMark
 constexpr uint32_t kToExternal = 1u << 21;         // reg4[21]  ToExternalAddressRegMark
+constexpr uint32_t kVirtualNodePortDNAT = 0xa9fe00fcu;  // config.VirtualNodePortDNATIPv4 169.254.0.252
 constexpr uint32_t kRemoteEndpoint = 1u << 26;     // reg4[26]  RemoteEndpointRegMark
 constexpr uint32_t kEpUnionMask = 0x7ffffu;        // reg4[0..18] EpUnionField
 
@@ -188,8 +190,8 @@ static std::string service_key(const IPAddr& ip, uint16_t port, uint8_t proto) {
 // InstallServiceFlows (client.go:790-807) -> serviceLBFlows (pipeline.go:2373-2431).
 int FeatureService::install_service_flows(const gpc_service_config& c) {
   if (!ip_proto(c.protocol) || c.family != 4) return -GPC_EINVAL;
-  if (c.affinity_timeout || c.is_nodeport || c.is_dsr || c.is_nested || (c.is_external && c.traffic_policy_local))
-    return -GPC_EINVAL;  // learn / NodePort / DSR / multi-cluster / short-circuit flows: not modelled
+  if (c.affinity_timeout || c.is_dsr || c.is_nested || (c.is_external && c.traffic_policy_local))
+    return -GPC_EINVAL;  // learn / DSR / multi-cluster / short-circuit flows: not modelled
   const IPAddr ip = to_ip(c.ip, 4);
   const uint32_t gid = c.traffic_policy_local ? c.local_group_id : c.cluster_group_id;  // TrafficPolicyGroupID
   Flow f;
@@ -201,8 +203,12 @@ int FeatureService::install_service_flows(const gpc_service_config& c) {
   f.m.tp_dst = c.port;
   f.m.tp_dst_m = 0xffff;
   match_reg(f.m, 4, kEpToSelect, kEpStateMask);
-  f.m.nw_dst.set = true;
-  f.m.nw_dst.addr = ip;
+  if (c.is_nodeport) {  // ToNodePortAddressRegMark instead of the Service IP (pipeline.go:2381-2387)
+    match_reg(f.m, 4, kToNodePort, kToNodePort);
+  } else {
+    f.m.nw_dst.set = true;
+    f.m.nw_dst.addr = ip;
+  }
   f.acts.push_back(set_reg(0, kRewriteMac, kRewriteMac));
   f.acts.push_back(set_reg(4, kEpSelected, kEpStateMask));
   if (c.is_external) f.acts.push_back(set_reg(4, kToExternal, kToExternal));
@@ -225,6 +231,31 @@ int FeatureService::uninstall_service_flows(const uint8_t* ip, uint8_t family, u
 int FeatureService::install_pod(const uint8_t* ip, uint8_t family, uint32_t ofport) {
   if (family != 4) return -GPC_EINVAL;
   pods_[to_ip(ip, 4).v4()] = ofport;
+  generation_++;
+  return GPC_OK;
+}
+
+int FeatureService::set_node_port_addresses(const uint32_t* v4, size_t n) {
+  for (auto it = cached_.begin(); it != cached_.end();)
+    it = it->first.compare(0, 2, "NP") == 0 ? cached_.erase(it) : std::next(it);
+  std::vector<uint32_t> addrs;
+  for (size_t i = 0; i < n; i++)
+    if ((v4[i] >> 24) != 127u) addrs.push_back(v4[i]);  // loopback: not NodePort traffic from a Pod
+  if (n) addrs.push_back(kVirtualNodePortDNAT);  // the gateway's DNATed NodePort connections
+  for (uint32_t a : addrs) {
+    Flow f;
+    f.table = TB_NODEPORT_MARK;
+    f.priority = kPriorityNormal;
+    f.cookie = cookie();
+    set_proto(f.m, 0, 4);
+    f.m.nw_dst.set = true;
+    f.m.nw_dst.addr.fam = 4;
+    for (int k = 0; k < 4; k++) f.m.nw_dst.addr.b[k] = uint8_t(a >> (24 - 8 * k));
+    f.acts.push_back(set_reg(4, kToNodePort, kToNodePort));
+    char key[24];
+    std::snprintf(key, sizeof key, "NP%08x", a);
+    cached_[key] = {f};
+  }
   generation_++;
   return GPC_OK;
 }
@@ -310,9 +341,17 @@ int FeatureService::build_image(std::vector<uint32_t>* blob, std::string* err) c
     bool reg7;
   };
   std::vector<Svc> svcs;
+  std::vector<uint32_t> node_port_addrs;
+  bool any_node_port = false;
   for (auto& kv : cached_)
     for (auto& f : kv.second) {
-      if (f.table == TB_ENDPOINT_DNAT) {
+      if (f.table == TB_NODEPORT_MARK) {
+        if (!f.m.nw_dst.set || f.m.nw_dst.plen >= 0) {
+          *err = "unsupported NodePortMark flow: " + f.str();
+          return -GPC_EINVAL;
+        }
+        node_port_addrs.push_back(f.m.nw_dst.addr.v4());
+      } else if (f.table == TB_ENDPOINT_DNAT) {
         if (!(f.m.reg_present & (1u << 3)) || !(f.m.reg_present & (1u << 4)) || f.acts.empty() ||
             f.acts[0].kind != ACT_CT_DNAT) {
           *err = "unsupported EndpointDNAT flow: " + f.str();
@@ -320,13 +359,17 @@ int FeatureService::build_image(std::vector<uint32_t>* blob, std::string* err) c
         }
         dnat[{f.m.nw_proto, f.m.reg_v[3], uint16_t(f.m.reg_v[4] & 0xffffu)}] = true;
       } else if (f.table == TB_SERVICE_LB) {
-        Svc s{svc_key(f.m.nw_proto, f.m.nw_dst.addr.v4(), f.m.tp_dst), 0, false};
+        // a NodePort Service (ToNodePortAddressRegMark, no Service IP) is keyed by address 0
+        const bool node_port = (f.m.reg_present & (1u << 4)) && (f.m.reg_m[4] & kToNodePort) && (f.m.reg_v[4] & kToNodePort);
+        any_node_port |= node_port;
+        Svc s{svc_key(f.m.nw_proto, node_port ? 0u : f.m.nw_dst.addr.v4(), f.m.tp_dst), 0, false};
         bool grp = false;
         for (auto& a : f.acts) {
           if (a.kind == ACT_GROUP) s.gid = a.a, grp = true;
           if (a.kind == ACT_SET_REG && a.a == 7) s.reg7 = true;
         }
-        if (!grp || !f.m.nw_dst.set || f.m.nw_dst.plen >= 0 || !f.m.has_tp_dst || f.m.tp_dst_m != 0xffff) {
+        if (!grp || node_port == f.m.nw_dst.set || (f.m.nw_dst.set && f.m.nw_dst.plen >= 0) || !f.m.has_tp_dst ||
+            f.m.tp_dst_m != 0xffff) {
           *err = "unsupported ServiceLB flow: " + f.str();
           return -GPC_EINVAL;
         }
@@ -393,7 +436,16 @@ int FeatureService::build_image(std::vector<uint32_t>* blob, std::string* err) c
   hdr.n_svc = uint32_t(svc_words.size() / 4);
   hdr.ep_off = hdr.svc_off + uint32_t(svc_words.size());
   hdr.n_ep = uint32_t(ep_words.size() / 4);
-  blob->assign(hdr.ep_off + ep_words.size(), 0u);
+  // NodePort addresses: probed only when some ServiceLB flow is a NodePort one
+  if (!any_node_port) node_port_addrs.clear();
+  if (node_port_addrs.size() > kSvcMaxNodePortAddrs) {
+    *err = "too many NodePort addresses";
+    return -GPC_EINVAL;
+  }
+  hdr.np_off = hdr.ep_off + uint32_t(ep_words.size());
+  hdr.n_np = uint32_t(node_port_addrs.size());
+  blob->assign(hdr.np_off + node_port_addrs.size(), 0u);
+  std::copy(node_port_addrs.begin(), node_port_addrs.end(), blob->begin() + hdr.np_off);
   std::memcpy(blob->data(), &hdr, sizeof hdr);
   for (auto& e : kv) {
     const uint32_t mb = svc_map_bit(e.first, hdr.map_log2);

@@ -23,6 +23,9 @@ class FeatureService {
   int install_service_flows(const gpc_service_config& c);
   int uninstall_service_flows(const uint8_t* ip, uint8_t family, uint16_t port, uint8_t proto);
   int install_pod(const uint8_t* ip, uint8_t family, uint32_t ofport);
+  // NodePort addresses (NewClient's nodePortAddressesIPv4 with proxyAll): the NodePortMark flows
+  // (pipeline.go:2282-2314) for each non-loopback address and the virtual NodePort DNAT IP
+  int set_node_port_addresses(const uint32_t* v4, size_t n);
   int uninstall_pod(const uint8_t* ip, uint8_t family);
 
   std::string dump_flows() const;   // FlowModToString lines of the realized Service flows

@@ -128,7 +128,7 @@ EXPORTS = ["gpc_create", "gpc_destroy", "gpc_initialize", "gpc_install_rule", "g
            "gpc_install_service_group", "gpc_uninstall_service_group", "gpc_install_endpoint_flows",
            "gpc_uninstall_endpoint_flows", "gpc_install_service_flows", "gpc_uninstall_service_flows", "gpc_install_pod",
            "gpc_uninstall_pod", "gpc_dump_groups", "gpc_classify_lb", "gpc_classify_host_lb", "gpc_debug_service_image",
-           "gpc_abi_version", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
+           "gpc_abi_version", "gpc_set_node_port_addresses", "gpc_classify6", "gpc_classify6_host", "gpc_debug_image6", "gpc_new_dns_conjunction",
            "gpc_add_dns_conj_addrs", "gpc_del_dns_conj_addrs", "gpc_network_policy_flow_keys", "gpc_stream_epoch", "gpc_trace", "gpc_replay",
            "gpc_set_launch_timing", "gpc_launch_times", "gpc_create_multi", "gpc_n_devices", "gpc_classify_on",
            "gpc_classify6_on", "gpc_classify_host_on", "gpc_counters_on", "gpc_debug_epoch6", "gpc_debug_fail_uploads"]
@@ -185,6 +185,7 @@ def load(path: str = LIB_PATH):
     lib.gpc_install_service_flows.argtypes = [vp, C.POINTER(gpc_service_config)]
     lib.gpc_uninstall_service_flows.argtypes = [vp, u8p, C.c_uint8, C.c_uint16, C.c_uint8]
     lib.gpc_install_pod.argtypes = [vp, u8p, C.c_uint8, C.c_uint32]
+    lib.gpc_set_node_port_addresses.argtypes = [vp, u8p, C.c_uint8, sz]
     lib.gpc_uninstall_pod.argtypes = [vp, u8p, C.c_uint8]
     lib.gpc_dump_groups.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]
     lib.gpc_classify_lb.argtypes = [vp, C.POINTER(gpc_pkt_soa), sz, vp, vp, i32, vp]
@@ -579,6 +580,17 @@ class Classifier:
     def uninstall_pod(self, ip):
         fam, b = _ip_bytes(ip)
         _check(self.lib.gpc_uninstall_pod(self.h, b, fam), "UninstallPodFlows")
+
+    def set_node_port_addresses(self, ips):
+        """NewClient's nodePortAddressesIPv4 with proxyAll (pipeline.go:2282-2314 nodePortMarkFlows);
+        [] turns NodePort marking off."""
+        buf = (C.c_uint8 * (16 * max(1, len(ips))))()
+        for i, ip in enumerate(ips):
+            fam, b = _ip_bytes(ip)
+            if fam != 4:
+                raise GpcError(-GPC_EINVAL, "NodePort addresses: IPv4 only")
+            C.memmove(C.byref(buf, 16 * i), b, 4)
+        _check(self.lib.gpc_set_node_port_addresses(self.h, buf, 4, len(ips)), "gpc_set_node_port_addresses")
 
     def dump_groups(self) -> List[str]:
         need = C.c_size_t()

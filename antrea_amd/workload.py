@@ -243,12 +243,19 @@ def config3(seed=RULE_SEED, n_policies_per_dir=500, rules_per_policy=100) -> Wor
 SVC_PROTOS = (("TCP", 6), ("UDP", 17), ("SCTP", 132))
 
 
+NODE_PORT_ADDRESSES = ("192.168.77.100", "192.168.77.101")  # the Node's NodePort addresses (nodeport_frac > 0)
+VIRTUAL_NODE_PORT_DNAT = "169.254.0.252"                    # config.VirtualNodePortDNATIPv4
+
+
 def add_services(wl: Workload, n_services: int, eps_per_service: int, seed=RULE_SEED + 4, remote_frac=0.7,
-                 noep_frac=0.02, local_policy_frac=0.1, svc_frac=0.5) -> Workload:
+                 noep_frac=0.02, local_policy_frac=0.1, svc_frac=0.5, nodeport_frac=0.0) -> Workload:
     """ClusterIP Services (10.96.0.0/12) with `eps_per_service` Endpoints each: local Endpoints are
     the workload's local Pods (ofports known to the Pod map), remote ones are Pods on other Nodes
     (10.128.0.0/9). A fraction of Services has no Endpoints, a fraction Local traffic policy.
-    `svc_frac` of the generated packets are aimed at a Service (ip, port, protocol)."""
+    `svc_frac` of the generated packets are aimed at a Service (ip, port, protocol).
+    `nodeport_frac` > 0: that fraction are NodePort Services (installed with the virtual NodePort
+    DNAT IP, as the proxier does, on ports 30000-32767 unique per protocol); their packets go to one
+    of NODE_PORT_ADDRESSES or the virtual IP; wl.node_port_addresses is set."""
     rng = np.random.default_rng(seed)
     base = int(ipaddress.ip_address("10.96.0.0"))
     ips = base + 1 + rng.choice(1 << 20, size=n_services, replace=False)
@@ -276,6 +283,23 @@ def add_services(wl: Workload, n_services: int, eps_per_service: int, seed=RULE_
             wl.endpoint_flows.append((proto, eps))
         wl.services.append({"ip": _ip(ips[i]), "port": int(ports[i]), "protocol": proto, "cluster_group_id": cgid,
                             "local_group_id": lgid, "traffic_policy_local": bool(local)})
+    if nodeport_frac > 0:  # (drawn after the ClusterIP set: other workloads keep their streams)
+        nrng = np.random.default_rng(seed + 17)
+        addrs = [int(ipaddress.ip_address(a)) for a in NODE_PORT_ADDRESSES + (VIRTUAL_NODE_PORT_DNAT,)]
+        taken = set()
+        for i in np.nonzero(nrng.random(n_services) < nodeport_frac)[0]:
+            s = wl.services[i]
+            while True:
+                port = int(nrng.integers(30000, 32768))
+                if (s["protocol"], port) not in taken:
+                    break
+            taken.add((s["protocol"], port))
+            if s["traffic_policy_local"] and s["local_group_id"] in wl.groups:  # (external + Local: not modelled)
+                wl.groups[s["cluster_group_id"]] = wl.groups.pop(s["local_group_id"])
+            s.update(ip=VIRTUAL_NODE_PORT_DNAT, port=port, is_nodeport=True, is_external=True, traffic_policy_local=False)
+            ips[i] = addrs[int(nrng.integers(len(addrs)))]  # the packets' destination
+            ports[i] = port
+        wl.node_port_addresses = list(NODE_PORT_ADDRESSES)
     wl.svc_meta = {"ip": ips.astype(np.uint32), "port": ports.astype(np.uint16),
                    "proto": np.array([SVC_PROTOS[k][1] for k in pk], np.uint8)}
     wl.svc_frac = svc_frac
@@ -287,6 +311,8 @@ def install_services(clf, wl: Workload):
     Service flows) plus the Pod map."""
     for ip, port in wl.pods.items():
         clf.install_pod(_ip(ip), port)
+    if getattr(wl, "node_port_addresses", None):
+        clf.set_node_port_addresses(wl.node_port_addresses)
     for gid, eps in wl.groups.items():
         clf.install_service_group(gid, eps)
     for proto, eps in wl.endpoint_flows:

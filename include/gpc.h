@@ -402,8 +402,11 @@ int gpc_install_endpoint_flows(gpc_ctx* ctx, uint8_t protocol, uint8_t family, c
 /* UninstallEndpointFlows(protocol, endpoints) error                         client.go:772 */
 int gpc_uninstall_endpoint_flows(gpc_ctx* ctx, uint8_t protocol, uint8_t family, const gpc_endpoint* eps, size_t n);
 /* InstallServiceFlows(*types.ServiceConfig) error                           client.go:790
- * Supported: ClusterIP / LoadBalancer / ExternalIP Services (optionally Local traffic policy)
- * without session affinity, NodePort, DSR or multi-cluster nesting; other configs -GPC_EINVAL. */
+ * Supported: ClusterIP / LoadBalancer / ExternalIP / NodePort Services (optionally Local traffic
+ * policy) without session affinity, DSR, multi-cluster nesting or the external + Local
+ * short-circuit; other configs -GPC_EINVAL. A NodePort Service (is_nodeport; the caller passes the
+ * virtual NodePort DNAT IP 169.254.0.252 as its ip, as the proxier does) matches packets to the
+ * NodePort addresses (gpc_set_node_port_addresses) by protocol and port (pipeline.go:2381-2387). */
 int gpc_install_service_flows(gpc_ctx* ctx, const gpc_service_config* cfg);
 /* UninstallServiceFlows(svcIP, svcPort, protocol) error                     client.go:809 */
 int gpc_uninstall_service_flows(gpc_ctx* ctx, const uint8_t* ip, uint8_t family, uint16_t port, uint8_t protocol);
@@ -411,6 +414,12 @@ int gpc_uninstall_service_flows(gpc_ctx* ctx, const uint8_t* ip, uint8_t family,
  * (reg1 TargetOFPortField) for traffic DNATed to a local Endpoint. */
 int gpc_install_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family, uint32_t ofport);
 int gpc_uninstall_pod(gpc_ctx* ctx, const uint8_t* ip, uint8_t family);
+/* NodePort addresses of the Node (NewClient nodePortAddressesIPv4 with proxyAll; ABI 6): one
+ * NodePortMark flow per non-loopback address plus the virtual NodePort DNAT IP 169.254.0.252
+ * (pipeline.go:2282-2314), loading ToNodePortAddressRegMark (reg4[19]) for the ServiceLB NodePort
+ * flows. `ips`: n IPv4 addresses of 16 bytes each (the address in the first 4); family 4 only;
+ * n = 0 removes them (proxyAll off). Replaces the previous set. */
+int gpc_set_node_port_addresses(gpc_ctx* ctx, const uint8_t* ips, uint8_t family, size_t n);
 /* ovs-ofctl dump-groups style text of the realized groups, '\n' separated. */
 int gpc_dump_groups(gpc_ctx* ctx, char* buf, size_t cap, size_t* needed);
 

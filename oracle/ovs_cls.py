@@ -190,6 +190,14 @@ class Pipeline:
         if pkt["proto"] not in (6, 17, 132) or not self.tables.get("ServiceLB"):
             return pkt, 0, None
         st = {"regs": {4: EP_TO_SELECT}, "ct_label": 0, "conj_id": 0}
+        # PreRoutingClassifier resubmits to NodePortMark first when proxyAll installed it
+        # (pipeline.go:3014-3034): ToNodePortAddressRegMark for the NodePort addresses (:2282-2314)
+        m, _ = classifier_lookup(self.tables.get("NodePortMark", []), pkt, st, allow_conj=False)
+        for a in (m["actions"] if m is not None else []):
+            if a[0] == "set_reg":
+                _, r, v, msk = a
+                msk = 0xFFFFFFFF if msk is None else msk
+                st["regs"][r] = (st["regs"].get(r, 0) & ~msk) | (v & msk)
         f, _ = classifier_lookup(self.tables["ServiceLB"], pkt, st, allow_conj=False)
         if f is None:
             return pkt, 0, None

@@ -18,9 +18,13 @@ reference's dump format (`pkg/ovs/openflow/utils.go` FlowModToString, as the gol
   EpToSelectRegMark + Service IP / protocol / port, loading RewriteMACRegMark, EpSelectedRegMark and
   (AntreaPolicy on) ServiceGroupIDField = the group it selects, then `group:`.
 
+* `nodePortMarkFlows` (`pipeline.go:2282-2314`, proxyAll): ToNodePortAddressRegMark (reg4[19]) for
+  packets to a NodePort address or the virtual NodePort DNAT IP; a NodePort Service's ServiceLB
+  flow matches that mark and the port instead of the Service IP (`:2381-2387`).
+
 Only the shapes the product's data path takes are restated (IPv4; no session affinity learn flow,
-NodePort, DSR, nested Services, nor the short-circuit flow of external Local Services): the others
-are rejected by both sides. Pinned by the
+DSR, nested Services, nor the short-circuit flow of external Local Services): the others are
+rejected by both sides. Pinned by the
 Service goldens of `client_test.go` (tests/golden/service_flows.json, tests/test_service.py).
 """
 from __future__ import annotations
@@ -40,6 +44,8 @@ REWRITE_MAC = (0x200, 0x200)           # RewriteMACRegMark: reg0[9]
 SVC_NO_EP = (0x4000, 0x4000)           # SvcNoEpRegMark: reg0[14]
 REMOTE_EP = (0x4000000, 0x4000000)     # RemoteEndpointRegMark: reg4[26]
 TO_EXTERNAL = (0x200000, 0x200000)     # ToExternalAddressRegMark: reg4[21]
+TO_NODE_PORT = (0x80000, 0x80000)      # ToNodePortAddressRegMark: reg4[19]
+VIRTUAL_NODE_PORT_DNAT = "169.254.0.252"  # config.VirtualNodePortDNATIPv4
 
 
 def _ipv4(ip: str) -> int:
@@ -118,8 +124,21 @@ class FeatureService:
             self.cached_flows.pop(self._endpoint_key(ep, protocol), None)
 
     # --- Service flows (client.go:790-814)
+    # --- NodePortMark (pipeline.go:2282-2314, proxyAll): one flow per non-loopback NodePort address
+    # and one for the virtual NodePort DNAT IP
+    def set_node_port_addresses(self, ips):
+        for k in [k for k in self.cached_flows if k.startswith("NP")]:
+            del self.cached_flows[k]
+        addrs = [ip for ip in ips if not ipaddress.ip_address(ip).is_loopback]
+        if ips:
+            addrs.append(VIRTUAL_NODE_PORT_DNAT)
+        for ip in addrs:
+            self.cached_flows["NP%08x" % _ipv4(ip)] = [
+                "cookie=0x%x, table=NodePortMark, priority=%d,ip,nw_dst=%s actions=set_field:0x%x/0x%x->reg4" % (
+                    self.cookie, PRIORITY_NORMAL, ip, TO_NODE_PORT[0], TO_NODE_PORT[1])]
+
     def install_service_flows(self, cfg: dict):
-        for k in ("affinity_timeout", "is_nodeport", "is_dsr", "is_nested"):
+        for k in ("affinity_timeout", "is_dsr", "is_nested"):
             if cfg.get(k):
                 raise ValueError("Service shape %s is not restated (the product rejects it too)" % k)
         if cfg.get("is_external") and cfg.get("traffic_policy_local"):  # the short-circuit flow (:2417-2422)
@@ -132,9 +151,12 @@ class FeatureService:
         if self.enable_antrea_policy:
             acts.append("set_field:0x%x->reg7" % gid)
         acts.append("group:%d" % gid)
-        flow = ("cookie=0x%x, table=ServiceLB, priority=%d,%s,reg4=0x%x/0x%x,nw_dst=%s,tp_dst=%d actions=%s" % (
-            self.cookie, PRIORITY_NORMAL, PROTOCOLS[proto], EP_TO_SELECT[0], EP_TO_SELECT[1], cfg["ip"],
-            int(cfg["port"]), ",".join(acts)))
+        if cfg.get("is_nodeport"):  # ToNodePortAddressRegMark instead of the Service IP (pipeline.go:2381-2387)
+            match = "reg4=0x%x/0x%x" % (EP_TO_SELECT[0] | TO_NODE_PORT[0], EP_TO_SELECT[1] | TO_NODE_PORT[1])
+        else:
+            match = "reg4=0x%x/0x%x,nw_dst=%s" % (EP_TO_SELECT[0], EP_TO_SELECT[1], cfg["ip"])
+        flow = ("cookie=0x%x, table=ServiceLB, priority=%d,%s,%s,tp_dst=%d actions=%s" % (
+            self.cookie, PRIORITY_NORMAL, PROTOCOLS[proto], match, int(cfg["port"]), ",".join(acts)))
         _ipv4(cfg["ip"])
         self.cached_flows["S%s%s%x" % (cfg["ip"], PROTOCOLS[proto], int(cfg["port"]))] = [flow]
 
@@ -152,6 +174,8 @@ class FeatureService:
 def install_services(svc: FeatureService, wl):
     """The AntreaProxy calls for wl's Services, in the order antrea_amd.workload.install_services
     makes them (client.go:710-815: groups, Endpoint flows, Service flows)."""
+    if getattr(wl, "node_port_addresses", None):
+        svc.set_node_port_addresses(wl.node_port_addresses)
     for gid, eps in wl.groups.items():
         svc.install_service_group(gid, eps)
     for proto, eps in wl.endpoint_flows:

@@ -186,16 +186,16 @@ def test_gpu_delta_epochs(name, group):
 
 
 @pytest.mark.parametrize("group", [-1, 1], ids=["plain", "grouped"])
-@pytest.mark.parametrize("name", ["C1", "C4"])
+@pytest.mark.parametrize("name", ["C1", "C1np", "C4"])
 def test_gpu_service_stage(name, group):
     """AntreaProxy stage on the device: verdicts and per-packet LB results equal the oracle (small:
-    C1 + 60 Services against the Python oracle; full: C4 = C3 + 10k Services x 10 Endpoints against
-    the C oracle's fixture, 100k packets), with and without the packet grouping pre-pass (LB results
-    are scattered back to caller order)."""
+    C1 + 60 Services against the Python oracle, C1np with 40 % of them NodePort Services; full: C4 =
+    C3 + 10k Services x 10 Endpoints against the C oracle's fixture, 100k packets), with and without
+    the packet grouping pre-pass (LB results are scattered back to caller order)."""
     from tests.test_service import _oracle, _svc_workload
     from tests.golden import make_parity_fixtures as fx
-    if name == "C1":
-        wl = _svc_workload("C1", 61)
+    if name.startswith("C1"):
+        wl = _svc_workload(name, 61)
         n = 3000
         cols = workload.gen_packets(wl, n, seed=61)
     else:  # the full-scale C4 fixture: the C oracle's AntreaProxy stage over every packet
@@ -210,7 +210,7 @@ def test_gpu_service_stage(name, group):
     c.commit()
     got, lb = c.classify_host(cols, lb=True)
     assert ((lb["flags"] & gpc.LB_HIT) != 0).mean() > 0.3
-    if name == "C1":
+    if name.startswith("C1"):
         o, olb = _oracle(wl, c, cols, n)
         _cmp(got, o, cols)
         assert (lb == olb).all()

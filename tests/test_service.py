@@ -50,8 +50,7 @@ def test_service_flows_golden(case):
     assert c.dump_flows() == []
 
 
-@pytest.mark.parametrize("extra", [{"affinity_timeout": 100}, {"is_nodeport": True, "is_external": True},
-                                   {"is_dsr": True, "is_external": True}, {"is_nested": True},
+@pytest.mark.parametrize("extra", [{"affinity_timeout": 100}, {"is_dsr": True, "is_external": True}, {"is_nested": True},
                                    {"is_external": True, "traffic_policy_local": True}])
 def test_unsupported_service_configs_fail_loudly(extra):
     c = gpc.Classifier()
@@ -61,9 +60,12 @@ def test_unsupported_service_configs_fail_loudly(extra):
 
 
 def _svc_workload(name, seed):
-    wl = workload.config1(seed=seed) if name == "C1" else workload.config3(seed=seed, n_policies_per_dir=6,
-                                                                              rules_per_policy=8)
-    return workload.add_services(wl, 60, 4, seed=seed, noep_frac=0.1, local_policy_frac=0.2)
+    """C1 / C3s + 60 Services; "C1np": 40 % of them NodePort Services (packets to the Node's NodePort
+    addresses and the virtual NodePort DNAT IP)."""
+    wl = workload.config1(seed=seed) if name.startswith("C1") else workload.config3(seed=seed, n_policies_per_dir=6,
+                                                                                       rules_per_policy=8)
+    return workload.add_services(wl, 60, 4, seed=seed, noep_frac=0.1, local_policy_frac=0.2,
+                                 nodeport_frac=0.4 if name.endswith("np") else 0.0)
 
 
 def _oracle(wl, clf, cols, n):
@@ -72,7 +74,8 @@ def _oracle(wl, clf, cols, n):
     fnp = oc.FeatureNetworkPolicy()
     fnp.initialize()
     fnp.batch_install_policy_rule_flows(copy.deepcopy(wl.rules))
-    svc_flows = [f for f in clf.dump_flows() if "table=ServiceLB" in f or "table=EndpointDNAT" in f]
+    svc_flows = [f for f in clf.dump_flows() if any(t in f for t in ("table=ServiceLB", "table=EndpointDNAT",
+                                                                  "table=NodePortMark"))]
     tiers = {r["flow_id"]: int(r.get("tier_priority") or 0) for r in wl.rules}
     pipe = ovs_cls.Pipeline(fnp.dump_flows() + svc_flows, tiers, clf.dump_groups(), wl.pods)
     out = np.zeros((n, 2), dtype=gpc.VERDICT_DTYPE)
@@ -97,7 +100,7 @@ def _product(wl):
     return c
 
 
-@pytest.mark.parametrize("name,seed", [("C1", 51), ("C3s", 52)])
+@pytest.mark.parametrize("name,seed", [("C1", 51), ("C3s", 52), ("C1np", 54)])
 def test_service_stage_vs_oracle(name, seed):
     wl = _svc_workload(name, seed)
     n = 2500
@@ -112,6 +115,10 @@ def test_service_stage_vs_oracle(name, seed):
     hits = (lb["flags"] & gpc.LB_HIT) != 0
     assert hits.mean() > 0.3 and (lb["flags"] & gpc.LB_NO_ENDPOINT).any() and (lb["flags"] & gpc.LB_DNAT).any()
     assert (got[:, 0]["table"] == gpc.VTABLE_ENDPOINT_DNAT).any()
+    if name.endswith("np"):  # NodePort Services reached through the Node's addresses and the virtual IP
+        import ipaddress
+        for a in workload.NODE_PORT_ADDRESSES + (workload.VIRTUAL_NODE_PORT_DNAT,):
+            assert (hits & (cols["dst"] == int(ipaddress.ip_address(a)))).sum() > 5, a
     # the policy stage saw the Endpoint: reg7 rules aside, DNATed packets carry the Endpoint address
     assert (lb["endpoint_ip"][hits & ((lb["flags"] & gpc.LB_NO_ENDPOINT) == 0)] != 0).all()
 
@@ -183,15 +190,14 @@ def test_oracle_service_flows_golden(case):
     assert s.dump_flows() == []
 
 
-@pytest.mark.parametrize("extra", [{"affinity_timeout": 100}, {"is_nodeport": True, "is_external": True},
-                                   {"is_dsr": True, "is_external": True}, {"is_nested": True},
+@pytest.mark.parametrize("extra", [{"affinity_timeout": 100}, {"is_dsr": True, "is_external": True}, {"is_nested": True},
                                    {"is_external": True, "traffic_policy_local": True}])
 def test_oracle_unsupported_service_configs(extra):
     with pytest.raises(ValueError):
         osvc.FeatureService().install_service_flows(dict(GOLD["service_flows"][0]["config"], **extra))
 
 
-@pytest.mark.parametrize("name,seed", [("C1", 61), ("C3s", 62)])
+@pytest.mark.parametrize("name,seed", [("C1", 61), ("C3s", 62), ("C1np", 63)])
 def test_oracle_service_compiler_equals_product(name, seed):
     """The oracle's Service flows and groups for a whole Service workload (remote, local, Local-policy
     and Endpoint-less Services, shared Endpoints, an external Service) equal the product's dumps --
@@ -205,7 +211,7 @@ def test_oracle_service_compiler_equals_product(name, seed):
     s = osvc.FeatureService()
     osvc.install_services(s, wl)
     prod = sorted(f for f in c.dump_flows() if any(t in f for t in ("table=ServiceLB", "table=EndpointDNAT",
-                                                                    "table=SNATMark")))
+                                                                    "table=SNATMark", "table=NodePortMark")))
     assert prod == s.dump_flows() and len(prod) > 10
     assert c.dump_groups() == s.dump_groups()
     for cfg in wl.services[::3]:
@@ -215,6 +221,67 @@ def test_oracle_service_compiler_equals_product(name, seed):
     c.install_service_group(gid, eps[:1])
     s.install_service_group(gid, eps[:1])
     prod = sorted(f for f in c.dump_flows() if any(t in f for t in ("table=ServiceLB", "table=EndpointDNAT",
-                                                                    "table=SNATMark")))
+                                                                    "table=SNATMark", "table=NodePortMark")))
     assert prod == s.dump_flows()
     assert c.dump_groups() == s.dump_groups()
+
+
+def _nodeport_golden():
+    """client_test.go "Service NodePort,SessionAffinity": its priority-200 ServiceLB flow, the match
+    this path implements (ToNodePortAddressRegMark + protocol + port, no Service IP). Session
+    affinity itself is not modelled, so the EpToLearn load (0x30000) reads EpSelected (0x20000)."""
+    case = next(c for c in GOLD["service_flows_nodeport_affinity"])
+    line = case["expected"][0]
+    assert "reg4=0x90000/0xf0000,tp_dst=80" in line and "nw_dst" not in line
+    return case["config"], line.replace("set_field:0x30000/0x70000->reg4", "set_field:0x20000/0x70000->reg4")
+
+
+def test_nodeport_service_flow_golden():
+    cfg, want = _nodeport_golden()
+    cfg = dict(cfg, affinity_timeout=0)
+    c = gpc.Classifier()
+    c.install_service_flows(cfg)
+    assert c.dump_flows() == [want]
+    s = osvc.FeatureService()
+    s.install_service_flows(cfg)
+    assert s.dump_flows() == [want]
+
+
+def test_nodeport_mark_flows():
+    """nodePortMarkFlows (pipeline.go:2282-2314): one flow per non-loopback NodePort address plus the
+    virtual NodePort DNAT IP; replaced as a set; [] removes them. Product == oracle restatement."""
+    c, s = gpc.Classifier(), osvc.FeatureService()
+    for ips in (["192.168.77.100", "127.0.0.1", "10.0.2.15"], ["192.168.77.101"], []):
+        c.set_node_port_addresses(ips)
+        s.set_node_port_addresses(ips)
+        got = sorted(f for f in c.dump_flows() if "table=NodePortMark" in f)
+        assert got == s.dump_flows()
+        assert len(got) == (len([i for i in ips if not i.startswith("127.")]) + 1 if ips else 0)
+        assert all("actions=set_field:0x80000/0x80000->reg4" in f for f in got)
+    assert not any("nw_dst=127.0.0.1" in f for f in s.dump_flows())
+
+
+def test_nodeport_packets():
+    """A packet to a NodePort address (or the virtual NodePort DNAT IP) on a NodePort Service's port
+    is load-balanced; the same port on another address, or with NodePort addresses unset, is not."""
+    import ipaddress
+    cfg, _ = _nodeport_golden()
+    cfg = dict(cfg, affinity_timeout=0)
+    eps = [{"ip": "10.10.0.100", "port": 8080, "is_local": False, "node_name": "n1"}]
+    base = {"src": int(ipaddress.ip_address("10.10.0.5")), "proto": 17, "sport": 40000, "dport": 80, "out_port": 0}
+    for addrs in (["192.168.77.100"], []):
+        c = gpc.Classifier()
+        c.initialize()
+        c.set_node_port_addresses(addrs)
+        c.install_service_group(cfg["cluster_group_id"], eps)
+        c.install_service_flows(cfg)
+        emu.commit_host(c)
+        dsts = ["192.168.77.100", "169.254.0.252", "192.168.77.200"]
+        cols = {k: np.array([v] * len(dsts)) for k, v in base.items()}
+        cols["dst"] = np.array([int(ipaddress.ip_address(d)) for d in dsts], np.uint32)
+        cols = {k: v.astype({"src": np.uint32, "dst": np.uint32, "proto": np.uint8, "sport": np.uint16,
+                             "dport": np.uint16, "out_port": np.uint32}[k]) for k, v in cols.items()}
+        lb = np.zeros(len(dsts), dtype=gpc.LB_DTYPE)
+        emu.classify(c, cols, lb=lb)
+        hit = (lb["flags"] & gpc.LB_HIT) != 0
+        assert list(hit) == ([True, True, False] if addrs else [False, False, False]), (addrs, lb)
