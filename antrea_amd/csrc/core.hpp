@@ -1991,14 +1991,19 @@ GPC_HD TablePart eval_ext(const View& v, uint32_t table, const Pkt& p, uint32_t 
     if (!((hits >> i) & 1u)) continue;
     const uint32_t val = p.ax[a], h = ext_kind_hash(v, table, b, p);
     const uint32_t meta = table | (a << 3) | (b < 16u ? 0u : kExtComposite);
+    // both levels' bucket ranges are loaded before either is walked (two loads in flight, not two
+    // dependent rounds); an empty level reads the range [0, 0)
+    uint32_t rng[2][2] = {{0u, 0u}, {0u, 0u}};
+#pragma unroll
+    for (uint32_t lv = 0; lv < 2; lv++)
+      if (lv ? eh->b_n : eh->n) {
+        const uint32_t* bk = pool + (lv ? eh->b_bkt_off : eh->bkt_off) + (h & ((1u << (lv ? eh->b_bkt_log2 : eh->bkt_log2)) - 1u));
+        GPC_TOUCH(bk, 8);
+        load_pair(bk, &rng[lv][0], &rng[lv][1]);
+      }
     for (uint32_t lv = 0; lv < 2; lv++) {  // D, then B
-    if (!(lv ? eh->b_n : eh->n)) continue;
-    const uint32_t* bk = pool + (lv ? eh->b_bkt_off : eh->bkt_off) + (h & ((1u << (lv ? eh->b_bkt_log2 : eh->bkt_log2)) - 1u));
     const uint32_t eo = lv ? eh->b_ent_off : eh->ent_off;
-    uint32_t e, end;
-    GPC_TOUCH(bk, 8);
-    load_pair(bk, &e, &end);
-    for (; e < end; e++) {
+    for (uint32_t e = rng[lv][0], end = rng[lv][1]; e < end; e++) {
       const uint32_t* en = pool + eo + e * kExtEntWords;
       GPC_TOUCH(en, 32);
 #if defined(__HIPCC__)
