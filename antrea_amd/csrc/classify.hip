@@ -24,12 +24,16 @@ __device__ unsigned long long gpc_stamp_acc[32];  // [16 * (kStage == 2) + regio
 #ifndef GPC_WAVES_PER_EU
 #define GPC_WAVES_PER_EU 6
 #endif
-// Delta-epoch kernels (extension and journal modes) run at 5 waves per SIMD: 96 VGPRs hold them
-// without spills (at 6 they spilled 9-31 VGPRs, 16-52 B of scratch per lane), and C5 measured
-// 6.00 vs 6.10 ms per step (profiles/r05rs_occupancy_parking_ab.txt). The base kernels stay at 6:
-// C3 5.09 ms at 6 waves against 5.54 at 5.
+// Journal-mode kernels run at 5 waves per SIMD: 96 VGPRs hold them without spills (at 6 they
+// spill 13-44 VGPRs, 36-52 B of scratch per lane), and C5 measured 6.00 vs 6.10 ms per step
+// (profiles/r05rs_occupancy_parking_ab.txt). The base kernels stay at 6 (C3 5.09 ms at 6 waves
+// against 5.54 at 5), and since round 6 the extension-mode ones too: the two-level extension probe
+// with its bucket ranges loaded up front fits 80 VGPRs without spills (tools/kres.sh).
 #ifndef GPC_DELTA_WAVES_PER_EU
 #define GPC_DELTA_WAVES_PER_EU 5
+#endif
+#ifndef GPC_EXT_WAVES_PER_EU
+#define GPC_EXT_WAVES_PER_EU 6
 #endif
 #ifndef GPC_BLOCK
 #define GPC_BLOCK 64
@@ -455,7 +459,7 @@ __device__ __forceinline__ void classify_one(const EpochArgs& ep, const gpc_pkt_
 
 // kDelta: the epoch mode (core.hpp kModeBase / kModeExt / kModeJournal).
 template <int kDelta, bool kSvc, int kStage, bool kSort = false>
-__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta != kModeBase ? GPC_DELTA_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
+__global__ __launch_bounds__(block_threads<kSort>()) __attribute__((amdgpu_waves_per_eu(kDelta == kModeJournal ? GPC_DELTA_WAVES_PER_EU : kDelta == kModeExt ? GPC_EXT_WAVES_PER_EU : GPC_WAVES_PER_EU))) void classify_kernel(
     EpochArgs ep, gpc_pkt_soa pk, uint64_t n, uint4* __restrict__ out, uint4* __restrict__ lb_out,
     unsigned long long* __restrict__ counters, int count, const uint32_t* __restrict__ orig, uint2* __restrict__ mid,
     uint32_t xcd_order, uint2* __restrict__ gout, uint4* __restrict__ park) {
