@@ -1959,6 +1959,14 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     }
     std::memcpy(ctx->stage, jn.pool.data() + jn.uploaded, tail_bytes);
   }
+  // the first delta commit after a full build would otherwise allocate the pinned staging buffer
+  // (hipHostMalloc of 16 MB: ~0.3 s on the box, which every op queued behind it waited for: C5
+  // op-latency p99 302 ms); allocated with the full build instead, outside the churn
+  if (!tail && full && !ctx->stage && !std::getenv("GPC_LAZY_STAGE")) {
+    const size_t cap = size_t(16) << 20;
+    if (!hip_ok(hipHostMalloc(&ctx->stage, cap, hipHostMallocPortable))) ctx->stage_bytes = cap;
+    else ctx->stage = nullptr;
+  }
   const uint32_t jhdr = jn.active() ? jn.hdr_off : 0;
   // the IPv6 journal tail (delta epochs), staged the same way; a new pool on every slot when the
   // IPv6 base is new or its journal starts (lockstep: every slot has the same IPv6 base)
