@@ -391,7 +391,7 @@ def _churn_loop(ops, rate, max_batch, stop, rec, interval=0.0):
         ops.clf.commit()
         done = time.perf_counter()
         due_t = t0 + (first + np.arange(due)) / rate
-        rec.append((due, done - tc, done - due_t))
+        rec.append((due, done - tc, done - due_t, now - t0, tc - now))
 
 
 def _churn_converge(ops, wl, dev, world):
@@ -935,6 +935,15 @@ def main(argv=None):
     starts = [dp.event() for _ in range(args.steps)]
     ends = [dp.event() for _ in range(args.steps)]
     lat, th = [], None
+    # The harness's own heap (the workload's 100 k rule dicts, C5's op log growing by 10 k dicts a
+    # second) makes CPython's cyclic collector pause every thread for up to ~0.6 s while it holds
+    # the GIL: the launch loop stalled (C5 step max 564 ms, op p99 680 ms). Nothing of the library
+    # is collected; the harness freezes its heap (before the control thread starts: the collection itself
+    # holds the GIL for ~0.3 s) and collects again after the timed region.
+    import gc
+    gc.collect()
+    gc.freeze()
+    gc.disable()
     if churn:
         import threading
         import numpy as np
@@ -963,14 +972,6 @@ def main(argv=None):
             time.sleep(0.01)
         lat.clear()
     _log("timed region: %d steps of %d packets" % (args.steps, n))
-    # The harness's own heap (the workload's 100 k rule dicts, C5's op log growing by 10 k dicts a
-    # second) makes CPython's cyclic collector pause every thread for up to ~0.6 s while it holds
-    # the GIL: the launch loop stalled (C5 step max 564 ms, op p99 680 ms). Nothing of the library
-    # is collected; the harness freezes its heap and collects again after the timed region.
-    import gc
-    gc.collect()
-    gc.freeze()
-    gc.disable()
     # HIP events around each kernel of the timed calls (gpc_launch_times; the library keeps at most
     # 4096 calls: a longer run, e.g. C5 over 30 s, is timed per kernel over its first 4096 steps)
     dp.set_launch_timing(min(args.steps, 4096))
@@ -1005,6 +1006,12 @@ def main(argv=None):
                   "op_latency_ms": {"p50": pct(op_ms, 50), "p99": pct(op_ms, 99),
                                     "max": round(float(op_ms.max()), 3) if len(op_ms) else None},
                   "commit_ms": {"p50": pct(commit_ms, 50), "p99": pct(commit_ms, 99)},
+                  # the commit whose ops waited longest: when it ran (seconds into the control loop),
+                  # how long applying its ops and the commit took
+                  "worst_commit": (lambda r: {"at_s": round(r[3], 3), "ops": int(r[0]), "apply_ms": round(r[4] * 1e3, 2),
+                                              "commit_ms": round(r[1] * 1e3, 2),
+                                              "op_latency_ms": round(float(r[2].max()) * 1e3, 2)})(
+                      max(rec, key=lambda r: float(r[2].max()))) if rec else None,
                   "overlay_rules_end": st["n_overlay_rules"], "tombstones_end": st["n_tombstones"],
                   "ext_rules_end": st["n_ext_rules"], "ext_values_end": st["n_ext_values"],
                   "full_builds": st["n_full_builds"] - st0["n_full_builds"],
