@@ -988,7 +988,6 @@ def main(argv=None):
         dist.barrier()
     dp.sync()
     elapsed = time.perf_counter() - t_start
-    gc.enable()
     update = None
     if churn:
         stop.set()
@@ -1023,6 +1022,7 @@ def main(argv=None):
             update["candidate_adds"] = len(cands)
         if world > 1:
             update["ranks"] = _churn_converge(churn_ops, wl, dev, world)
+    gc.enable()  # (after the control thread stopped: the op log's first collection is long)
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     launches = dp.launch_times()
     dp.set_launch_timing(0)
