@@ -161,6 +161,12 @@ constexpr size_t kDeltaMinRules = 16384;
 constexpr size_t kDeltaFraction = 4;
 constexpr size_t kPendingCapFactor = 2;  // journal allowance while a background compaction is pending
 constexpr size_t kPoolWords = size_t(256) << 20;  // 1 GiB journal pool per base (HBM is 288 GB)
+// Pool collection bar: journal entries are chained by 24-bit entry indexes (32-B entries: the first
+// 2^27 words of the pool), so the collection runs well before that; 3/8 of the pool (96 M words)
+// rather than 1/4 makes C5 mixed collect every ~7 s instead of ~5 s (each collection is a 110-180 ms
+// commit the ops due meanwhile wait for).
+constexpr size_t kPoolGcWords = kPoolWords * 3 / 8;
+static_assert(kPoolGcWords < (size_t(1) << 27), "collect before the 24-bit journal entry indexes run out");
 constexpr size_t kMinUploadBytes = size_t(1) << 20;
 constexpr size_t kExtCompactValues = size_t(1) << 16;  // live point-extension values that ask for a compaction
 constexpr size_t kGcDeadMin = 2048;  // dead journal versions that ask for a pool collection (and 2x the live rules)
@@ -1776,7 +1782,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
     // Cost ~ the rules touched since the base (C5 mixed: ~8 k); the alternative, a compaction, is
     // a whole image build (seconds) plus a base upload.
     if (!full && !installed && ctx->journal.active() && !std::getenv("GPC_NO_POOL_GC") &&
-        (ctx->journal.pool.size() > kPoolWords / 4 ||
+        (ctx->journal.pool.size() > kPoolGcWords ||
          ctx->journal.n_dead_versions() > std::max<size_t>(env_u32("GPC_GC_DEAD_MIN", kGcDeadMin, 1, 1u << 30),
                                                            2 * size_t(ctx->journal.n_live)))) {
       std::string err;
@@ -1822,7 +1828,7 @@ static int commit_impl(gpc_ctx* ctx, bool force_full) {
   const bool hold_ext = !std::getenv("GPC_COMPACT_FOLD_EXT") && ctx->journal.n_ext_values() <= kExtCompactValues;
   if (!full && ca >= 0 && !ctx->comp_pending &&
       (ctx->journal.n_live + (hold_ext ? 0u : ctx->journal.n_ext_rules()) > soft ||
-       ctx->journal.n_ext_values() > kExtCompactValues || ctx->journal.pool.size() > kPoolWords / 4)) {
+       ctx->journal.n_ext_values() > kExtCompactValues || ctx->journal.pool.size() > kPoolGcWords)) {
     {
       std::lock_guard<std::mutex> c(ctx->comp.mu);
       if (ctx->comp.enabled && !ctx->comp.busy && !ctx->comp.ready) {

@@ -2900,6 +2900,10 @@ int Journal::apply(const FeatureNP& np, SlotMap& slots, const std::set<uint32_t>
           if (!keyed) {
             const uint32_t e[kJEntWords] = {jt.always[k], 0u, (orid << kJOridShift), off, pf[0] & 0xffu, pf[1], pf[2], pf[3]};
             const uint32_t eo = append(e, kJEntWords, kJEntWords);
+            if (eo / kJEntWords >= (1u << 24)) {
+              *err = "journal pool exceeds 24-bit entry offsets";
+              return -GPC_ENOMEM;
+            }
             jt.always[k] = (eo / kJEntWords) | (std::min(255u, (jt.always[k] >> 24) + 1u) << 24);
             continue;
           }
