@@ -18,6 +18,7 @@
 #include <random>
 #include <queue>
 #include <set>
+#include <thread>
 #include <tuple>
 
 namespace gpc {
@@ -2446,8 +2447,15 @@ int Journal::rebuild(const FeatureNP& np, SlotMap& slots, std::string* err) {
   j.touched_hard_ = touched_hard_;
   std::set<uint32_t> live;
   for (auto& kv : live_) live.insert(kv.first);
+  const auto t0 = std::chrono::steady_clock::now();
   const int rc = j.apply(np, slots, live, touched_hard_, err);
   if (rc) return rc;
+  if (std::getenv("GPC_COMPACT_DEBUG"))
+    std::fprintf(stderr, "pool collection: apply of %zu live rules + extension index %.1f ms\n", live.size(),
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  // the old host mirror (hundreds of MB) is released off the control thread: unmapping it took
+  // tens of ms of the collection's commit
+  std::thread([old = std::move(pool)]() mutable { std::vector<uint32_t>().swap(old); }).detach();
   *this = std::move(j);
   return GPC_OK;
 }
@@ -2492,6 +2500,16 @@ static size_t ext_entries_of(const R& e) {
 // instead of 1.3 MB re-emitting everything. Returns the ExtHdr offset (0: no extensions).
 constexpr size_t kExtDeltaMin = 4096, kExtDeltaFrac = 8;
 uint32_t Journal::emit_ext() {
+  const auto te0 = std::chrono::steady_clock::now();
+  struct Report {
+    std::chrono::steady_clock::time_point t;
+    const Journal* j;
+    ~Report() {
+      if (std::getenv("GPC_EXT_TIMING"))
+        std::fprintf(stderr, "emit_ext: %.2f ms (%zu entries)\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count(), j->ext_entries_);
+    }
+  } report{te0, this};
   for (uint32_t c : ext_dirty_) {  // the changed rules leave B (their entries go to D, if any)
     auto it = extb_ents_.find(c);
     if (it != extb_ents_.end()) {
